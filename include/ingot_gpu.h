@@ -1,0 +1,292 @@
+/*
+ * ingot_gpu.h — C ABI of the MI355X (gfx950) batched L2/L3/L4 header extractor.
+ *
+ * This is the drop-in boundary for ingot's per-packet parse path.  In ingot the
+ * path sits behind Rust traits, not an FFI:
+ *
+ *   HeaderParse::parse / parse_choice      ingot-types/src/lib.rs:137-147
+ *   Success<T, B> = (T, Option<Denom>, B)   ingot-types/src/lib.rs:208
+ *   <Chain>::parse_slice(from)              ingot-macros/src/parse.rs:496-509
+ *   PacketParseError { label, inner }       ingot-types/src/error.rs:119-171
+ *   ParseError (8 kinds)                    ingot-types/src/error.rs:21-44
+ *
+ * and it is called once per packet by the caller's loop
+ * (ingot-examples/benches/packet.rs:136-172).  The entry points below replace
+ * that loop + the parse bodies for a whole batch at once: the caller owns a
+ * packet arena in device memory (borrow semantics: nothing is copied, nothing
+ * is allocated per call) and gets one fixed-size record per packet that says
+ * what `parse_slice` would have returned — Ok with the layer views as
+ * (offset, kind) pairs and the remainder offset, or the PacketParseError
+ * (failing layer index == label, ParseError discriminant).
+ *
+ * Plain C, plain pointers and sizes; `stream` is a hipStream_t passed as void*
+ * (NULL = the null stream).  Every call is asynchronous on `stream`.  API
+ * errors are negative ints (see ingot_gpu_strerror); per-packet parse errors
+ * live in the records and are never API errors — like ingot, malformed input
+ * never fails the call.
+ *
+ * Threading: a context is bound to one device; calls on distinct contexts or
+ * distinct streams may run concurrently.  The context holds no per-call state.
+ */
+#ifndef INGOT_GPU_H
+#define INGOT_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define INGOT_GPU_ABI_VERSION 1
+
+/* ---------------------------------------------------------------------------
+ * Per-packet status: 0 = Ok, else 1 + the ParseError discriminant in the
+ * declaration order of ingot-types/src/error.rs:22-44.  On the single-slice
+ * chains below only UNWANTED, TOO_SMALL and CANNOT_ACCEPT are reachable
+ * (SURVEY §8a A17); the others are listed so the numbering is ingot's.
+ * ------------------------------------------------------------------------- */
+enum ingot_status {
+    INGOT_OK = 0,
+    INGOT_ERR_UNWANTED = 1,
+    INGOT_ERR_NEEDS_HINT = 2,
+    INGOT_ERR_TOO_SMALL = 3,
+    INGOT_ERR_STRADDLED_HEADER = 4,
+    INGOT_ERR_NO_REMAINING_CHUNKS = 5,
+    INGOT_ERR_CANNOT_ACCEPT = 6,
+    INGOT_ERR_REJECT = 7,
+    INGOT_ERR_ILLEGAL_VALUE = 8
+};
+
+/* ---------------------------------------------------------------------------
+ * Parse chains (the `#[derive(Parse)]` structs the batch is parsed as).
+ *
+ * UDP_PARSER   ingot-examples/src/packets.rs:18-24
+ *              eth: Ethernet, l3: L3 (v4|v6), l4: from L4 (tcp|udp) -> Udp
+ *              layer labels "eth", "l3", "l4"
+ * GENERIC_ULP  ingot-examples/src/packets.rs:54-60  (control = exit_on_arp)
+ *              inner_eth: Ethernet, inner_l3: Option<L3>, inner_ulp: Option<Ulp>
+ *              layer labels "inner_eth", "inner_l3", "inner_ulp"
+ * VLAN_ULP     build-defined (ingot declares VlanBody, ethernet.rs:57-65, but
+ *              no chain uses it): eth, 0..2 x VlanBody while the ethertype is
+ *              0x8100/0x9100, L3, Ulp; no control.  Labels "eth", "vlan",
+ *              "l3", "l4".  Parity for this chain is unpinned by the reference.
+ * ------------------------------------------------------------------------- */
+enum ingot_chain {
+    INGOT_CHAIN_UDP_PARSER = 0,
+    INGOT_CHAIN_GENERIC_ULP = 1,
+    INGOT_CHAIN_VLAN_ULP = 2,
+    INGOT_CHAIN_COUNT = 3
+};
+
+enum ingot_l3_kind { INGOT_L3_NONE = 0, INGOT_L3_IPV4 = 1, INGOT_L3_IPV6 = 2 };
+enum ingot_l4_kind {
+    INGOT_L4_NONE = 0,
+    INGOT_L4_TCP = 1,
+    INGOT_L4_UDP = 2,
+    INGOT_L4_ICMPV4 = 3,
+    INGOT_L4_ICMPV6 = 4
+};
+
+/* rec.flags */
+#define INGOT_REC_ACCEPTED 0x01u /* a parse control accepted early (parse.rs:221-254) */
+
+/* ---------------------------------------------------------------------------
+ * ingot_rec — the 16-byte per-packet result.
+ *
+ * Fields are filled as the chain walks, so an error record still shows how
+ * far the walk got:
+ *   status/err_layer  Ok, or (1+ParseError, index of the failing layer label)
+ *                     err_layer = 0xff when Ok.
+ *   l3_kind/l4_kind   set when the L3 / L4 choice selects a variant (before
+ *                     that variant is parsed).
+ *   l3_off/l4_off     frame offset where the L3 / L4 layer starts (0 = never
+ *                     reached).
+ *   payload_off       offset of the remainder: bytes consumed by the headers
+ *                     that parsed successfully (== remainder start on Ok).
+ *   ethertype         the Ethertype hint handed to the L3 choice (after VLAN
+ *                     tags); 0 if Ethernet did not parse.
+ *   l4_proto          the IpProtocol hint handed to the L4 choice (IPv6: the
+ *                     last extension header's next_header, ip.rs:180-181,
+ *                     util.rs:189-228).
+ *   n_vlan/n_v6ext    VLAN tags / IPv6 extension headers fully parsed.
+ * ------------------------------------------------------------------------- */
+typedef struct ingot_rec {
+    uint8_t status;
+    uint8_t err_layer;
+    uint8_t l3_kind;
+    uint8_t l4_kind;
+    uint8_t n_vlan;
+    uint8_t n_v6ext;
+    uint8_t l4_proto;
+    uint8_t flags;
+    uint16_t l3_off;
+    uint16_t l4_off;
+    uint16_t payload_off;
+    uint16_t ethertype;
+} ingot_rec;
+
+/* One IPv6 extension header as ingot's getters see it
+ * (IpV6ExtFragment ip.rs:190-200, IpV6Ext6564 ip.rs:202-211). */
+#define INGOT_EH_FRAGMENT 1
+#define INGOT_EH_RFC6564 2
+#define INGOT_MAX_EH_FIELDS 4 /* first 4 EHs are materialised; count is exact */
+
+typedef struct ingot_v6eh {
+    uint32_t ident;         /* fragment: ident (u32be) */
+    uint16_t frag_offset;   /* fragment: fragment_offset (u13be) */
+    uint16_t off;           /* frame offset of this EH */
+    uint8_t kind;           /* INGOT_EH_FRAGMENT / INGOT_EH_RFC6564 */
+    uint8_t next_header;    /* both */
+    uint8_t ext_len;        /* 6564: ext_len; fragment: reserved */
+    uint8_t frag_res_more;  /* fragment: res << 1 | more_frags */
+} ingot_v6eh;
+
+/* ---------------------------------------------------------------------------
+ * ingot_fields — every getter of every header on the chain, materialised
+ * (parity mode).  Values are exactly what ingot's generated XRef getters
+ * return (bitfield.rs:40-315 BE bit order; NetworkRepr conversions applied:
+ * `*_ecn` is Ecn::from_network (3 -> Capable0 == 1, ip.rs:111-119), flags are
+ * bitflags from_bits_truncate (identity on the stored bits)).  Variable-length
+ * fields (options, EH data) are given as (offset, length) into the frame.
+ * Headers that were not reached are all-zero.
+ * ------------------------------------------------------------------------- */
+typedef struct ingot_fields {
+    ingot_rec rec;                      /*   0 */
+    /* 32-bit */
+    uint32_t v6_flow_label;             /*  16 */
+    uint32_t tcp_sequence;              /*  20 */
+    uint32_t tcp_acknowledgement;       /*  24 */
+    /* 16-bit */
+    uint16_t eth_ethertype;             /*  28 */
+    uint16_t vlan_vid[2];               /*  30 */
+    uint16_t vlan_ethertype[2];         /*  34 */
+    uint16_t v4_total_len;              /*  38 */
+    uint16_t v4_identification;         /*  40 */
+    uint16_t v4_fragment_offset;        /*  42 */
+    uint16_t v4_checksum;               /*  44 */
+    uint16_t v4_options_off;            /*  46 */
+    uint16_t v4_options_len;            /*  48 */
+    uint16_t v6_payload_len;            /*  50 */
+    uint16_t v6_ext_off;                /*  52  RepeatedView span start */
+    uint16_t v6_ext_len;                /*  54  RepeatedView span bytes */
+    uint16_t l4_source;                 /*  56  tcp/udp source */
+    uint16_t l4_destination;            /*  58  tcp/udp destination */
+    uint16_t tcp_window_size;           /*  60 */
+    uint16_t tcp_checksum;              /*  62 */
+    uint16_t tcp_urgent_ptr;            /*  64 */
+    uint16_t tcp_options_off;           /*  66 */
+    uint16_t tcp_options_len;           /*  68 */
+    uint16_t udp_length;                /*  70 */
+    uint16_t udp_checksum;              /*  72 */
+    uint16_t icmp_checksum;             /*  74 */
+    /* 8-bit */
+    uint8_t eth_destination[6];         /*  76 */
+    uint8_t eth_source[6];              /*  82 */
+    uint8_t vlan_priority[2];           /*  88 */
+    uint8_t vlan_dei[2];                /*  90 */
+    uint8_t v4_version;                 /*  92 */
+    uint8_t v4_ihl;                     /*  93 */
+    uint8_t v4_dscp;                    /*  94 */
+    uint8_t v4_ecn_raw;                 /*  95 */
+    uint8_t v4_ecn;                     /*  96 */
+    uint8_t v4_flags;                   /*  97 */
+    uint8_t v4_hop_limit;               /*  98 */
+    uint8_t v4_protocol;                /*  99 */
+    uint8_t v4_source[4];               /* 100 */
+    uint8_t v4_destination[4];          /* 104 */
+    uint8_t v6_version;                 /* 108 */
+    uint8_t v6_dscp;                    /* 109 */
+    uint8_t v6_ecn_raw;                 /* 110 */
+    uint8_t v6_ecn;                     /* 111 */
+    uint8_t v6_next_header;             /* 112 */
+    uint8_t v6_hop_limit;               /* 113 */
+    uint8_t v6_source[16];              /* 114 */
+    uint8_t v6_destination[16];         /* 130 */
+    uint8_t tcp_data_offset;            /* 146 */
+    uint8_t tcp_reserved;               /* 147 */
+    uint8_t tcp_flags;                  /* 148 */
+    uint8_t icmp_ty;                    /* 149 */
+    uint8_t icmp_code;                  /* 150 */
+    uint8_t icmp_rest_of_hdr[4];        /* 151 */
+    uint8_t _pad0;                      /* 155 */
+    ingot_v6eh v6_eh[INGOT_MAX_EH_FIELDS]; /* 156 (4 x 12) */
+    uint8_t _pad1[52];                  /* 204 -> 256 */
+} ingot_fields;
+
+#ifdef __cplusplus
+static_assert(sizeof(ingot_rec) == 16, "ingot_rec is 16 bytes");
+static_assert(sizeof(ingot_v6eh) == 12, "ingot_v6eh is 12 bytes");
+static_assert(sizeof(ingot_fields) == 256, "ingot_fields is 256 bytes");
+#endif
+
+/* API return codes (negative). */
+#define INGOT_GPU_SUCCESS 0
+#define INGOT_GPU_EINVAL (-1)   /* bad argument (null pointer, bad chain ...) */
+#define INGOT_GPU_EHIP (-2)     /* a HIP runtime call failed */
+#define INGOT_GPU_ENOMEM (-3)   /* context allocation failed */
+#define INGOT_GPU_ENODEV (-4)   /* no such device / no gfx950 code object */
+#define INGOT_GPU_ERANGE (-5)   /* size outside what the ABI supports */
+
+typedef struct ingot_gpu_ctx ingot_gpu_ctx;
+
+/* Library / ABI identification. */
+int ingot_gpu_abi_version(void);
+const char* ingot_gpu_build_info(void);
+
+/* Context: binds a device.  Cheap; owns no per-call buffers. */
+int ingot_gpu_ctx_create(int device, ingot_gpu_ctx** out);
+void ingot_gpu_ctx_destroy(ingot_gpu_ctx* ctx);
+int ingot_gpu_ctx_device(const ingot_gpu_ctx* ctx);
+
+/*
+ * Batched `<Chain>::parse_slice` over frames in a device arena.
+ *
+ *   d_arena   device pointer to the packet bytes
+ *   d_off     per-packet byte offset into d_arena (u64)
+ *   d_len     per-packet length in bytes (u16)
+ *   n         number of packets
+ *   chain     enum ingot_chain
+ *   d_out     n records (device memory, 16 B each)
+ *
+ * Replaces the caller's per-packet loop over `parse_slice`
+ * (ingot-examples/benches/packet.rs:136-172) for the whole batch.
+ */
+int ingot_gpu_parse(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
+                    const uint64_t* d_off, const uint16_t* d_len, uint64_t n,
+                    int chain, ingot_rec* d_out, void* stream);
+
+/*
+ * Same, for fixed-stride arenas (ring buffers with one frame per slot):
+ * frame i starts at d_arena + i*stride; its length is d_len[i], or `stride`
+ * when d_len is NULL.  stride must be a multiple of 16 and <= 65535 and
+ * d_arena 16-byte aligned.  No descriptor bytes are read when d_len is NULL.
+ */
+int ingot_gpu_parse_strided(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
+                            uint32_t stride, const uint16_t* d_len, uint64_t n,
+                            int chain, ingot_rec* d_out, void* stream);
+
+/*
+ * Parity mode: every getter of every parsed header (ingot_fields, 256 B per
+ * packet).  Same inputs as ingot_gpu_parse; d_off may be NULL to select the
+ * strided layout with `stride` (ignored otherwise).
+ */
+int ingot_gpu_fields(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
+                     const uint64_t* d_off, const uint16_t* d_len,
+                     uint32_t stride, uint64_t n, int chain,
+                     ingot_fields* d_out, void* stream);
+
+/* Error strings. */
+const char* ingot_gpu_strerror(int api_code);
+/* ParseError name as ingot prints it (error.rs:49-60): "Unwanted", ... ;
+ * "Ok" for 0, NULL if out of range. */
+const char* ingot_parse_error_name(int status);
+/* Layer label of a chain (the PacketParseError label, parse.rs:36-50). */
+const char* ingot_chain_layer_label(int chain, int layer);
+int ingot_chain_layer_count(int chain);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* INGOT_GPU_H */

@@ -1,0 +1,488 @@
+"""ingot_amd — MI355X-native batched L2/L3/L4 header extraction with ingot's
+parse semantics.
+
+Host-side mirror of the reference's parse interface above the C ABI
+(include/ingot_gpu.h).  The batch API (`Context.parse*`) is the hot path; the
+per-packet classes `UdpParser`, `GenericUlp`, `VlanUlp` mirror ingot's
+`#[derive(Parse)]` chains (`Chain::parse(bytes) -> (headers, None, remainder)`
+raising `PacketParseError{label, inner}`) so tests read like the reference's
+own (ingot-examples/src/tests.rs).  Everything runs through the gfx950
+library; nothing here parses bytes on the CPU.
+
+Device memory, streams and torch.distributed come from PyTorch (plumbing).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional
+
+from . import _lib
+from .abi import (  # noqa: F401  (re-exports)
+    ABI_VERSION,
+    CHAIN_LABELS,
+    FIELDS_BYTES,
+    FIELDS_DTYPE,
+    GEN_SEED,
+    MAX_EH_FIELDS,
+    REC_ACCEPTED,
+    REC_BYTES,
+    REC_DTYPE,
+    STATUS_OK,
+    Chain,
+    GenProfile,
+    IngotFields,
+    IngotRec,
+    L3Kind,
+    L4Kind,
+    ParseError,
+)
+
+__all__ = [
+    "Chain", "Context", "GenProfile", "PacketParseError", "ParseError", "UdpParser",
+    "GenericUlp", "VlanUlp", "gen_frames", "gen_lengths", "records_to_numpy",
+    "fields_to_numpy", "load_library",
+]
+
+
+def load_library() -> ctypes.CDLL:
+    return _lib.load()
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def _ptr(t) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _stream(stream) -> Optional[int]:
+    torch = _torch()
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+
+
+class PacketParseError(Exception):
+    """ingot_types::PacketParseError (ingot-types/src/error.rs:119-171):
+    the failing layer's label plus the ParseError."""
+
+    def __init__(self, label: str, inner: ParseError):
+        super().__init__(f"{label}: {inner.name}")
+        self.label = label
+        self.inner = inner
+
+    def header(self) -> str:
+        return self.label
+
+    def error(self) -> ParseError:
+        return self.inner
+
+
+class Context:
+    """One device.  Mirrors `ingot_gpu_ctx`; all calls are async on `stream`
+    (default: torch's current stream on that device)."""
+
+    def __init__(self, device: int = 0):
+        self._lib = _lib.load()
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.ingot_gpu_ctx_create(int(device), ctypes.byref(h)),
+                   "ingot_gpu_ctx_create")
+        self._h = h
+        self.device = int(device)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.ingot_gpu_ctx_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def _check_dev(self, *tensors) -> None:
+        for t in tensors:
+            if t is not None and (not t.is_cuda or t.device.index != self.device):
+                raise ValueError("tensors must live on the context's device")
+
+    def parse(self, arena, off, lens, chain: Chain, out=None, stream=None):
+        """Batched `<chain>::parse_slice` over frames (off[i], lens[i]) of arena.
+
+        arena: uint8 cuda tensor; off: int64 (u64 offsets); lens: uint16.
+        Returns an (n, 16) uint8 tensor of ingot_rec records.
+        """
+        torch = _torch()
+        n = off.numel()
+        if lens.numel() != n:
+            raise ValueError("off and lens must have the same length")
+        if out is None:
+            out = torch.empty((n, REC_BYTES), dtype=torch.uint8, device=arena.device)
+        self._check_dev(arena, off, lens, out)
+        _lib.check(self._lib.ingot_gpu_parse(self._h, _ptr(arena), _ptr(off), _ptr(lens), n,
+                                             int(chain), _ptr(out), _stream(stream)),
+                   "ingot_gpu_parse")
+        return out
+
+    def parse_strided(self, arena, stride: int, n: int, chain: Chain, lens=None, out=None,
+                      stream=None):
+        torch = _torch()
+        if out is None:
+            out = torch.empty((n, REC_BYTES), dtype=torch.uint8, device=arena.device)
+        self._check_dev(arena, lens, out)
+        _lib.check(self._lib.ingot_gpu_parse_strided(self._h, _ptr(arena), int(stride),
+                                                     _ptr(lens), n, int(chain), _ptr(out),
+                                                     _stream(stream)),
+                   "ingot_gpu_parse_strided")
+        return out
+
+    def fields(self, arena, off, lens, chain: Chain, stride: int = 0, n: Optional[int] = None,
+               out=None, stream=None):
+        """Parity mode: (n, 256) uint8 tensor of ingot_fields blocks."""
+        torch = _torch()
+        if n is None:
+            n = off.numel()
+        if out is None:
+            out = torch.empty((n, FIELDS_BYTES), dtype=torch.uint8, device=arena.device)
+        self._check_dev(arena, off, lens, out)
+        _lib.check(self._lib.ingot_gpu_fields(self._h, _ptr(arena), _ptr(off), _ptr(lens),
+                                              int(stride), n, int(chain), _ptr(out),
+                                              _stream(stream)),
+                   "ingot_gpu_fields")
+        return out
+
+
+def records_to_numpy(t):
+    """(n, 16) uint8 tensor/array -> numpy structured array of ingot_rec."""
+    import numpy as np
+
+    a = t.cpu().numpy() if hasattr(t, "cpu") else np.asarray(t)
+    return np.ascontiguousarray(a).view(REC_DTYPE).reshape(-1)
+
+
+def fields_to_numpy(t):
+    import numpy as np
+
+    a = t.cpu().numpy() if hasattr(t, "cpu") else np.asarray(t)
+    return np.ascontiguousarray(a).view(FIELDS_DTYPE).reshape(-1)
+
+
+# ---------------------------------------------------------------------------
+# Synthetic traffic (include/ingot_pktgen.h)
+# ---------------------------------------------------------------------------
+def gen_lengths(profile: GenProfile, n: int, seed: int = GEN_SEED, first: int = 0,
+                device: int = 0, stream=None):
+    torch = _torch()
+    lens = torch.empty(n, dtype=torch.uint16, device=f"cuda:{device}")
+    _lib.check(_lib.load().ingot_pktgen_lengths(int(profile), seed, first, n, _ptr(lens),
+                                                _stream(stream)), "ingot_pktgen_lengths")
+    return lens
+
+
+def gen_frames(profile: GenProfile, n: int, seed: int = GEN_SEED, first: int = 0,
+               stride: Optional[int] = None, device: int = 0, stream=None, slack: int = 256):
+    """Generate n frames on `device`.  Returns (arena, off, lens).
+
+    stride=None packs frames back-to-back (u64 offsets); a stride lays them
+    out one per slot (off=None).  `slack` extra arena bytes follow the last
+    frame.
+    """
+    torch = _torch()
+    dev = f"cuda:{device}"
+    lib = _lib.load()
+    if stride is not None:
+        if profile == GenProfile.V4UDP64:
+            lens = None
+        else:
+            lens = gen_lengths(profile, n, seed, first, device, stream)
+            lens = torch.minimum(lens.to(torch.int32), torch.tensor(stride, device=dev)).to(
+                torch.uint16)
+        nbytes = n * stride + slack
+        arena = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        _lib.check(lib.ingot_pktgen_fill(int(profile), seed, first, n, None, int(stride),
+                                         _ptr(lens), _ptr(arena), nbytes, _stream(stream)),
+                   "ingot_pktgen_fill")
+        return arena, None, lens
+    lens = gen_lengths(profile, n, seed, first, device, stream)
+    ends = lens.to(torch.int64).cumsum(0)
+    off = ends - lens.to(torch.int64)
+    total = int(ends[-1].item()) if n else 0
+    nbytes = total + slack
+    arena = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    _lib.check(lib.ingot_pktgen_fill(int(profile), seed, first, n, _ptr(off), 0, _ptr(lens),
+                                     _ptr(arena), nbytes, _stream(stream)), "ingot_pktgen_fill")
+    return arena, off, lens
+
+
+# ---------------------------------------------------------------------------
+# Per-packet mirror of ingot's chain API, on the device path.
+# ---------------------------------------------------------------------------
+@dataclass
+class _View:
+    """Getter view over one parsed header (values from the ingot_fields block)."""
+
+    frame: bytes
+    f: object  # numpy.void of FIELDS_DTYPE
+    off: int
+
+
+class EthernetView(_View):
+    def destination(self) -> bytes:
+        return bytes(self.f["eth_destination"])
+
+    def source(self) -> bytes:
+        return bytes(self.f["eth_source"])
+
+    def ethertype(self) -> int:
+        return int(self.f["eth_ethertype"])
+
+
+class VlanView(_View):
+    idx: int = 0
+
+    def priority(self) -> int:
+        return int(self.f["vlan_priority"][self.idx])
+
+    def dei(self) -> int:
+        return int(self.f["vlan_dei"][self.idx])
+
+    def vid(self) -> int:
+        return int(self.f["vlan_vid"][self.idx])
+
+    def ethertype(self) -> int:
+        return int(self.f["vlan_ethertype"][self.idx])
+
+
+class Ipv4View(_View):
+    kind = L3Kind.IPV4
+
+    def __getattr__(self, name):
+        key = "v4_" + name
+        if key in FIELDS_DTYPE.names:
+            v = self.f[key]
+            return (lambda: bytes(v)) if v.shape else (lambda: int(v))
+        raise AttributeError(name)
+
+    def options_ref(self) -> bytes:
+        o, n = int(self.f["v4_options_off"]), int(self.f["v4_options_len"])
+        return self.frame[o:o + n]
+
+    def next_layer(self) -> int:
+        return int(self.f["v4_protocol"])
+
+
+@dataclass
+class V6Eh:
+    kind: int
+    next_header: int
+    ext_len: int
+    fragment_offset: int
+    res: int
+    more_frags: int
+    ident: int
+    off: int
+
+
+class Ipv6View(_View):
+    kind = L3Kind.IPV6
+    hint: int = 0
+
+    def __getattr__(self, name):
+        key = "v6_" + name
+        if key in FIELDS_DTYPE.names:
+            v = self.f[key]
+            return (lambda: bytes(v)) if v.shape else (lambda: int(v))
+        raise AttributeError(name)
+
+    def extension_headers(self) -> list:
+        n = min(int(self.f["rec"]["n_v6ext"]), MAX_EH_FIELDS)
+        out = []
+        for e in self.f["v6_eh"][:n]:
+            frm = int(e["frag_res_more"])
+            out.append(V6Eh(int(e["kind"]), int(e["next_header"]), int(e["ext_len"]),
+                            int(e["frag_offset"]), frm >> 1, frm & 1, int(e["ident"]),
+                            int(e["off"])))
+        return out
+
+    def v6ext_bytes(self) -> bytes:
+        o, n = int(self.f["v6_ext_off"]), int(self.f["v6_ext_len"])
+        return self.frame[o:o + n]
+
+    def next_layer(self) -> int:
+        return self.hint
+
+
+class TcpView(_View):
+    kind = L4Kind.TCP
+
+    def source(self) -> int:
+        return int(self.f["l4_source"])
+
+    def destination(self) -> int:
+        return int(self.f["l4_destination"])
+
+    def __getattr__(self, name):
+        key = "tcp_" + name
+        if key in FIELDS_DTYPE.names:
+            return lambda: int(self.f[key])
+        raise AttributeError(name)
+
+    def options_ref(self) -> bytes:
+        o, n = int(self.f["tcp_options_off"]), int(self.f["tcp_options_len"])
+        return self.frame[o:o + n]
+
+
+class UdpView(_View):
+    kind = L4Kind.UDP
+
+    def source(self) -> int:
+        return int(self.f["l4_source"])
+
+    def destination(self) -> int:
+        return int(self.f["l4_destination"])
+
+    def length(self) -> int:
+        return int(self.f["udp_length"])
+
+    def checksum(self) -> int:
+        return int(self.f["udp_checksum"])
+
+
+class IcmpView(_View):
+    def ty(self) -> int:
+        return int(self.f["icmp_ty"])
+
+    def code(self) -> int:
+        return int(self.f["icmp_code"])
+
+    def checksum(self) -> int:
+        return int(self.f["icmp_checksum"])
+
+    def rest_of_hdr(self) -> bytes:
+        return bytes(self.f["icmp_rest_of_hdr"])
+
+
+class IcmpV4View(IcmpView):
+    kind = L4Kind.ICMPV4
+
+
+class IcmpV6View(IcmpView):
+    kind = L4Kind.ICMPV6
+
+
+@dataclass
+class Headers:
+    """The parsed chain (`ValidUdpParser` etc.): one attribute per layer,
+    named as the reference struct's fields; Option<> layers may be None."""
+
+    names: tuple
+    layers: dict
+    rec: object
+
+    def __getattr__(self, name):
+        layers = self.__dict__.get("layers", {})
+        if name in layers:
+            return layers[name]
+        raise AttributeError(name)
+
+
+_default_ctx: dict = {}
+
+
+def _ctx_for(device: int) -> Context:
+    if device not in _default_ctx:
+        _default_ctx[device] = Context(device)
+    return _default_ctx[device]
+
+
+def parse_frames(frames: list, chain: Chain, device: int = 0):
+    """Run the device fields kernel on a list of frames; returns (records
+    structured array, fields structured array)."""
+    import numpy as np
+
+    torch = _torch()
+    ctx = _ctx_for(device)
+    dev = f"cuda:{device}"
+    lens_l = [len(f) for f in frames]
+    offs_l, o = [], 0
+    for ln in lens_l:
+        offs_l.append(o)
+        o += (ln + 15) // 16 * 16 + 16
+    buf = np.zeros(max(o, 16) + 64, dtype=np.uint8)
+    for f, off in zip(frames, offs_l):
+        buf[off:off + len(f)] = np.frombuffer(bytes(f), dtype=np.uint8)
+    arena = torch.from_numpy(buf).to(dev)
+    off = torch.tensor(offs_l, dtype=torch.int64, device=dev)
+    lens = torch.tensor(lens_l, dtype=torch.int32, device=dev).to(torch.uint16)
+    recs = ctx.parse(arena, off, lens, chain)
+    flds = ctx.fields(arena, off, lens, chain)
+    torch.cuda.synchronize(device)
+    return records_to_numpy(recs), fields_to_numpy(flds)
+
+
+class _ChainParser:
+    chain: Chain
+    names: tuple
+
+    @classmethod
+    def parse(cls, frame: bytes, device: int = 0):
+        """`<Chain>::parse(frame)` on the device: (headers, None, remainder),
+        or raises PacketParseError(label, ParseError)."""
+        recs, flds = parse_frames([bytes(frame)], cls.chain, device)
+        return cls._assemble(bytes(frame), recs[0], flds[0])
+
+    parse_slice = parse
+
+    @classmethod
+    def _assemble(cls, frame: bytes, r, f):
+        status = int(r["status"])
+        if status != STATUS_OK:
+            raise PacketParseError(CHAIN_LABELS[cls.chain][int(r["err_layer"])],
+                                   ParseError(status))
+        layers = {}
+        eth_name, l3_name, l4_name = cls.names[0], cls.names[-2], cls.names[-1]
+        layers[eth_name] = EthernetView(frame, f, 0)
+        if cls.chain == Chain.VlanUlp:
+            tags = []
+            for k in range(int(r["n_vlan"])):
+                v = VlanView(frame, f, 14 + 4 * k)
+                v.idx = k
+                tags.append(v)
+            layers["vlan"] = tags
+        l3 = None
+        if int(r["l3_kind"]) == L3Kind.IPV4:
+            l3 = Ipv4View(frame, f, int(r["l3_off"]))
+        elif int(r["l3_kind"]) == L3Kind.IPV6:
+            l3 = Ipv6View(frame, f, int(r["l3_off"]))
+            l3.hint = int(r["l4_proto"])
+        layers[l3_name] = l3
+        l4 = None
+        k4 = int(r["l4_kind"])
+        cls4 = {L4Kind.TCP: TcpView, L4Kind.UDP: UdpView, L4Kind.ICMPV4: IcmpV4View,
+                L4Kind.ICMPV6: IcmpV6View}.get(k4)
+        if cls4 is not None:
+            l4 = cls4(frame, f, int(r["l4_off"]))
+        layers[l4_name] = l4
+        hdrs = Headers(cls.names, layers, r)
+        return hdrs, None, frame[int(r["payload_off"]):]
+
+
+class UdpParser(_ChainParser):
+    """ingot-examples/src/packets.rs:18-24"""
+
+    chain = Chain.UdpParser
+    names = ("eth", "l3", "l4")
+
+
+class GenericUlp(_ChainParser):
+    """ingot-examples/src/packets.rs:54-60"""
+
+    chain = Chain.GenericUlp
+    names = ("inner_eth", "inner_l3", "inner_ulp")
+
+
+class VlanUlp(_ChainParser):
+    """Build-defined Ethernet / 0-2 VlanBody / L3 / Ulp chain."""
+
+    chain = Chain.VlanUlp
+    names = ("eth", "vlan", "l3", "l4")

@@ -1,0 +1,81 @@
+"""ctypes binding of the in-tree native library (ingot_amd/lib/libingot_gpu.so).
+
+The library is the product: there is no Python or CPU fallback for any entry
+point.  If it is missing, importing the compute API raises, loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "lib" / "libingot_gpu.so"
+
+c_u8p = ctypes.c_void_p
+c_u64 = ctypes.c_uint64
+
+# (name, restype, argtypes) — exactly the declarations of include/ingot_gpu.h
+# and include/ingot_pktgen.h.
+SIGNATURES = {
+    "ingot_gpu_abi_version": (ctypes.c_int, []),
+    "ingot_gpu_build_info": (ctypes.c_char_p, []),
+    "ingot_gpu_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "ingot_gpu_ctx_destroy": (None, [ctypes.c_void_p]),
+    "ingot_gpu_ctx_device": (ctypes.c_int, [ctypes.c_void_p]),
+    "ingot_gpu_parse": (
+        ctypes.c_int,
+        [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, c_u64, ctypes.c_int, c_u8p, ctypes.c_void_p],
+    ),
+    "ingot_gpu_parse_strided": (
+        ctypes.c_int,
+        [ctypes.c_void_p, c_u8p, ctypes.c_uint32, c_u8p, c_u64, ctypes.c_int, c_u8p,
+         ctypes.c_void_p],
+    ),
+    "ingot_gpu_fields": (
+        ctypes.c_int,
+        [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, ctypes.c_uint32, c_u64, ctypes.c_int, c_u8p,
+         ctypes.c_void_p],
+    ),
+    "ingot_gpu_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "ingot_parse_error_name": (ctypes.c_char_p, [ctypes.c_int]),
+    "ingot_chain_layer_label": (ctypes.c_char_p, [ctypes.c_int, ctypes.c_int]),
+    "ingot_chain_layer_count": (ctypes.c_int, [ctypes.c_int]),
+    "ingot_pktgen_lengths": (
+        ctypes.c_int, [ctypes.c_int, c_u64, c_u64, c_u64, c_u8p, ctypes.c_void_p],
+    ),
+    "ingot_pktgen_fill": (
+        ctypes.c_int,
+        [ctypes.c_int, c_u64, c_u64, c_u64, c_u8p, ctypes.c_uint32, c_u8p, c_u8p, c_u64,
+         ctypes.c_void_p],
+    ),
+}
+
+_lib: ctypes.CDLL | None = None
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load libingot_gpu.so (once) and bind every exported signature."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise NativeLibraryMissing(
+            f"{LIB_PATH} is missing: build it with `python -m ingot_amd.build` "
+            "(hipcc --offload-arch=gfx950); there is no fallback path"
+        )
+    lib = ctypes.CDLL(str(LIB_PATH))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(code: int, what: str) -> None:
+    if code != 0:
+        msg = load().ingot_gpu_strerror(code).decode()
+        raise RuntimeError(f"{what} failed: {msg} ({code})")

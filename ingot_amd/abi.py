@@ -1,0 +1,182 @@
+"""ctypes / numpy mirrors of the C ABI types in include/ingot_gpu.h.
+
+These are plain data layouts (no behaviour); `tests/test_abi.py` checks the
+sizes and offsets against the header with a compiled probe.
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+
+import numpy as np
+
+ABI_VERSION = 1
+
+
+class ParseError(enum.IntEnum):
+    """ingot_types::ParseError (ingot-types/src/error.rs:22-44); value = status byte.
+
+    The record stores 1 + the Rust discriminant so that 0 can mean Ok.
+    """
+
+    Unwanted = 1
+    NeedsHint = 2
+    TooSmall = 3
+    StraddledHeader = 4
+    NoRemainingChunks = 5
+    CannotAccept = 6
+    Reject = 7
+    IllegalValue = 8
+
+
+STATUS_OK = 0
+
+
+class Chain(enum.IntEnum):
+    """Parse chains (include/ingot_gpu.h enum ingot_chain)."""
+
+    UdpParser = 0    # ingot-examples/src/packets.rs:18-24
+    GenericUlp = 1   # ingot-examples/src/packets.rs:54-60
+    VlanUlp = 2      # build-defined (VlanBody, ethernet.rs:57-65)
+
+
+CHAIN_LABELS = {
+    Chain.UdpParser: ("eth", "l3", "l4"),
+    Chain.GenericUlp: ("inner_eth", "inner_l3", "inner_ulp"),
+    Chain.VlanUlp: ("eth", "vlan", "l3", "l4"),
+}
+
+
+class L3Kind(enum.IntEnum):
+    NONE = 0
+    IPV4 = 1
+    IPV6 = 2
+
+
+class L4Kind(enum.IntEnum):
+    NONE = 0
+    TCP = 1
+    UDP = 2
+    ICMPV4 = 3
+    ICMPV6 = 4
+
+
+REC_ACCEPTED = 0x01
+MAX_EH_FIELDS = 4
+
+
+class IngotRec(ctypes.Structure):
+    _fields_ = [
+        ("status", ctypes.c_uint8),
+        ("err_layer", ctypes.c_uint8),
+        ("l3_kind", ctypes.c_uint8),
+        ("l4_kind", ctypes.c_uint8),
+        ("n_vlan", ctypes.c_uint8),
+        ("n_v6ext", ctypes.c_uint8),
+        ("l4_proto", ctypes.c_uint8),
+        ("flags", ctypes.c_uint8),
+        ("l3_off", ctypes.c_uint16),
+        ("l4_off", ctypes.c_uint16),
+        ("payload_off", ctypes.c_uint16),
+        ("ethertype", ctypes.c_uint16),
+    ]
+
+
+class IngotV6Eh(ctypes.Structure):
+    _fields_ = [
+        ("ident", ctypes.c_uint32),
+        ("frag_offset", ctypes.c_uint16),
+        ("off", ctypes.c_uint16),
+        ("kind", ctypes.c_uint8),
+        ("next_header", ctypes.c_uint8),
+        ("ext_len", ctypes.c_uint8),
+        ("frag_res_more", ctypes.c_uint8),
+    ]
+
+
+U8, U16, U32 = ctypes.c_uint8, ctypes.c_uint16, ctypes.c_uint32
+
+
+class IngotFields(ctypes.Structure):
+    _fields_ = [
+        ("rec", IngotRec),
+        ("v6_flow_label", U32),
+        ("tcp_sequence", U32),
+        ("tcp_acknowledgement", U32),
+        ("eth_ethertype", U16),
+        ("vlan_vid", U16 * 2),
+        ("vlan_ethertype", U16 * 2),
+        ("v4_total_len", U16),
+        ("v4_identification", U16),
+        ("v4_fragment_offset", U16),
+        ("v4_checksum", U16),
+        ("v4_options_off", U16),
+        ("v4_options_len", U16),
+        ("v6_payload_len", U16),
+        ("v6_ext_off", U16),
+        ("v6_ext_len", U16),
+        ("l4_source", U16),
+        ("l4_destination", U16),
+        ("tcp_window_size", U16),
+        ("tcp_checksum", U16),
+        ("tcp_urgent_ptr", U16),
+        ("tcp_options_off", U16),
+        ("tcp_options_len", U16),
+        ("udp_length", U16),
+        ("udp_checksum", U16),
+        ("icmp_checksum", U16),
+        ("eth_destination", U8 * 6),
+        ("eth_source", U8 * 6),
+        ("vlan_priority", U8 * 2),
+        ("vlan_dei", U8 * 2),
+        ("v4_version", U8),
+        ("v4_ihl", U8),
+        ("v4_dscp", U8),
+        ("v4_ecn_raw", U8),
+        ("v4_ecn", U8),
+        ("v4_flags", U8),
+        ("v4_hop_limit", U8),
+        ("v4_protocol", U8),
+        ("v4_source", U8 * 4),
+        ("v4_destination", U8 * 4),
+        ("v6_version", U8),
+        ("v6_dscp", U8),
+        ("v6_ecn_raw", U8),
+        ("v6_ecn", U8),
+        ("v6_next_header", U8),
+        ("v6_hop_limit", U8),
+        ("v6_source", U8 * 16),
+        ("v6_destination", U8 * 16),
+        ("tcp_data_offset", U8),
+        ("tcp_reserved", U8),
+        ("tcp_flags", U8),
+        ("icmp_ty", U8),
+        ("icmp_code", U8),
+        ("icmp_rest_of_hdr", U8 * 4),
+        ("_pad0", U8),
+        ("v6_eh", IngotV6Eh * MAX_EH_FIELDS),
+        ("_pad1", U8 * 52),
+    ]
+
+
+assert ctypes.sizeof(IngotRec) == 16
+assert ctypes.sizeof(IngotV6Eh) == 12
+assert ctypes.sizeof(IngotFields) == 256
+
+REC_DTYPE = np.dtype(IngotRec)
+FIELDS_DTYPE = np.dtype(IngotFields)
+REC_BYTES = REC_DTYPE.itemsize
+FIELDS_BYTES = FIELDS_DTYPE.itemsize
+
+
+class GenProfile(enum.IntEnum):
+    """Synthetic traffic profiles (include/ingot_pktgen.h)."""
+
+    ADVERSARIAL = 0
+    V4UDP64 = 2
+    MIXED = 3
+    VLAN_V6EH = 4
+    FLOWS = 5
+
+
+GEN_SEED = 20250808

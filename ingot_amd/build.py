@@ -1,0 +1,86 @@
+"""Build the native library in-tree: ingot_amd/lib/libingot_gpu.so (gfx950).
+
+    python -m ingot_amd.build [--force]
+
+Each HIP/C++ source is compiled to an object with hipcc (in parallel), then
+linked into one shared library.  Objects are rebuilt when a source or any
+header under include/ or csrc/ is newer.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+BUILD = PKG / "build"
+LIB = PKG / "lib" / "libingot_gpu.so"
+SOURCES = ["parse.hip", "pktgen.hip", "api.cpp"]
+ARCH = "gfx950"
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found: the gfx950 library cannot be built")
+
+
+def _headers() -> list[Path]:
+    return sorted((ROOT / "include").glob("*.h")) + sorted(CSRC.glob("*.h"))
+
+
+def _stale(target: Path, deps: list[Path]) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def _compile(src: Path, obj: Path) -> None:
+    cmd = [
+        hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+        "-Wall", "-Wno-unused-function",
+        f"-I{ROOT / 'include'}", "-c", str(src), "-o", str(obj),
+    ]
+    if src.suffix == ".cpp":
+        cmd[1:1] = ["-x", "hip"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    BUILD.mkdir(exist_ok=True)
+    LIB.parent.mkdir(exist_ok=True)
+    headers = _headers()
+    jobs = []
+    objs = []
+    for name in SOURCES:
+        src = CSRC / name
+        obj = BUILD / (name + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [src] + headers):
+            jobs.append((src, obj))
+    if jobs:
+        with cf.ThreadPoolExecutor(max_workers=min(len(jobs), 4)) as ex:
+            for f in [ex.submit(_compile, s, o) for s, o in jobs]:
+                f.result()
+    if force or jobs or _stale(LIB, objs):
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB)]
+        cmd += [str(o) for o in objs]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if verbose:
+        print(f"built {LIB}")
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)

@@ -1,0 +1,159 @@
+// api.cpp — the C ABI (include/ingot_gpu.h) over the HIP kernels.
+//
+// Argument checking, context handling and the string tables that mirror
+// ingot's error surface: ParseError::as_cstr (ingot-types/src/error.rs:49-60)
+// and the per-layer labels a generated chain attaches to PacketParseError
+// (ingot-macros/src/parse.rs:36-50, field names from
+// ingot-examples/src/packets.rs:18-24, 54-60).
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <new>
+
+#include "../../include/ingot_gpu.h"
+#include "kernels.h"
+
+struct ingot_gpu_ctx {
+    int device;
+    uint32_t max_blocks;  // 0 = automatic grid sizing (INGOT_GPU_MAX_BLOCKS overrides)
+};
+
+namespace {
+
+const char* const kParseErrorNames[] = {
+    "Ok",           "Unwanted",       "NeedsHint", "TooSmall",    "StraddledHeader",
+    "NoRemainingChunks", "CannotAccept", "Reject",    "IllegalValue",
+};
+
+const char* const kUdpParserLabels[] = {"eth", "l3", "l4"};
+const char* const kGenericUlpLabels[] = {"inner_eth", "inner_l3", "inner_ulp"};
+const char* const kVlanUlpLabels[] = {"eth", "vlan", "l3", "l4"};
+
+int chain_ok(int chain) { return chain >= 0 && chain < INGOT_CHAIN_COUNT; }
+
+int from_hip(hipError_t e) { return e == hipSuccess ? INGOT_GPU_SUCCESS : INGOT_GPU_EHIP; }
+
+// Make the context's device current for the launch (callers may juggle
+// devices on one thread).
+int enter(const ingot_gpu_ctx* ctx) {
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess) return INGOT_GPU_EHIP;
+    if (cur != ctx->device && hipSetDevice(ctx->device) != hipSuccess) return INGOT_GPU_EHIP;
+    return INGOT_GPU_SUCCESS;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ingot_gpu_abi_version(void) { return INGOT_GPU_ABI_VERSION; }
+
+const char* ingot_gpu_build_info(void) {
+    return "ingot_gpu " __DATE__ " gfx950 (LDS-DMA staged wave-per-64-packet parse)";
+}
+
+int ingot_gpu_ctx_create(int device, ingot_gpu_ctx** out) {
+    if (!out) return INGOT_GPU_EINVAL;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count)
+        return INGOT_GPU_ENODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return INGOT_GPU_EHIP;
+    // Code objects are built for gfx950 only.
+    if (prop.gcnArchName[0] && std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return INGOT_GPU_ENODEV;
+    ingot_gpu_ctx* c = new (std::nothrow) ingot_gpu_ctx{device, 0};
+    if (!c) return INGOT_GPU_ENOMEM;
+    if (const char* mb = std::getenv("INGOT_GPU_MAX_BLOCKS")) c->max_blocks = (uint32_t)std::atoi(mb);
+    *out = c;
+    return INGOT_GPU_SUCCESS;
+}
+
+void ingot_gpu_ctx_destroy(ingot_gpu_ctx* ctx) { delete ctx; }
+
+int ingot_gpu_ctx_device(const ingot_gpu_ctx* ctx) { return ctx ? ctx->device : -1; }
+
+int ingot_gpu_parse(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
+                    const uint16_t* d_len, uint64_t n, int chain, ingot_rec* d_out,
+                    void* stream) {
+    if (!ctx || !chain_ok(chain)) return INGOT_GPU_EINVAL;
+    if (n == 0) return INGOT_GPU_SUCCESS;
+    if (!d_arena || !d_off || !d_len || !d_out) return INGOT_GPU_EINVAL;
+    if (int e = enter(ctx)) return e;
+    ingot_gpu::ParseArgs a{d_arena, d_off, d_len, 0, n, d_out, nullptr};
+    return from_hip(ingot_gpu::launch_parse(a, ingot_gpu::LAYOUT_INDEXED, chain, false,
+                                            ctx->max_blocks, (hipStream_t)stream));
+}
+
+int ingot_gpu_parse_strided(ingot_gpu_ctx* ctx, const uint8_t* d_arena, uint32_t stride,
+                            const uint16_t* d_len, uint64_t n, int chain, ingot_rec* d_out,
+                            void* stream) {
+    if (!ctx || !chain_ok(chain)) return INGOT_GPU_EINVAL;
+    if (n == 0) return INGOT_GPU_SUCCESS;
+    if (!d_arena || !d_out) return INGOT_GPU_EINVAL;
+    if (stride == 0 || stride % 16u != 0 || stride > 65535u) return INGOT_GPU_ERANGE;
+    if (((uintptr_t)d_arena & 15u) != 0) return INGOT_GPU_EINVAL;
+    if (int e = enter(ctx)) return e;
+    ingot_gpu::ParseArgs a{d_arena, nullptr, d_len, stride, n, d_out, nullptr};
+    return from_hip(ingot_gpu::launch_parse(a, ingot_gpu::LAYOUT_STRIDED, chain, false,
+                                            ctx->max_blocks, (hipStream_t)stream));
+}
+
+int ingot_gpu_fields(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
+                     const uint16_t* d_len, uint32_t stride, uint64_t n, int chain,
+                     ingot_fields* d_out, void* stream) {
+    if (!ctx || !chain_ok(chain)) return INGOT_GPU_EINVAL;
+    if (n == 0) return INGOT_GPU_SUCCESS;
+    if (!d_arena || !d_out) return INGOT_GPU_EINVAL;
+    int layout = ingot_gpu::LAYOUT_INDEXED;
+    if (!d_off) {
+        if (stride == 0 || stride % 16u != 0 || stride > 65535u) return INGOT_GPU_ERANGE;
+        if (((uintptr_t)d_arena & 15u) != 0) return INGOT_GPU_EINVAL;
+        layout = ingot_gpu::LAYOUT_STRIDED;
+    } else if (!d_len) {
+        return INGOT_GPU_EINVAL;
+    }
+    if (int e = enter(ctx)) return e;
+    ingot_gpu::ParseArgs a{d_arena, d_off, d_len, stride, n, nullptr, d_out};
+    return from_hip(
+        ingot_gpu::launch_parse(a, layout, chain, true, ctx->max_blocks, (hipStream_t)stream));
+}
+
+const char* ingot_gpu_strerror(int code) {
+    switch (code) {
+    case INGOT_GPU_SUCCESS: return "success";
+    case INGOT_GPU_EINVAL: return "invalid argument";
+    case INGOT_GPU_EHIP: return "HIP runtime error";
+    case INGOT_GPU_ENOMEM: return "out of host memory";
+    case INGOT_GPU_ENODEV: return "no such gfx950 device";
+    case INGOT_GPU_ERANGE: return "size outside the supported range";
+    default: return "unknown error";
+    }
+}
+
+const char* ingot_parse_error_name(int status) {
+    if (status < 0 || status > INGOT_ERR_ILLEGAL_VALUE) return nullptr;
+    return kParseErrorNames[status];
+}
+
+int ingot_chain_layer_count(int chain) {
+    switch (chain) {
+    case INGOT_CHAIN_UDP_PARSER: return 3;
+    case INGOT_CHAIN_GENERIC_ULP: return 3;
+    case INGOT_CHAIN_VLAN_ULP: return 4;
+    default: return -1;
+    }
+}
+
+const char* ingot_chain_layer_label(int chain, int layer) {
+    if (layer < 0 || layer >= ingot_chain_layer_count(chain)) return nullptr;
+    switch (chain) {
+    case INGOT_CHAIN_UDP_PARSER: return kUdpParserLabels[layer];
+    case INGOT_CHAIN_GENERIC_ULP: return kGenericUlpLabels[layer];
+    default: return kVlanUlpLabels[layer];
+    }
+}
+
+}  // extern "C"

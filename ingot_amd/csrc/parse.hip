@@ -1,0 +1,487 @@
+// parse.hip — CDNA4 (gfx950) batched L2/L3/L4 header extraction.
+//
+// Replaces ingot's per-packet parse path for a whole batch:
+//   * the chain driver `parse_slice` (ingot-macros/src/parse.rs:496-509,
+//     layer fragments 292-416) -> `walk()`;
+//   * the generated per-header bodies `HeaderParse::parse_choice`
+//     (ingot-macros/src/packet/mod.rs:1831-2005) over Accessor chunks
+//     (ingot-types/src/accessor.rs:30-67) -> the per-layer blocks of `walk()`;
+//   * the `#[choice]` dispatch (choice.rs:231-246) -> ethertype / protocol
+//     switches; the IPv6 extension-header loop RepeatedView::parse_choice
+//     (ingot-types/src/util.rs:189-228) -> the EH loop;
+//   * the XRef getters (bitfield.rs:40-315) -> `Frame::get(Field)` over the
+//     constexpr layouts in layouts.h.
+//
+// Execution model (one lane per packet, 64 packets per wave-tile):
+//   1. descriptors: lane i loads its own (offset, len) — coalesced;
+//   2. staging: the wave copies the first bytes of its 64 frames (a window of
+//      NCH 16-B chunks per frame) HBM -> LDS with `global_load_lds_dwordx4`
+//      (LDS-DMA, 1 KiB per wave instruction, no VGPR round trip).  The LDS
+//      image is lane-linear per instruction, so the per-packet chunk order is
+//      XOR-swizzled on the *source* address (power-of-two NCH) to keep both
+//      per-lane dword reads (4-way floor) and b128 reads conflict-free;
+//   3. parse: each lane walks Ethernet -> (VLAN) -> IPv4/IPv6(+EHs) -> L4 on
+//      its own window, reading big-endian fields with aligned LDS dword pairs
+//      + v_alignbyte; bytes past the window (long option / EH chains) are read
+//      straight from HBM by the lanes that need them;
+//   4. output: one 16-B record per lane (dwordx4, fully coalesced), or the
+//      256-B field block in parity mode.
+// No MFMA: this is integer field extraction bounded by HBM bandwidth.
+#include <hip/hip_runtime.h>
+
+#include "../../include/ingot_gpu.h"
+#include "kernels.h"
+#include "layouts.h"
+
+namespace ingot_gpu {
+namespace {
+
+using namespace layout;
+
+constexpr uint32_t WAVE = 64;
+constexpr uint32_t WAVES = 4;
+constexpr uint32_t BLOCK = WAVE * WAVES;
+
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) void lds_void;
+
+// Slot (16-B unit) of chunk c of packet p inside a wave's LDS image.
+// NCH = 4: g(p) = (p>>2)&3; NCH = 8: g(p) = (p>>1)&7 (see header comment);
+// other NCH: linear.
+template <uint32_t NCH>
+__device__ __forceinline__ uint32_t swz(uint32_t p) {
+    if constexpr (NCH == 4) return (p >> 2) & 3u;
+    else if constexpr (NCH == 8) return (p >> 1) & 7u;
+    else return 0u;
+}
+
+template <uint32_t NCH>
+__device__ __forceinline__ uint32_t slot_of(uint32_t p, uint32_t c) {
+    return NCH * p + (c ^ swz<NCH>(p));
+}
+
+// One lane's view of its frame: LDS window for the first bytes, HBM beyond.
+template <uint32_t NCH>
+struct Frame {
+    const lds_u32* win;  // this wave's LDS image
+    uint32_t p;          // packet index within the wave (== lane)
+    uint32_t sh;         // frame start inside its first staged chunk (0..15)
+    uint32_t avail;      // frame bytes [0, avail) are staged in LDS
+    uint32_t len;        // frame length
+    const uint8_t* g;    // frame start in HBM
+
+    __device__ __forceinline__ uint32_t dw(uint32_t b) const {
+        return win[slot_of<NCH>(p, b >> 4) * 4u + ((b >> 2) & 3u)];
+    }
+
+    // n (1..4) bytes at frame offset i as a big-endian integer.
+    // Caller guarantees i + n <= len (every read follows its bounds check).
+    __device__ __forceinline__ uint32_t be(uint32_t i, uint32_t n) const {
+        uint32_t v;
+        if (i + n <= avail) {
+            const uint32_t b = sh + i;
+            const uint32_t a = b & ~3u;
+            const uint32_t d0 = dw(a);
+            const uint32_t d1 = ((b & 3u) + n > 4u) ? dw(a + 4u) : 0u;
+            const uint32_t x = __builtin_amdgcn_alignbyte(d1, d0, b & 3u);  // bytes b.. little-endian
+            v = __builtin_bswap32(x) >> (32u - 8u * n);
+        } else {
+            v = 0;
+            for (uint32_t k = 0; k < n; ++k) v = (v << 8) | g[i + k];
+        }
+        return v;
+    }
+
+    // Getter of a layout field of the header starting at `hdr`.
+    __device__ __forceinline__ uint32_t get(uint32_t hdr, Field f) const {
+        return (be(hdr + f.byte0(), f.nbytes()) >> f.rshift()) & f.mask();
+    }
+};
+
+struct Rec {
+    uint32_t status, err_layer, l3_kind, l4_kind, n_vlan, n_v6ext, l4_proto, flags;
+    uint32_t l3_off, l4_off, payload_off, ethertype;
+};
+
+__device__ __forceinline__ uint4 pack(const Rec& r) {
+    uint4 o;
+    o.x = r.status | (r.err_layer << 8) | (r.l3_kind << 16) | (r.l4_kind << 24);
+    o.y = r.n_vlan | (r.n_v6ext << 8) | (r.l4_proto << 16) | (r.flags << 24);
+    o.z = (r.l3_off & 0xffffu) | (r.l4_off << 16);
+    o.w = (r.payload_off & 0xffffu) | (r.ethertype << 16);
+    return o;
+}
+
+__device__ __forceinline__ uint32_t eh_class(uint32_t h) {
+    // IpProtocol::class (ip.rs:40-54)
+    if (h == 44u) return EH_FRAGMENT;
+    const bool r6564 = h == 0u || h == 43u || h == 60u || h == 135u || h == 139u || h == 140u ||
+                       h == 253u || h == 254u;
+    return r6564 ? EH_RFC6564 : EH_NONE;
+}
+
+__device__ __forceinline__ uint8_t ecn_from_network(uint32_t raw) {
+    return (uint8_t)(raw == 3u ? 1u : raw);  // Ecn::from_network, ip.rs:111-119
+}
+
+template <class FR>
+__device__ __forceinline__ void copy_bytes(const FR& f, uint32_t at, uint8_t* dst, uint32_t n) {
+    for (uint32_t k = 0; k < n; k += 4) {
+        const uint32_t m = n - k < 4u ? n - k : 4u;  // never read past the field
+        const uint32_t v = f.be(at + k, m) << (8u * (4u - m));
+        dst[k] = (uint8_t)(v >> 24);
+        dst[k + 1] = (uint8_t)(v >> 16);
+        if (k + 2 < n) dst[k + 2] = (uint8_t)(v >> 8);
+        if (k + 3 < n) dst[k + 3] = (uint8_t)v;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The chain walk: `<Chain>::parse_slice` for one frame.
+// Layer indices are the chain's PacketParseError labels (parse.rs:36-50).
+// ---------------------------------------------------------------------------
+template <int CHAIN, bool FIELDS, class FR>
+__device__ __forceinline__ void walk(const FR& f, Rec& r, ingot_fields* F) {
+    constexpr uint32_t L_L3 = CHAIN == INGOT_CHAIN_VLAN_ULP ? 2u : 1u;
+    constexpr uint32_t L_L4 = L_L3 + 1u;
+    constexpr bool ULP = CHAIN != INGOT_CHAIN_UDP_PARSER;  // Ulp vs L4 choice
+    const uint32_t len = f.len;
+
+    r = Rec{};
+    r.err_layer = 0xffu;
+#define FAIL(layer, code)          \
+    do {                           \
+        r.status = (code);         \
+        r.err_layer = (layer);     \
+        return;                    \
+    } while (0)
+
+    // -- layer 0: Ethernet (ethernet.rs:46-55); Accessor 14 B else TooSmall.
+    if (len < eth::LEN) FAIL(0u, INGOT_ERR_TOO_SMALL);
+    uint32_t et = f.get(0, eth::ethertype);
+    uint32_t p = eth::LEN;
+    r.payload_off = p;
+    r.ethertype = et;
+    if constexpr (FIELDS) {
+        copy_bytes(f, 0, F->eth_destination, 6);
+        copy_bytes(f, 6, F->eth_source, 6);
+        F->eth_ethertype = (uint16_t)et;
+    }
+
+    // GenericUlp: control = exit_on_arp on inner_eth (packets.rs:45-51); the
+    // Option<> sled allows Accept at layer 0 (parse.rs:144-156, 221-254).
+    if constexpr (CHAIN == INGOT_CHAIN_GENERIC_ULP) {
+        if (et == ET_ARP) {
+            r.flags = INGOT_REC_ACCEPTED;
+            return;
+        }
+    }
+
+    // -- build-defined VLAN layer: up to two VlanBody tags (ethernet.rs:57-65).
+    if constexpr (CHAIN == INGOT_CHAIN_VLAN_ULP) {
+        for (uint32_t v = 0; v < 2u && (et == ET_VLAN || et == ET_QINQ); ++v) {
+            if (len - p < vlan::LEN) FAIL(1u, INGOT_ERR_TOO_SMALL);
+            if constexpr (FIELDS) {
+                F->vlan_priority[v] = (uint8_t)f.get(p, vlan::priority);
+                F->vlan_dei[v] = (uint8_t)f.get(p, vlan::dei);
+                F->vlan_vid[v] = (uint16_t)f.get(p, vlan::vid);
+            }
+            et = f.get(p, vlan::ethertype);
+            if constexpr (FIELDS) F->vlan_ethertype[v] = (uint16_t)et;
+            p += vlan::LEN;
+            r.n_vlan = v + 1u;
+            r.payload_off = p;
+            r.ethertype = et;
+        }
+    }
+
+    // -- L3 choice (choices.rs:17-21): IPV4 -> Ipv4, IPV6 -> Ipv6, else Unwanted.
+    uint32_t proto;
+    if (et == ET_IPV4) {
+        r.l3_kind = INGOT_L3_IPV4;
+        r.l3_off = p;
+        if (len - p < ipv4::LEN) FAIL(L_L3, INGOT_ERR_TOO_SMALL);
+        const uint32_t ihl = f.get(p, ipv4::ihl);
+        const uint32_t opt = ihl * 4u > 20u ? ihl * 4u - 20u : 0u;  // ip.rs:91 saturating_sub
+        if (len - p - ipv4::LEN < opt) FAIL(L_L3, INGOT_ERR_TOO_SMALL);
+        proto = f.get(p, ipv4::protocol);
+        if constexpr (FIELDS) {
+            F->v4_version = (uint8_t)f.get(p, ipv4::version);
+            F->v4_ihl = (uint8_t)ihl;
+            F->v4_dscp = (uint8_t)f.get(p, ipv4::dscp);
+            F->v4_ecn_raw = (uint8_t)f.get(p, ipv4::ecn);
+            F->v4_ecn = ecn_from_network(F->v4_ecn_raw);
+            F->v4_total_len = (uint16_t)f.get(p, ipv4::total_len);
+            F->v4_identification = (uint16_t)f.get(p, ipv4::identification);
+            F->v4_flags = (uint8_t)f.get(p, ipv4::flags);
+            F->v4_fragment_offset = (uint16_t)f.get(p, ipv4::fragment_offset);
+            F->v4_hop_limit = (uint8_t)f.get(p, ipv4::hop_limit);
+            F->v4_protocol = (uint8_t)proto;
+            F->v4_checksum = (uint16_t)f.get(p, ipv4::checksum);
+            copy_bytes(f, p + 12u, F->v4_source, 4);
+            copy_bytes(f, p + 16u, F->v4_destination, 4);
+            F->v4_options_off = (uint16_t)(p + ipv4::LEN);
+            F->v4_options_len = (uint16_t)opt;
+        }
+        p += ipv4::LEN + opt;
+    } else if (et == ET_IPV6) {
+        r.l3_kind = INGOT_L3_IPV6;
+        r.l3_off = p;
+        if (len - p < ipv6::LEN) FAIL(L_L3, INGOT_ERR_TOO_SMALL);
+        // subparse(on_next_layer): hint = next_header (mod.rs:1933-1938), then
+        // RepeatedView::parse_choice over the rest of the slice (util.rs:206-216).
+        uint32_t h = f.get(p, ipv6::next_header);
+        uint32_t q = p + ipv6::LEN;
+        uint32_t n_eh = 0;
+        bool bad = false;
+        while (q < len) {
+            const uint32_t c = eh_class(h);
+            if (c == EH_NONE) break;  // Err(Unwanted) => break
+            uint32_t used, nh, x = 0;
+            if (c == EH_FRAGMENT) {
+                if (len - q < v6frag::LEN) { bad = true; break; }
+                nh = f.be(q, 1);
+                used = v6frag::LEN;
+            } else {
+                if (len - q < v6ext6564::FIXED) { bad = true; break; }
+                x = f.be(q, 2);
+                nh = x >> 8;
+                used = 8u + 8u * (x & 0xffu);  // 2 + (6 + ext_len*8), ip.rs:209
+                if (len - q < used) { bad = true; break; }
+            }
+            if constexpr (FIELDS) {
+                if (n_eh < INGOT_MAX_EH_FIELDS) {
+                    ingot_v6eh* e = &F->v6_eh[n_eh];
+                    e->kind = (uint8_t)c;
+                    e->off = (uint16_t)q;
+                    e->next_header = (uint8_t)nh;
+                    if (c == EH_FRAGMENT) {
+                        e->ext_len = (uint8_t)f.get(q, v6frag::reserved);
+                        e->frag_offset = (uint16_t)f.get(q, v6frag::fragment_offset);
+                        e->frag_res_more = (uint8_t)((f.get(q, v6frag::res) << 1) |
+                                                     f.get(q, v6frag::more_frags));
+                        e->ident = f.get(q, v6frag::ident);
+                    } else {
+                        e->ext_len = (uint8_t)(x & 0xffu);
+                        e->frag_offset = 0;
+                        e->frag_res_more = 0;
+                        e->ident = 0;
+                    }
+                }
+            }
+            ++n_eh;
+            q += used;
+            h = nh;
+        }
+        r.n_v6ext = n_eh > 255u ? 255u : n_eh;
+        if (bad) {
+            if constexpr (FIELDS) {
+                for (uint32_t k = 0; k < INGOT_MAX_EH_FIELDS; ++k) F->v6_eh[k] = ingot_v6eh{};
+            }
+            FAIL(L_L3, INGOT_ERR_TOO_SMALL);
+        }
+        proto = h;
+        if constexpr (FIELDS) {
+            F->v6_version = (uint8_t)f.get(p, ipv6::version);
+            F->v6_dscp = (uint8_t)f.get(p, ipv6::dscp);
+            F->v6_ecn_raw = (uint8_t)f.get(p, ipv6::ecn);
+            F->v6_ecn = ecn_from_network(F->v6_ecn_raw);
+            F->v6_flow_label = f.get(p, ipv6::flow_label);
+            F->v6_payload_len = (uint16_t)f.get(p, ipv6::payload_len);
+            F->v6_next_header = (uint8_t)f.get(p, ipv6::next_header);
+            F->v6_hop_limit = (uint8_t)f.get(p, ipv6::hop_limit);
+            copy_bytes(f, p + ipv6::SOURCE_BYTE, F->v6_source, 16);
+            copy_bytes(f, p + ipv6::DESTINATION_BYTE, F->v6_destination, 16);
+            F->v6_ext_off = (uint16_t)(p + ipv6::LEN);
+            F->v6_ext_len = (uint16_t)(q - p - ipv6::LEN);
+        }
+        p = q;
+    } else {
+        FAIL(L_L3, INGOT_ERR_UNWANTED);
+    }
+    r.payload_off = p;
+    r.l4_proto = proto;
+
+    // -- L4 choice (choices.rs:25-29) / Ulp choice (choices.rs:32-38).
+    uint32_t kind;
+    if (proto == IPP_TCP) kind = INGOT_L4_TCP;
+    else if (proto == IPP_UDP) kind = INGOT_L4_UDP;
+    else if (ULP && proto == IPP_ICMP) kind = INGOT_L4_ICMPV4;
+    else if (ULP && proto == IPP_ICMP_V6) kind = INGOT_L4_ICMPV6;
+    else FAIL(L_L4, INGOT_ERR_UNWANTED);
+    r.l4_kind = kind;
+    r.l4_off = p;
+    if (kind == INGOT_L4_TCP) {
+        if (len - p < tcp::LEN) FAIL(L_L4, INGOT_ERR_TOO_SMALL);
+        const uint32_t doff = f.get(p, tcp::data_offset);
+        const uint32_t opt = doff * 4u > 20u ? doff * 4u - 20u : 0u;  // tcp.rs:28
+        if (len - p - tcp::LEN < opt) FAIL(L_L4, INGOT_ERR_TOO_SMALL);
+        if constexpr (FIELDS) {
+            F->l4_source = (uint16_t)f.get(p, tcp::source);
+            F->l4_destination = (uint16_t)f.get(p, tcp::destination);
+            F->tcp_sequence = f.get(p, tcp::sequence);
+            F->tcp_acknowledgement = f.get(p, tcp::acknowledgement);
+            F->tcp_data_offset = (uint8_t)doff;
+            F->tcp_reserved = (uint8_t)f.get(p, tcp::reserved);
+            F->tcp_flags = (uint8_t)f.get(p, tcp::flags);  // from_bits_truncate: all 8 bits
+            F->tcp_window_size = (uint16_t)f.get(p, tcp::window_size);
+            F->tcp_checksum = (uint16_t)f.get(p, tcp::checksum);
+            F->tcp_urgent_ptr = (uint16_t)f.get(p, tcp::urgent_ptr);
+            F->tcp_options_off = (uint16_t)(p + tcp::LEN);
+            F->tcp_options_len = (uint16_t)opt;
+        }
+        p += tcp::LEN + opt;
+    } else if (kind == INGOT_L4_UDP) {
+        if (len - p < udp::LEN) FAIL(L_L4, INGOT_ERR_TOO_SMALL);
+        if constexpr (FIELDS) {
+            F->l4_source = (uint16_t)f.get(p, udp::source);
+            F->l4_destination = (uint16_t)f.get(p, udp::destination);
+            F->udp_length = (uint16_t)f.get(p, udp::length);
+            F->udp_checksum = (uint16_t)f.get(p, udp::checksum);
+        }
+        p += udp::LEN;
+    } else {
+        if (len - p < icmp::LEN) FAIL(L_L4, INGOT_ERR_TOO_SMALL);
+        if constexpr (FIELDS) {
+            F->icmp_ty = (uint8_t)f.get(p, icmp::ty);
+            F->icmp_code = (uint8_t)f.get(p, icmp::code);
+            F->icmp_checksum = (uint16_t)f.get(p, icmp::checksum);
+            copy_bytes(f, p + 4u, F->icmp_rest_of_hdr, 4);
+        }
+        p += icmp::LEN;
+    }
+    r.payload_off = p;
+    // UdpParser: `#[ingot(from = "L4<Q>")] l4: UdpPacket` converts after the
+    // parse; a Tcp variant is Unwanted (choice.rs:153-187, parse.rs:196-200).
+    if constexpr (CHAIN == INGOT_CHAIN_UDP_PARSER) {
+        if (kind != INGOT_L4_UDP) FAIL(L_L4, INGOT_ERR_UNWANTED);
+    }
+#undef FAIL
+}
+
+// ---------------------------------------------------------------------------
+// Kernel.
+// ---------------------------------------------------------------------------
+template <uint32_t NCH, int LAYOUT, int CHAIN, bool FIELDS>
+__global__ __launch_bounds__(BLOCK) void k_parse(ParseArgs a) {
+    constexpr uint32_t WIN = NCH * 16u;
+    constexpr uint32_t WAVE_DW = WAVE * NCH * 4u;  // dwords per wave image
+    // +16 dwords: the second dword of a pair read may run past the last image.
+    __shared__ __attribute__((aligned(16))) uint32_t s_win[WAVES * WAVE_DW + 16];
+
+    const uint32_t lane = threadIdx.x & (WAVE - 1u);
+    const uint32_t wave = threadIdx.x / WAVE;
+    uint32_t* wimg = s_win + wave * WAVE_DW;
+    const uint64_t ntiles = (a.n + WAVE - 1u) / WAVE;
+
+    for (uint64_t t = (uint64_t)blockIdx.x * WAVES + wave; t < ntiles;
+         t += (uint64_t)gridDim.x * WAVES) {
+        const uint64_t i = t * WAVE + lane;
+        const bool valid = i < a.n;
+        uint64_t off;
+        uint32_t len;
+        if constexpr (LAYOUT == LAYOUT_STRIDED) {
+            off = i * a.stride;
+            len = valid ? (a.len ? (uint32_t)a.len[i] : a.stride) : 0u;
+            if (len > a.stride) len = a.stride;  // a slot holds at most one frame
+        } else {
+            off = valid ? a.off[i] : 0u;
+            len = valid ? (uint32_t)a.len[i] : 0u;
+        }
+        const uint64_t base = off & ~(uint64_t)15;
+        const uint32_t sh = (uint32_t)(off & 15u);
+        const uint32_t take = len < WIN - sh ? len : WIN - sh;
+        const uint32_t nch = (sh + take + 15u) >> 4;
+
+        // Stage: instruction k, lane L fills LDS slot q = 64k + L, i.e.
+        // packet p = q / NCH, swizzled chunk c.  (LDS-DMA: lane-linear image.)
+#pragma unroll
+        for (uint32_t k = 0; k < NCH; ++k) {
+            const uint32_t q = k * WAVE + lane;
+            const uint32_t pp = q / NCH;
+            const uint32_t c = (q - pp * NCH) ^ swz<NCH>(pp);
+            const uint32_t np = (uint32_t)__shfl((int)nch, (int)pp);
+            uint64_t bp;
+            if constexpr (LAYOUT == LAYOUT_STRIDED) {
+                bp = (t * WAVE + pp) * a.stride;
+            } else {
+                bp = (uint64_t)__shfl((long long)base, (int)pp);
+            }
+            if (c < np) {
+                __builtin_amdgcn_global_load_lds((const void*)(a.arena + bp + 16u * c),
+                                                 (lds_void*)(wimg + k * WAVE * 4u), 16, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+        Frame<NCH> fr{(const lds_u32*)wimg, lane, sh, take, len, a.arena + off};
+        Rec r;
+        if constexpr (FIELDS) {
+            ingot_fields* F = a.fields + (valid ? i : 0);
+            if (valid) {
+                uint4* z = reinterpret_cast<uint4*>(F);
+#pragma unroll
+                for (int k = 0; k < 16; ++k) z[k] = make_uint4(0, 0, 0, 0);
+                walk<CHAIN, true>(fr, r, F);
+                reinterpret_cast<uint4*>(F)[0] = pack(r);
+            }
+        } else {
+            walk<CHAIN, false>(fr, r, nullptr);
+            if (valid) reinterpret_cast<uint4*>(a.out)[i] = pack(r);
+        }
+        // The next tile's LDS-DMA overwrites this image: every lane's reads
+        // above have returned (their values were consumed by the store).
+    }
+}
+
+template <uint32_t NCH, int LAYOUT, bool FIELDS>
+hipError_t launch_chain(const ParseArgs& a, int chain, uint32_t grid, hipStream_t s) {
+    switch (chain) {
+    case INGOT_CHAIN_UDP_PARSER:
+        hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_UDP_PARSER, FIELDS>), dim3(grid),
+                           dim3(BLOCK), 0, s, a);
+        break;
+    case INGOT_CHAIN_GENERIC_ULP:
+        hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_GENERIC_ULP, FIELDS>), dim3(grid),
+                           dim3(BLOCK), 0, s, a);
+        break;
+    default:
+        hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_VLAN_ULP, FIELDS>), dim3(grid),
+                           dim3(BLOCK), 0, s, a);
+        break;
+    }
+    return hipGetLastError();
+}
+
+uint32_t grid_for(uint64_t n, uint32_t lds_bytes_per_block, uint32_t max_blocks) {
+    const uint64_t tiles = (n + WAVE - 1) / WAVE;
+    const uint64_t want = (tiles + WAVES - 1) / WAVES;
+    uint32_t per_cu = 163840u / (lds_bytes_per_block ? lds_bytes_per_block : 1u);
+    if (per_cu > 8u) per_cu = 8u;
+    if (per_cu < 1u) per_cu = 1u;
+    uint64_t cap = max_blocks ? max_blocks : 256ull * per_cu;
+    uint64_t g = want < cap ? want : cap;
+    return (uint32_t)(g ? g : 1);
+}
+
+}  // namespace
+
+hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, bool fields,
+                        uint32_t max_blocks, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    if (layout_kind == LAYOUT_STRIDED) {
+        if (a.stride <= 64u) {
+            const uint32_t g = grid_for(a.n, WAVES * WAVE * 4u * 16u, max_blocks);
+            return fields ? launch_chain<4, LAYOUT_STRIDED, true>(a, chain, g, s)
+                          : launch_chain<4, LAYOUT_STRIDED, false>(a, chain, g, s);
+        }
+        const uint32_t g = grid_for(a.n, WAVES * WAVE * 8u * 16u, max_blocks);
+        return fields ? launch_chain<8, LAYOUT_STRIDED, true>(a, chain, g, s)
+                      : launch_chain<8, LAYOUT_STRIDED, false>(a, chain, g, s);
+    }
+    const uint32_t g = grid_for(a.n, WAVES * WAVE * 9u * 16u, max_blocks);
+    return fields ? launch_chain<9, LAYOUT_INDEXED, true>(a, chain, g, s)
+                  : launch_chain<9, LAYOUT_INDEXED, false>(a, chain, g, s);
+}
+
+}  // namespace ingot_gpu

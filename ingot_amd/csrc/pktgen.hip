@@ -1,0 +1,366 @@
+// pktgen.hip — deterministic synthetic traffic (include/ingot_pktgen.h).
+//
+// Bench/test infrastructure, not the parse path.  Every frame is a pure
+// function of (profile, seed, index): `plan()` draws the header chain and the
+// length from a counter-based SplitMix64 stream, `write_headers()` lays the
+// bytes down.  Two passes: a coalesced pattern fill of the whole arena (payload
+// and gaps), then one lane per frame writing its header bytes (clipped to the
+// frame length, so truncated frames never spill into their neighbours).
+#include <hip/hip_runtime.h>
+
+#include "../../include/ingot_gpu.h"
+#include "../../include/ingot_pktgen.h"
+
+namespace {
+
+struct Rng {
+    uint64_t s;
+    __device__ explicit Rng(uint64_t seed, uint64_t idx, uint64_t stream = 0) {
+        s = seed * 0x9E3779B97F4A7C15ull ^ (idx + 0x632BE59BD9B4E019ull) * 0xD1B54A32D192ED03ull ^
+            stream * 0x8CB92BA72F3D8DD7ull;
+        next();
+    }
+    __device__ uint64_t next() {
+        uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    }
+    __device__ uint32_t u32() { return (uint32_t)(next() >> 32); }
+    __device__ uint32_t range(uint32_t lo, uint32_t hi) {  // inclusive
+        return lo + (uint32_t)(((next() >> 32) * (uint64_t)(hi - lo + 1)) >> 32);
+    }
+    __device__ bool chance(uint32_t permille) { return range(0, 999) < permille; }
+    __device__ double unit() { return (double)(next() >> 11) * (1.0 / 9007199254740992.0); }
+};
+
+struct Plan {
+    uint32_t len;
+    uint32_t n_vlan;
+    uint32_t tpid[2];
+    uint32_t ethertype;  // after tags
+    uint32_t ihl;
+    uint32_t n_eh;
+    uint32_t eh_type[4];
+    uint32_t eh_ext[4];
+    uint32_t proto;  // L4 protocol (the last next_header)
+    uint32_t doff;
+    uint32_t flow;   // 0 = none, else 1..FLOWS_N
+    uint32_t hdr_len;
+};
+
+// Zipf(s) over {1..n} by rejection-inversion (Hörmann & Derflinger 1996).
+struct Zipf {
+    double s, n;
+    __device__ double h(double x) const { return exp(-s * log(x)); }
+    __device__ static double helper1(double x) { return fabs(x) > 1e-8 ? log1p(x) / x : 1 - x * (0.5 - x * (1.0 / 3.0 - 0.25 * x)); }
+    __device__ static double helper2(double x) { return fabs(x) > 1e-8 ? expm1(x) / x : 1 + x * 0.5 * (1 + x * (1.0 / 3.0) * (1 + 0.25 * x)); }
+    __device__ double hint(double x) const { const double lx = log(x); return helper2((1 - s) * lx) * lx; }
+    __device__ double hinv(double x) const {
+        double t = x * (1 - s);
+        if (t < -1) t = -1;
+        return exp(helper1(t) * x);
+    }
+    __device__ uint32_t sample(Rng& r) const {
+        const double hx1 = hint(1.5) - 1.0, hn = hint(n + 0.5);
+        const double sv = 2.0 - hinv(hint(2.5) - h(2.0));
+        for (int it = 0; it < 64; ++it) {
+            const double u = hn + r.unit() * (hx1 - hn);
+            const double x = hinv(u);
+            double k = floor(x + 0.5);
+            if (k < 1) k = 1;
+            if (k > n) k = n;
+            if (k - x <= sv || u >= hint(k + 0.5) - h(k)) return (uint32_t)k;
+        }
+        return 1;
+    }
+};
+
+constexpr uint32_t EH_CHOICES_C3[4] = {0, 60, 43, 44};
+
+__device__ uint32_t eh_len(uint32_t type, uint32_t ext) { return type == 44 ? 8u : 8u + 8u * ext; }
+
+__device__ Plan plan(int profile, uint64_t seed, uint64_t i) {
+    Rng r(seed, i);
+    Plan p{};
+    uint32_t hdr = 14;
+    if (profile == INGOT_GEN_V4UDP64) {
+        p.len = 64;
+        p.ethertype = 0x0800;
+        p.ihl = 5;
+        p.proto = 17;
+        p.hdr_len = 42;
+        return p;
+    }
+    if (profile == INGOT_GEN_ADVERSARIAL) {
+        // Random chain; everything the parser must reject appears.
+        const uint32_t ets[8] = {0x0800, 0x86dd, 0x8100, 0x9100, 0x0806, 0x0800, 0x86dd, 0};
+        uint32_t et = ets[r.range(0, 7)];
+        if (et == 0) et = r.range(0, 0xffff);
+        p.n_vlan = 0;
+        while ((et == 0x8100 || et == 0x9100) && p.n_vlan < 2) {
+            p.tpid[p.n_vlan++] = et;
+            hdr += 4;
+            const uint32_t nx[5] = {0x0800, 0x86dd, 0x8100, 0x9100, 0x0806};
+            et = nx[r.range(0, 4)];
+        }
+        // a third TPID stays as the inner ethertype (L3 choice -> Unwanted)
+        p.ethertype = et;
+        const uint32_t protos[12] = {6, 17, 1, 58, 0, 43, 44, 60, 59, 253, 135, 50};
+        if (et == 0x0800) {
+            p.ihl = r.chance(600) ? 5 : r.range(0, 15);
+            hdr += (p.ihl * 4 > 20 ? p.ihl * 4 : 20);
+            p.proto = r.chance(900) ? protos[r.range(0, 11)] : r.range(0, 255);
+        } else if (et == 0x86dd) {
+            hdr += 40;
+            p.n_eh = r.chance(500) ? 0 : r.range(1, 4);
+            const uint32_t ehs[10] = {0, 43, 44, 60, 135, 139, 140, 253, 254, 44};
+            for (uint32_t k = 0; k < p.n_eh; ++k) {
+                p.eh_type[k] = ehs[r.range(0, 9)];
+                p.eh_ext[k] = r.chance(700) ? r.range(0, 2) : r.range(0, 255);
+                hdr += eh_len(p.eh_type[k], p.eh_ext[k]);
+            }
+            p.proto = r.chance(900) ? protos[r.range(0, 11)] : r.range(0, 255);
+        }
+        if (p.proto == 6) {
+            p.doff = r.chance(600) ? 5 : r.range(0, 15);
+            hdr += (p.doff * 4 > 20 ? p.doff * 4 : 20);
+        } else {
+            hdr += 8;
+        }
+        p.hdr_len = hdr;
+        // Lengths cluster around the chain's end so every truncation point is hit.
+        const uint32_t mode = r.range(0, 9);
+        uint32_t len;
+        if (mode < 4) len = hdr + r.range(0, 32);
+        else if (mode < 8) len = r.range(0, hdr + 8);
+        else len = r.range(0, 160);
+        p.len = len > 65535u ? 65535u : len;
+        return p;
+    }
+
+    // MIXED / VLAN_V6EH / FLOWS
+    const bool c4 = profile != INGOT_GEN_MIXED;
+    if (c4 && r.chance(500)) {
+        if (r.chance(200)) {
+            p.n_vlan = 2;
+            p.tpid[0] = 0x9100;
+            p.tpid[1] = 0x8100;
+        } else {
+            p.n_vlan = 1;
+            p.tpid[0] = 0x8100;
+        }
+        hdr += 4 * p.n_vlan;
+    }
+    bool v6 = r.chance(500);
+    bool tcp = r.chance(500);
+    if (profile == INGOT_GEN_FLOWS) {
+        const Zipf z{1.1, (double)INGOT_GEN_FLOWS_N};
+        p.flow = z.sample(r);
+        Rng fr(seed ^ 0xF10Full, p.flow);
+        v6 = fr.chance(500);
+        tcp = fr.chance(500);
+    }
+    p.ethertype = v6 ? 0x86dd : 0x0800;
+    if (!v6) {
+        p.ihl = r.chance(900) ? 5 : r.range(6, 15);
+        hdr += p.ihl * 4;
+    } else {
+        hdr += 40;
+        const bool want_eh = c4 ? r.chance(500) : r.chance(200);
+        p.n_eh = want_eh ? r.range(1, 3) : 0;
+        for (uint32_t k = 0; k < p.n_eh; ++k) {
+            p.eh_type[k] = EH_CHOICES_C3[r.range(0, 3)];
+            p.eh_ext[k] = r.range(0, 3);
+            hdr += eh_len(p.eh_type[k], p.eh_ext[k]);
+        }
+    }
+    p.proto = tcp ? 6 : 17;
+    if (tcp) {
+        p.doff = r.chance(700) ? 5 : r.range(6, 15);
+        hdr += p.doff * 4;
+    } else {
+        hdr += 8;
+    }
+    p.hdr_len = hdr;
+    uint32_t len = r.range(64, 1500);
+    p.len = len < hdr ? hdr : len;
+    return p;
+}
+
+__global__ void k_lengths(int profile, uint64_t seed, uint64_t first, uint64_t n, uint16_t* out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (uint16_t)plan(profile, seed, first + i).len;
+}
+
+// Pattern fill: adversarial profiles get random bytes (so unknown fields are
+// arbitrary), the rest a cheap counter pattern.
+__global__ void k_pattern(int profile, uint64_t seed, uint8_t* arena, uint64_t bytes) {
+    const uint64_t words = bytes / 16;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < words;
+         w += (uint64_t)gridDim.x * blockDim.x) {
+        uint4 v;
+        if (profile == INGOT_GEN_ADVERSARIAL) {
+            Rng r(seed ^ 0xA5A5ull, w, 7);
+            const uint64_t a = r.next(), b = r.next();
+            v = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+        } else {
+            const uint32_t x = (uint32_t)(w * 0x01010101u);
+            v = make_uint4(x, x + 0x04040404u, x + 0x08080808u, x + 0x0c0c0c0cu);
+        }
+        reinterpret_cast<uint4*>(arena)[w] = v;
+    }
+    const uint64_t tail = words * 16;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < bytes - tail) arena[tail + t] = (uint8_t)(t * 13 + 7);
+}
+
+struct Writer {
+    uint8_t* f;
+    uint32_t len;
+    __device__ void u8(uint32_t at, uint32_t v) const {
+        if (at < len) f[at] = (uint8_t)v;
+    }
+    __device__ void u16(uint32_t at, uint32_t v) const { u8(at, v >> 8); u8(at + 1, v); }
+    __device__ void u32(uint32_t at, uint32_t v) const { u16(at, v >> 16); u16(at + 2, v); }
+    __device__ void rnd(uint32_t at, uint32_t n, Rng& r) const {
+        for (uint32_t k = 0; k < n; k += 4) {
+            const uint32_t v = r.u32();
+            for (uint32_t j = 0; j < 4 && k + j < n; ++j) u8(at + k + j, v >> (24 - 8 * j));
+        }
+    }
+};
+
+__device__ void write_frame(int profile, uint64_t seed, uint64_t i, const Plan& p, uint8_t* f,
+                            uint32_t len) {
+    Rng r(seed, i, 1);
+    Rng fr(seed ^ 0xF10Full, p.flow, 1);  // per-flow tuple (FLOWS)
+    Rng& tuple = p.flow ? fr : r;
+    const Writer w{f, len};
+    const bool adv = profile == INGOT_GEN_ADVERSARIAL;
+    uint32_t o = 0;
+    // Ethernet
+    if (profile == INGOT_GEN_V4UDP64) {
+        for (uint32_t k = 0; k < 6; ++k) w.u8(k, 0x00), w.u8(6 + k, 0xff);
+    } else {
+        w.rnd(0, 12, r);
+    }
+    w.u16(12, p.n_vlan ? p.tpid[0] : p.ethertype);
+    o = 14;
+    for (uint32_t v = 0; v < p.n_vlan; ++v) {
+        w.u16(o, r.u32());  // TCI
+        const uint32_t next = v + 1 < p.n_vlan ? p.tpid[v + 1] : p.ethertype;
+        w.u16(o + 2, next);
+        o += 4;
+    }
+    const uint32_t l3 = o;
+    if (p.ethertype == 0x0800) {
+        if (profile == INGOT_GEN_V4UDP64) {
+            w.u8(o, 0x45); w.u8(o + 1, 0); w.u16(o + 2, 50); w.u32(o + 4, 0);
+            w.u8(o + 8, 0xf0); w.u8(o + 9, 17); w.u16(o + 10, 0);
+            w.u32(o + 12, r.u32()); w.u32(o + 16, r.u32());
+            o += 20;
+            w.u16(o, r.u32()); w.u16(o + 2, r.u32()); w.u16(o + 4, 30); w.u16(o + 6, 0);
+            for (uint32_t k = 0; k < 8; ++k) w.u8(o + 8 + k, k);  // bench body 0..7
+            return;
+        }
+        const uint32_t hl = p.ihl * 4 > 20 ? p.ihl * 4 : 20;
+        w.u8(o, 0x40 | p.ihl);
+        w.u8(o + 1, r.u32());
+        w.u16(o + 2, len > l3 ? len - l3 : 0);
+        w.u16(o + 4, r.u32());
+        w.u16(o + 6, adv ? r.u32() : 0x4000);
+        w.u8(o + 8, r.range(1, 255));
+        w.u8(o + 9, p.proto);
+        w.u16(o + 10, r.u32());
+        w.u32(o + 12, tuple.u32());
+        w.u32(o + 16, tuple.u32());
+        if (hl > 20) w.rnd(o + 20, hl - 20, r);
+        o += hl;
+    } else if (p.ethertype == 0x86dd) {
+        w.u32(o, 0x60000000u | (r.u32() & 0x0fffffffu));
+        w.u16(o + 4, len > l3 + 40 ? len - l3 - 40 : 0);
+        w.u8(o + 6, p.n_eh ? p.eh_type[0] : p.proto);
+        w.u8(o + 7, r.range(1, 255));
+        for (uint32_t k = 0; k < 8; ++k) w.u32(o + 8 + 4 * k, tuple.u32());
+        o += 40;
+        for (uint32_t k = 0; k < p.n_eh; ++k) {
+            const uint32_t nh = k + 1 < p.n_eh ? p.eh_type[k + 1] : p.proto;
+            w.u8(o, nh);
+            if (p.eh_type[k] == 44) {
+                w.u8(o + 1, adv ? r.u32() : 0);
+                w.u16(o + 2, r.u32());
+                w.u32(o + 4, r.u32());
+                o += 8;
+            } else {
+                w.u8(o + 1, p.eh_ext[k]);
+                w.rnd(o + 2, 6 + 8 * p.eh_ext[k], r);
+                o += 8 + 8 * p.eh_ext[k];
+            }
+        }
+    } else {
+        return;  // unknown ethertype: the rest stays pattern
+    }
+    // L4
+    const uint32_t sport = tuple.u32() & 0xffffu, dport = tuple.u32() & 0xffffu;
+    if (p.proto == 6) {
+        const uint32_t hl = p.doff * 4 > 20 ? p.doff * 4 : 20;
+        w.u16(o, sport); w.u16(o + 2, dport);
+        w.u32(o + 4, r.u32()); w.u32(o + 8, r.u32());
+        w.u8(o + 12, (p.doff << 4) | (adv ? (r.u32() & 0xf) : 0));
+        w.u8(o + 13, r.u32());
+        w.u16(o + 14, r.u32()); w.u16(o + 16, r.u32()); w.u16(o + 18, r.u32());
+        if (hl > 20) w.rnd(o + 20, hl - 20, r);
+    } else if (p.proto == 17) {
+        w.u16(o, sport); w.u16(o + 2, dport);
+        w.u16(o + 4, len > o ? len - o : 0);
+        w.u16(o + 6, r.u32());
+    } else {
+        w.rnd(o, 8, r);
+    }
+}
+
+__global__ void k_headers(int profile, uint64_t seed, uint64_t first, uint64_t n,
+                          const uint64_t* off, uint32_t stride, const uint16_t* lens,
+                          uint8_t* arena, uint64_t arena_bytes) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Plan p = plan(profile, seed, first + i);
+    const uint64_t o = off ? off[i] : i * (uint64_t)stride;
+    uint32_t len = lens ? lens[i] : stride;
+    if (o >= arena_bytes) return;
+    if (o + len > arena_bytes) len = (uint32_t)(arena_bytes - o);
+    write_frame(profile, seed, first + i, p, arena + o, len);
+}
+
+int err(hipError_t e) { return e == hipSuccess ? INGOT_GPU_SUCCESS : INGOT_GPU_EHIP; }
+
+}  // namespace
+
+extern "C" int ingot_pktgen_lengths(int profile, uint64_t seed, uint64_t first, uint64_t n,
+                                    uint16_t* d_len, void* stream) {
+    if (n == 0) return INGOT_GPU_SUCCESS;
+    if (!d_len) return INGOT_GPU_EINVAL;
+    const uint32_t grid = (uint32_t)((n + 255) / 256);
+    hipLaunchKernelGGL(k_lengths, dim3(grid), dim3(256), 0, (hipStream_t)stream, profile, seed,
+                       first, n, d_len);
+    return err(hipGetLastError());
+}
+
+extern "C" int ingot_pktgen_fill(int profile, uint64_t seed, uint64_t first, uint64_t n,
+                                 const uint64_t* d_off, uint32_t stride, const uint16_t* d_len,
+                                 uint8_t* d_arena, uint64_t arena_bytes, void* stream) {
+    if (!d_arena || (!d_off && stride == 0) || (d_off && !d_len)) return INGOT_GPU_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    if (((uintptr_t)d_arena & 15u) != 0) return INGOT_GPU_EINVAL;
+    if (arena_bytes) {
+        hipLaunchKernelGGL(k_pattern, dim3(4096), dim3(256), 0, s, profile, seed, d_arena,
+                           arena_bytes);
+        if (hipGetLastError() != hipSuccess) return INGOT_GPU_EHIP;
+    }
+    if (n == 0) return INGOT_GPU_SUCCESS;
+    const uint32_t grid = (uint32_t)((n + 255) / 256);
+    hipLaunchKernelGGL(k_headers, dim3(grid), dim3(256), 0, s, profile, seed, first, n, d_off,
+                       stride, d_len, d_arena, arena_bytes);
+    return err(hipGetLastError());
+}

@@ -1,0 +1,131 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes wrapper of the CPU parse oracle.
+
+A scalar C restatement of ingot's parse path (oracle/ingot_oracle.c), pinned
+by the reference's own known-answer vectors (tests/golden/).  Only tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module; the product path (ingot_amd/) never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+from ingot_amd.abi import FIELDS_DTYPE, REC_DTYPE, Chain  # ABI layouts only
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "build" / "libingot_oracle.so"
+
+_lib = None
+
+
+def build(out_dir: str | os.PathLike | None = None, native: bool = False) -> Path:
+    """Compile the oracle with make.  `native` adds -march=native (used on the
+    GPU box for the CPU baseline); `out_dir` redirects the build."""
+    env = dict(os.environ)
+    args = ["make", "-s", "-C", str(HERE)]
+    target = LIB_PATH
+    if out_dir is not None:
+        args.append(f"OUT={out_dir}")
+        target = Path(out_dir) / "libingot_oracle.so"
+    if native:
+        args.append("ARCH=-march=native")
+    subprocess.run(args, check=True, env=env, capture_output=True)
+    return target
+
+
+def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
+    global _lib
+    if path is None and _lib is not None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        build()
+    lib = ctypes.CDLL(str(p))
+    vp = ctypes.c_void_p
+    lib.oracle_parse_one.argtypes = [vp, ctypes.c_uint32, ctypes.c_int, vp, vp]
+    lib.oracle_parse_one.restype = None
+    lib.oracle_parse_batch.argtypes = [vp, vp, vp, ctypes.c_uint32, ctypes.c_uint64,
+                                       ctypes.c_int, vp, vp, ctypes.c_int]
+    lib.oracle_parse_batch.restype = ctypes.c_int
+    lib.oracle_be_bits.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32]
+    lib.oracle_be_bits.restype = ctypes.c_uint64
+    lib.oracle_v6eh_class.argtypes = [ctypes.c_uint8]
+    lib.oracle_v6eh_class.restype = ctypes.c_int
+    lib.oracle_toeplitz.argtypes = [vp, ctypes.c_uint32, vp, ctypes.c_uint32]
+    lib.oracle_toeplitz.restype = ctypes.c_uint32
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def parse_one(frame: bytes, chain: Chain):
+    """-> (ingot_rec, ingot_fields) as numpy structured scalars."""
+    lib = load()
+    buf = np.frombuffer(bytes(frame) + b"\0" * 8, dtype=np.uint8).copy()
+    rec = np.zeros(1, dtype=REC_DTYPE)
+    fld = np.zeros(1, dtype=FIELDS_DTYPE)
+    lib.oracle_parse_one(_p(buf), len(frame), int(chain), _p(rec), _p(fld))
+    return rec[0], fld[0]
+
+
+def parse_batch(arena: np.ndarray, off: np.ndarray | None, lens: np.ndarray | None,
+                chain: Chain, stride: int = 0, n: int | None = None, fields: bool = False,
+                nthreads: int = 1, lib: ctypes.CDLL | None = None):
+    lib = lib or load()
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    if off is not None:
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        n = len(off) if n is None else n
+    if lens is not None:
+        lens = np.ascontiguousarray(lens, dtype=np.uint16)
+    if n is None:
+        raise ValueError("n is required for the strided layout")
+    rec = np.zeros(n, dtype=REC_DTYPE)
+    fld = np.zeros(n, dtype=FIELDS_DTYPE) if fields else None
+    rc = lib.oracle_parse_batch(_p(arena), _p(off), _p(lens), stride, n, int(chain), _p(rec),
+                                _p(fld), nthreads)
+    if rc != 0:
+        raise ValueError("oracle_parse_batch: bad arguments")
+    return (rec, fld) if fields else rec
+
+
+def be_bits(hdr: bytes, first_bit: int, n_bits: int) -> int:
+    buf = np.frombuffer(bytes(hdr) + b"\0" * 16, dtype=np.uint8).copy()
+    return int(load().oracle_be_bits(_p(buf), first_bit, n_bits))
+
+
+def v6eh_class(proto: int) -> int:
+    return int(load().oracle_v6eh_class(proto))
+
+
+def toeplitz(key: bytes, data: bytes) -> int:
+    k = np.frombuffer(bytes(key), dtype=np.uint8).copy()
+    d = np.frombuffer(bytes(data) + b"\0", dtype=np.uint8).copy()
+    return int(load().oracle_toeplitz(_p(k), len(key), _p(d), len(data)))
+
+
+HEADER_KINDS = {"ethernet": 0, "vlan": 1, "ipv4": 2, "ipv6": 3, "tcp": 4, "udp": 5, "icmp": 6,
+                "repeated_udp": 7}
+
+
+def parse_header(kind: str, data: bytes):
+    """Single-header `ValidX::parse`: -> (status, used, hint or None)."""
+    lib = load()
+    lib.oracle_parse_header.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32,
+                                        ctypes.POINTER(ctypes.c_uint32),
+                                        ctypes.POINTER(ctypes.c_uint32)]
+    lib.oracle_parse_header.restype = ctypes.c_int
+    buf = np.frombuffer(bytes(data) + b"\0" * 8, dtype=np.uint8).copy()
+    used, hint = ctypes.c_uint32(0), ctypes.c_uint32(0)
+    st = lib.oracle_parse_header(HEADER_KINDS[kind], _p(buf), len(data), ctypes.byref(used),
+                                 ctypes.byref(hint))
+    h = None if hint.value == 0xFFFFFFFF else hint.value
+    return st, used.value, h

@@ -1,0 +1,603 @@
+/*
+ * ingot_oracle.c — TEST INFRASTRUCTURE ONLY (parity checker + CPU baseline).
+ *
+ * Scalar CPU restatement of ingot's single-slice parse path.  Each function
+ * cites the reference file:line whose behaviour it restates; paths are
+ * relative to the reference checkout (oxidecomputer/ingot @ 2025-08-08).
+ * Nothing here is shipped: the product path (ingot_amd/, include/) never
+ * links this file, and bench.py times it only as the "port" CPU baseline.
+ *
+ * Parity pinning: tests/golden/kats.json holds the reference's own
+ * known-answer vectors (ingot/src/tests.rs, ingot-examples/src/tests.rs,
+ * ingot-examples/benches/packet.rs) and tests/test_oracle_golden.py checks
+ * this file against every one of them.
+ */
+#include "ingot_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ParseError discriminants + 1 (ingot-types/src/error.rs:22-44). */
+enum {
+    PE_OK = INGOT_OK,
+    PE_UNWANTED = INGOT_ERR_UNWANTED,
+    PE_NEEDS_HINT = INGOT_ERR_NEEDS_HINT,
+    PE_TOO_SMALL = INGOT_ERR_TOO_SMALL,
+    PE_CANNOT_ACCEPT = INGOT_ERR_CANNOT_ACCEPT
+};
+
+/* Ethertype constants (ingot/src/ethernet.rs:12-20). */
+#define ET_IPV4 0x0800u
+#define ET_ARP 0x0806u
+#define ET_VLAN 0x8100u
+#define ET_IPV6 0x86ddu
+#define ET_QINQ 0x9100u
+
+/* IpProtocol constants (ingot/src/ip.rs:20-38). */
+#define IPP_ICMP 1u
+#define IPP_TCP 6u
+#define IPP_UDP 17u
+#define IPP_ICMP_V6 58u
+
+/* ------------------------------------------------------------------------
+ * Field layout tables — a restatement of the ingot-macros layout rules
+ * (packet/mod.rs:547-821): fields in declaration order, packed, widths from
+ * the declared primitive (u4, u13be, u16be, [u8; 6] ...).  (bit offset, bits)
+ * ---------------------------------------------------------------------- */
+/* Ethernet (ethernet.rs:46-55): destination [u8;6], source [u8;6], ethertype u16be */
+#define ETH_LEN 14u
+/* VlanBody (ethernet.rs:57-65): priority u3, dei u1, vid u12be, ethertype u16be */
+#define VLAN_LEN 4u
+#define VLAN_PRIORITY 0, 3
+#define VLAN_DEI 3, 1
+#define VLAN_VID 4, 12
+#define VLAN_ETHERTYPE 16, 16
+/* Ipv4 (ip.rs:63-93) */
+#define V4_LEN 20u
+#define V4_VERSION 0, 4
+#define V4_IHL 4, 4
+#define V4_DSCP 8, 6
+#define V4_ECN 14, 2
+#define V4_TOTAL_LEN 16, 16
+#define V4_IDENT 32, 16
+#define V4_FLAGS 48, 3
+#define V4_FRAG_OFF 51, 13
+#define V4_HOP_LIMIT 64, 8
+#define V4_PROTOCOL 72, 8
+#define V4_CHECKSUM 80, 16
+/* Ipv6 (ip.rs:159-182) */
+#define V6_LEN 40u
+#define V6_VERSION 0, 4
+#define V6_DSCP 4, 6
+#define V6_ECN 10, 2
+#define V6_FLOW 12, 20
+#define V6_PAYLOAD_LEN 32, 16
+#define V6_NEXT_HEADER 48, 8
+#define V6_HOP_LIMIT 56, 8
+/* IpV6ExtFragment (ip.rs:190-200): next_header u8, reserved u8,
+ * fragment_offset u13be, res u2, more_frags u1, ident u32be */
+#define FRAG_LEN 8u
+#define FRAG_OFFSET 16, 13
+#define FRAG_RES 29, 2
+#define FRAG_MORE 31, 1
+#define FRAG_IDENT 32, 32
+/* IpV6Ext6564 (ip.rs:202-211): next_header u8, ext_len u8, data var_len */
+#define EH6564_FIXED 2u
+/* Tcp (tcp.rs:9-30) */
+#define TCP_LEN 20u
+#define TCP_DATA_OFFSET 96, 4
+#define TCP_RESERVED 100, 4
+/* Udp (udp.rs:8-15), IcmpV4/IcmpV6 (icmp.rs:42-50, 114-122) */
+#define UDP_LEN 8u
+#define ICMP_LEN 8u
+
+uint64_t oracle_be_bits(const uint8_t* hdr, uint32_t first_bit, uint32_t n_bits) {
+    /* bitfield.rs:40-186: the covering bytes, read as a big-endian integer,
+     * shifted right by the bits after the field's end in its last byte and
+     * masked to n_bits. */
+    uint32_t fb = first_bit / 8u;
+    uint32_t lb = (first_bit + n_bits + 7u) / 8u;
+    unsigned __int128 acc = 0;
+    for (uint32_t b = fb; b < lb; ++b) acc = (acc << 8) | hdr[b];
+    uint32_t right = (8u - ((first_bit + n_bits) % 8u)) % 8u;
+    acc >>= right;
+    uint64_t mask = (n_bits >= 64) ? ~(uint64_t)0 : (((uint64_t)1 << n_bits) - 1u);
+    return (uint64_t)acc & mask;
+}
+
+#define BITS(h, spec) ((uint32_t)oracle_be_bits((h), spec))
+
+static uint32_t be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
+
+/* Ecn::from_network (ip.rs:111-119): 3 maps to Capable0. */
+static uint8_t ecn_from_network(uint32_t raw) { return (uint8_t)(raw == 3 ? 1 : raw); }
+
+int oracle_v6eh_class(uint8_t proto) {
+    /* IpProtocol::class (ip.rs:40-54) */
+    switch (proto) {
+    case 44:
+        return INGOT_EH_FRAGMENT;
+    case 0: case 43: case 60: case 135: case 139: case 140: case 253: case 254:
+        return INGOT_EH_RFC6564;
+    default:
+        return 0;
+    }
+}
+
+/* ------------------------------------------------------------------------
+ * Per-header parse bodies: the generated `HeaderParse::parse_choice`
+ * (packet/mod.rs:1831-2005).  Each fixed chunk is an
+ * `Accessor::read_from_prefix` (accessor.rs:30-67: len >= size else TooSmall);
+ * each var_len chunk is `from.split_at(chunk_len)` else TooSmall
+ * (mod.rs:1867-1875).  `n` = bytes left in the slice.
+ * ---------------------------------------------------------------------- */
+static int parse_eth(const uint8_t* s, uint32_t n, uint32_t* used, uint32_t* hint) {
+    if (n < ETH_LEN) return PE_TOO_SMALL;
+    *used = ETH_LEN;
+    *hint = be16(s + 12); /* next_layer ethertype (ethernet.rs:53) */
+    return PE_OK;
+}
+
+static int parse_vlan(const uint8_t* s, uint32_t n, uint32_t* used, uint32_t* hint) {
+    if (n < VLAN_LEN) return PE_TOO_SMALL;
+    *used = VLAN_LEN;
+    *hint = be16(s + 2); /* next_layer ethertype (ethernet.rs:63) */
+    return PE_OK;
+}
+
+static int parse_ipv4(const uint8_t* s, uint32_t n, uint32_t* used, uint32_t* hint) {
+    if (n < V4_LEN) return PE_TOO_SMALL;
+    uint32_t ihl = BITS(s, V4_IHL);
+    uint32_t opt = ihl * 4 > 20 ? ihl * 4 - 20 : 0; /* saturating_sub, ip.rs:91 */
+    if (n - V4_LEN < opt) return PE_TOO_SMALL;
+    *used = V4_LEN + opt;
+    *hint = s[9]; /* next_layer protocol (ip.rs:80-81) */
+    return PE_OK;
+}
+
+/* LowRentV6Eh::parse_choice (ip.rs:184-188; choice.rs:193-246 with
+ * map_on = IpProtocol::class). */
+static int parse_v6eh(const uint8_t* s, uint32_t n, uint32_t hint, uint32_t* used,
+                      uint32_t* hint_out, int* kind) {
+    int c = oracle_v6eh_class((uint8_t)hint);
+    *kind = c;
+    if (c == 0) return PE_UNWANTED;
+    if (c == INGOT_EH_FRAGMENT) {
+        if (n < FRAG_LEN) return PE_TOO_SMALL;
+        *used = FRAG_LEN;
+    } else {
+        if (n < EH6564_FIXED) return PE_TOO_SMALL;
+        uint32_t data = 6u + (uint32_t)s[1] * 8u; /* ip.rs:209 */
+        if (n - EH6564_FIXED < data) return PE_TOO_SMALL;
+        *used = EH6564_FIXED + data;
+    }
+    *hint_out = s[0];
+    return PE_OK;
+}
+
+static void fill_eh(ingot_v6eh* e, const uint8_t* s, int kind, uint32_t off) {
+    memset(e, 0, sizeof *e);
+    e->kind = (uint8_t)kind;
+    e->off = (uint16_t)off;
+    e->next_header = s[0];
+    e->ext_len = s[1];
+    if (kind == INGOT_EH_FRAGMENT) {
+        e->frag_offset = (uint16_t)BITS(s, FRAG_OFFSET);
+        e->frag_res_more = (uint8_t)((BITS(s, FRAG_RES) << 1) | BITS(s, FRAG_MORE));
+        e->ident = BITS(s, FRAG_IDENT);
+    }
+}
+
+/* Ipv6 body: 40-B chunk, then the `subparse(on_next_layer)` Repeated<LowRentV6Eh>
+ * over the rest of the slice (mod.rs:1933-1975) = RepeatedView::parse_choice
+ * (util.rs:189-228): loop while bytes remain; Unwanted ends the chain, any
+ * other error is the header's error; the last EH's next_header is the hint. */
+static int parse_ipv6(const uint8_t* s, uint32_t n, uint32_t frame_off, uint32_t* used,
+                      uint32_t* hint, uint32_t* n_eh, ingot_fields* F) {
+    if (n < V6_LEN) return PE_TOO_SMALL;
+    uint32_t h = s[6];
+    const uint8_t* rest = s + V6_LEN;
+    uint32_t rn = n - V6_LEN;
+    uint32_t read = 0;
+    while (read < rn) {
+        uint32_t u = 0, h2 = 0;
+        int kind = 0;
+        int r = parse_v6eh(rest + read, rn - read, h, &u, &h2, &kind);
+        if (r == PE_UNWANTED) break;
+        if (r != PE_OK) return r;
+        if (F && *n_eh < INGOT_MAX_EH_FIELDS)
+            fill_eh(&F->v6_eh[*n_eh], rest + read, kind, frame_off + V6_LEN + read);
+        *n_eh += 1;
+        read += u;
+        h = h2;
+    }
+    *used = V6_LEN + read;
+    *hint = h;
+    return PE_OK;
+}
+
+static int parse_tcp(const uint8_t* s, uint32_t n, uint32_t* used) {
+    if (n < TCP_LEN) return PE_TOO_SMALL;
+    uint32_t doff = BITS(s, TCP_DATA_OFFSET);
+    uint32_t opt = doff * 4 > 20 ? doff * 4 - 20 : 0; /* tcp.rs:28 */
+    if (n - TCP_LEN < opt) return PE_TOO_SMALL;
+    *used = TCP_LEN + opt;
+    return PE_OK;
+}
+
+static int parse_fixed(uint32_t n, uint32_t size, uint32_t* used) {
+    if (n < size) return PE_TOO_SMALL;
+    *used = size;
+    return PE_OK;
+}
+
+/* ------------------------------------------------------------------------
+ * Getter materialisation (generated XRef getters, packet/mod.rs:1183-1479).
+ * ---------------------------------------------------------------------- */
+static void fields_eth(ingot_fields* F, const uint8_t* s) {
+    memcpy(F->eth_destination, s, 6);
+    memcpy(F->eth_source, s + 6, 6);
+    F->eth_ethertype = (uint16_t)be16(s + 12);
+}
+
+static void fields_vlan(ingot_fields* F, int i, const uint8_t* s) {
+    F->vlan_priority[i] = (uint8_t)BITS(s, VLAN_PRIORITY);
+    F->vlan_dei[i] = (uint8_t)BITS(s, VLAN_DEI);
+    F->vlan_vid[i] = (uint16_t)BITS(s, VLAN_VID);
+    F->vlan_ethertype[i] = (uint16_t)BITS(s, VLAN_ETHERTYPE);
+}
+
+static void fields_ipv4(ingot_fields* F, const uint8_t* s, uint32_t off, uint32_t used) {
+    F->v4_version = (uint8_t)BITS(s, V4_VERSION);
+    F->v4_ihl = (uint8_t)BITS(s, V4_IHL);
+    F->v4_dscp = (uint8_t)BITS(s, V4_DSCP);
+    F->v4_ecn_raw = (uint8_t)BITS(s, V4_ECN);
+    F->v4_ecn = ecn_from_network(F->v4_ecn_raw);
+    F->v4_total_len = (uint16_t)BITS(s, V4_TOTAL_LEN);
+    F->v4_identification = (uint16_t)BITS(s, V4_IDENT);
+    F->v4_flags = (uint8_t)BITS(s, V4_FLAGS); /* from_bits_truncate keeps all 3 */
+    F->v4_fragment_offset = (uint16_t)BITS(s, V4_FRAG_OFF);
+    F->v4_hop_limit = (uint8_t)BITS(s, V4_HOP_LIMIT);
+    F->v4_protocol = (uint8_t)BITS(s, V4_PROTOCOL);
+    F->v4_checksum = (uint16_t)BITS(s, V4_CHECKSUM);
+    memcpy(F->v4_source, s + 12, 4);
+    memcpy(F->v4_destination, s + 16, 4);
+    F->v4_options_off = (uint16_t)(off + V4_LEN);
+    F->v4_options_len = (uint16_t)(used - V4_LEN);
+}
+
+static void fields_ipv6(ingot_fields* F, const uint8_t* s, uint32_t off, uint32_t used) {
+    F->v6_version = (uint8_t)BITS(s, V6_VERSION);
+    F->v6_dscp = (uint8_t)BITS(s, V6_DSCP);
+    F->v6_ecn_raw = (uint8_t)BITS(s, V6_ECN);
+    F->v6_ecn = ecn_from_network(F->v6_ecn_raw);
+    F->v6_flow_label = BITS(s, V6_FLOW);
+    F->v6_payload_len = (uint16_t)BITS(s, V6_PAYLOAD_LEN);
+    F->v6_next_header = (uint8_t)BITS(s, V6_NEXT_HEADER);
+    F->v6_hop_limit = (uint8_t)BITS(s, V6_HOP_LIMIT);
+    memcpy(F->v6_source, s + 8, 16);
+    memcpy(F->v6_destination, s + 24, 16);
+    F->v6_ext_off = (uint16_t)(off + V6_LEN);
+    F->v6_ext_len = (uint16_t)(used - V6_LEN);
+}
+
+static void fields_tcp(ingot_fields* F, const uint8_t* s, uint32_t off, uint32_t used) {
+    F->l4_source = (uint16_t)be16(s);
+    F->l4_destination = (uint16_t)be16(s + 2);
+    F->tcp_sequence = (uint32_t)oracle_be_bits(s, 32, 32);
+    F->tcp_acknowledgement = (uint32_t)oracle_be_bits(s, 64, 32);
+    F->tcp_data_offset = (uint8_t)BITS(s, TCP_DATA_OFFSET);
+    F->tcp_reserved = (uint8_t)BITS(s, TCP_RESERVED);
+    F->tcp_flags = s[13];
+    F->tcp_window_size = (uint16_t)be16(s + 14);
+    F->tcp_checksum = (uint16_t)be16(s + 16);
+    F->tcp_urgent_ptr = (uint16_t)be16(s + 18);
+    F->tcp_options_off = (uint16_t)(off + TCP_LEN);
+    F->tcp_options_len = (uint16_t)(used - TCP_LEN);
+}
+
+static void fields_udp(ingot_fields* F, const uint8_t* s) {
+    F->l4_source = (uint16_t)be16(s);
+    F->l4_destination = (uint16_t)be16(s + 2);
+    F->udp_length = (uint16_t)be16(s + 4);
+    F->udp_checksum = (uint16_t)be16(s + 6);
+}
+
+static void fields_icmp(ingot_fields* F, const uint8_t* s) {
+    F->icmp_ty = s[0];
+    F->icmp_code = s[1];
+    F->icmp_checksum = (uint16_t)be16(s + 2);
+    memcpy(F->icmp_rest_of_hdr, s + 4, 4);
+}
+
+/* ------------------------------------------------------------------------
+ * Chain driver: generated `parse_slice` (parse.rs:496-509) running the layer
+ * fragments (parse.rs:292-416): layer 0 via parse, later layers via
+ * parse_choice(slice, prev_hint), errors tagged with the layer label,
+ * `from=` conversion after the parse (parse.rs:196-200), control fn after
+ * the layer (parse.rs:229-254), Option<> layers skipped once accepted.
+ * ---------------------------------------------------------------------- */
+typedef struct {
+    const uint8_t* f;
+    uint32_t len;
+    uint32_t p; /* bytes consumed */
+    ingot_rec* r;
+    ingot_fields* F;
+} walk_t;
+
+static void fail(walk_t* w, int layer, int code) {
+    w->r->status = (uint8_t)code;
+    w->r->err_layer = (uint8_t)layer;
+}
+
+/* L3 choice (ingot-examples/src/choices.rs:17-21; choice.rs:231-246). */
+static int layer_l3(walk_t* w, int layer, uint32_t et, uint32_t* proto) {
+    ingot_rec* r = w->r;
+    const uint8_t* s = w->f + w->p;
+    uint32_t n = w->len - w->p, used = 0, n_eh = 0;
+    int e;
+    if (et == ET_IPV4) {
+        r->l3_kind = INGOT_L3_IPV4;
+        r->l3_off = (uint16_t)w->p;
+        e = parse_ipv4(s, n, &used, proto);
+        if (e == PE_OK && w->F) fields_ipv4(w->F, s, w->p, used);
+    } else if (et == ET_IPV6) {
+        r->l3_kind = INGOT_L3_IPV6;
+        r->l3_off = (uint16_t)w->p;
+        e = parse_ipv6(s, n, w->p, &used, proto, &n_eh, w->F);
+        r->n_v6ext = (uint8_t)(n_eh > 255 ? 255 : n_eh);
+        if (w->F) {
+            if (e == PE_OK) fields_ipv6(w->F, s, w->p, used);
+            else memset(w->F->v6_eh, 0, sizeof w->F->v6_eh);
+        }
+    } else {
+        e = PE_UNWANTED;
+    }
+    if (e != PE_OK) {
+        fail(w, layer, e);
+        return e;
+    }
+    w->p += used;
+    r->payload_off = (uint16_t)w->p;
+    r->l4_proto = (uint8_t)*proto;
+    return PE_OK;
+}
+
+/* L4 choice (choices.rs:25-29) when ulp == 0, Ulp (choices.rs:32-38) when 1;
+ * udp_only applies UdpParser's `from = "L4<Q>"` conversion to UdpPacket. */
+static int layer_l4(walk_t* w, int layer, uint32_t proto, int ulp, int udp_only) {
+    ingot_rec* r = w->r;
+    const uint8_t* s = w->f + w->p;
+    uint32_t n = w->len - w->p, used = 0;
+    int e, kind;
+    if (proto == IPP_TCP) {
+        kind = INGOT_L4_TCP;
+    } else if (proto == IPP_UDP) {
+        kind = INGOT_L4_UDP;
+    } else if (ulp && proto == IPP_ICMP) {
+        kind = INGOT_L4_ICMPV4;
+    } else if (ulp && proto == IPP_ICMP_V6) {
+        kind = INGOT_L4_ICMPV6;
+    } else {
+        fail(w, layer, PE_UNWANTED);
+        return PE_UNWANTED;
+    }
+    r->l4_kind = (uint8_t)kind;
+    r->l4_off = (uint16_t)w->p;
+    if (kind == INGOT_L4_TCP) {
+        e = parse_tcp(s, n, &used);
+        if (e == PE_OK && w->F) fields_tcp(w->F, s, w->p, used);
+    } else if (kind == INGOT_L4_UDP) {
+        e = parse_fixed(n, UDP_LEN, &used);
+        if (e == PE_OK && w->F) fields_udp(w->F, s);
+    } else {
+        e = parse_fixed(n, ICMP_LEN, &used);
+        if (e == PE_OK && w->F) fields_icmp(w->F, s);
+    }
+    if (e != PE_OK) {
+        fail(w, layer, e);
+        return e;
+    }
+    w->p += used;
+    r->payload_off = (uint16_t)w->p;
+    if (udp_only && kind != INGOT_L4_UDP) {
+        /* TryFrom<ValidL4> for ValidUdp: wrong variant -> Unwanted
+         * (choice.rs:153-187), reported at the l4 label. */
+        fail(w, layer, PE_UNWANTED);
+        return PE_UNWANTED;
+    }
+    return PE_OK;
+}
+
+static int layer_eth(walk_t* w, uint32_t* et) {
+    uint32_t used = 0;
+    int e = parse_eth(w->f, w->len, &used, et);
+    if (e != PE_OK) {
+        fail(w, 0, e);
+        return e;
+    }
+    if (w->F) fields_eth(w->F, w->f);
+    w->p = used;
+    w->r->payload_off = (uint16_t)used;
+    w->r->ethertype = (uint16_t)*et;
+    return PE_OK;
+}
+
+void oracle_parse_one(const uint8_t* frame, uint32_t len, int chain, ingot_rec* rec,
+                      ingot_fields* fields) {
+    memset(rec, 0, sizeof *rec);
+    if (fields) memset(fields, 0, sizeof *fields);
+    walk_t w = {frame, len, 0, rec, fields};
+    uint32_t et = 0, proto = 0;
+    rec->err_layer = 0xff;
+
+    if (layer_eth(&w, &et) != PE_OK) goto out;
+
+    switch (chain) {
+    case INGOT_CHAIN_UDP_PARSER:
+        /* UdpParser { eth, l3: L3, #[ingot(from = "L4<Q>")] l4: UdpPacket }
+         * (ingot-examples/src/packets.rs:18-24) */
+        if (layer_l3(&w, 1, et, &proto) != PE_OK) goto out;
+        layer_l4(&w, 2, proto, 0, 1);
+        break;
+    case INGOT_CHAIN_GENERIC_ULP:
+        /* GenericUlp { #[ingot(control = exit_on_arp)] inner_eth,
+         *              inner_l3: Option<L3>, inner_ulp: Option<Ulp> }
+         * (packets.rs:45-60).  The trailing Option<> sled makes
+         * accept_allowed_from = 0 (parse.rs:144-156), so Accept on the eth
+         * layer is allowed and skips both optional layers. */
+        if (et == ET_ARP) {
+            rec->flags |= INGOT_REC_ACCEPTED;
+            break;
+        }
+        if (layer_l3(&w, 1, et, &proto) != PE_OK) goto out;
+        layer_l4(&w, 2, proto, 1, 0);
+        break;
+    case INGOT_CHAIN_VLAN_ULP:
+        /* Build-defined chain (no reference chain uses VlanBody). */
+        while ((et == ET_VLAN || et == ET_QINQ) && rec->n_vlan < 2) {
+            uint32_t used = 0;
+            const uint8_t* s = frame + w.p;
+            if (parse_vlan(s, len - w.p, &used, &et) != PE_OK) {
+                fail(&w, 1, PE_TOO_SMALL);
+                goto out;
+            }
+            if (fields) fields_vlan(fields, rec->n_vlan, s);
+            rec->n_vlan++;
+            w.p += used;
+            rec->payload_off = (uint16_t)w.p;
+            rec->ethertype = (uint16_t)et;
+        }
+        if (layer_l3(&w, 2, et, &proto) != PE_OK) goto out;
+        layer_l4(&w, 3, proto, 1, 0);
+        break;
+    default:
+        fail(&w, 0, PE_UNWANTED);
+        break;
+    }
+out:
+    if (rec->status == PE_OK) rec->err_layer = 0xff;
+    if (fields) fields->rec = *rec;
+}
+
+/* ------------------------------------------------------------------------
+ * Batch driver (pthreads, static contiguous partition).
+ * ---------------------------------------------------------------------- */
+typedef struct {
+    const uint8_t* arena;
+    const uint64_t* off;
+    const uint16_t* len;
+    uint32_t stride;
+    uint64_t lo, hi;
+    int chain;
+    ingot_rec* rec;
+    ingot_fields* fields;
+} job_t;
+
+static void* run_job(void* arg) {
+    job_t* j = (job_t*)arg;
+    for (uint64_t i = j->lo; i < j->hi; ++i) {
+        uint64_t o = j->off ? j->off[i] : i * (uint64_t)j->stride;
+        uint32_t l = j->len ? j->len[i] : j->stride;
+        oracle_parse_one(j->arena + o, l, j->chain, &j->rec[i], j->fields ? &j->fields[i] : 0);
+    }
+    return 0;
+}
+
+int oracle_parse_batch(const uint8_t* arena, const uint64_t* off, const uint16_t* len,
+                       uint32_t stride, uint64_t n, int chain, ingot_rec* rec,
+                       ingot_fields* fields, int nthreads) {
+    if ((!arena && n) || (!rec && n) || chain < 0 || chain >= INGOT_CHAIN_COUNT) return -1;
+    if (!off && stride == 0 && n) return -1;
+    if (nthreads < 1) nthreads = 1;
+    if ((uint64_t)nthreads > n) nthreads = n ? (int)n : 1;
+    job_t* jobs = (job_t*)calloc((size_t)nthreads, sizeof(job_t));
+    pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+    if (!jobs || !th) {
+        free(jobs);
+        free(th);
+        return -1;
+    }
+    uint64_t per = (n + (uint64_t)nthreads - 1) / (uint64_t)nthreads;
+    for (int t = 0; t < nthreads; ++t) {
+        uint64_t lo = per * (uint64_t)t, hi = lo + per;
+        if (lo > n) lo = n;
+        if (hi > n) hi = n;
+        job_t j = {arena, off, len, stride, lo, hi, chain, rec, fields};
+        jobs[t] = j;
+    }
+    int started = 0;
+    for (int t = 1; t < nthreads; ++t) {
+        if (pthread_create(&th[t], 0, run_job, &jobs[t]) != 0) break;
+        started = t;
+    }
+    run_job(&jobs[0]);
+    for (int t = 1; t <= started; ++t) pthread_join(th[t], 0);
+    /* any job whose thread failed to start runs here */
+    for (int t = started + 1; t < nthreads; ++t) run_job(&jobs[t]);
+    free(jobs);
+    free(th);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------
+ * Toeplitz hash (Microsoft RSS definition): for every set bit of the input,
+ * MSB first, XOR in the 32-bit window of the key starting at that bit.
+ * ---------------------------------------------------------------------- */
+uint32_t oracle_toeplitz(const uint8_t* key, uint32_t key_len, const uint8_t* data,
+                         uint32_t n) {
+    uint32_t result = 0;
+    if (key_len < n + 4) return 0;
+    uint64_t window = ((uint64_t)key[0] << 24) | ((uint64_t)key[1] << 16) |
+                      ((uint64_t)key[2] << 8) | key[3];
+    for (uint32_t i = 0; i < n; ++i) {
+        uint8_t next = key[i + 4];
+        for (int b = 7; b >= 0; --b) {
+            if (data[i] & (1u << b)) result ^= (uint32_t)(window >> 0);
+            window = ((window << 1) | ((next >> b) & 1u)) & 0xffffffffu;
+        }
+    }
+    return result;
+}
+
+/* ------------------------------------------------------------------------
+ * Header-level entry (single `ValidX::parse`), for the reference's
+ * header-level known-answer tests.  kind: 0 Ethernet, 1 VlanBody, 2 Ipv4,
+ * 3 Ipv6, 4 Tcp, 5 Udp, 6 IcmpV4/V6, 7 RepeatedView<Udp> (util.rs:189-228
+ * over a fixed 8-B header with a unit hint).  Returns the status; *used and
+ * *hint_out (0xffffffff = None) on Ok.
+ * ---------------------------------------------------------------------- */
+int oracle_parse_header(int kind, const uint8_t* s, uint32_t n, uint32_t* used,
+                        uint32_t* hint_out) {
+    uint32_t u = 0, h = 0xffffffffu, n_eh = 0;
+    int e;
+    switch (kind) {
+    case 0: e = parse_eth(s, n, &u, &h); break;
+    case 1: e = parse_vlan(s, n, &u, &h); break;
+    case 2: e = parse_ipv4(s, n, &u, &h); break;
+    case 3: e = parse_ipv6(s, n, 0, &u, &h, &n_eh, 0); break;
+    case 4: e = parse_tcp(s, n, &u); break;
+    case 5: e = parse_fixed(n, UDP_LEN, &u); break;
+    case 6: e = parse_fixed(n, ICMP_LEN, &u); break;
+    case 7: {
+        uint32_t read = 0;
+        e = PE_OK;
+        while (read < n) {
+            uint32_t uu = 0;
+            int r = parse_fixed(n - read, UDP_LEN, &uu);
+            if (r == PE_UNWANTED) break;
+            if (r != PE_OK) { e = r; break; }
+            read += uu;
+        }
+        u = read;
+        break;
+    }
+    default: return PE_UNWANTED;
+    }
+    if (e == PE_OK) {
+        *used = u;
+        *hint_out = h;
+    }
+    return e;
+}

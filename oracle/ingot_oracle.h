@@ -1,0 +1,60 @@
+/*
+ * ingot_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * A scalar CPU restatement of ingot's single-slice parse path, used as the
+ * parity checker for the HIP kernels and as the CPU baseline in bench.py.
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load it; the product library (ingot_amd/) never links or calls it.
+ *
+ * The reference (Rust, toolchain 1.81.0) cannot be built or run here: there is
+ * no cargo/rustc in this image.  This restatement is pinned by
+ * the reference's own known-answer tests, transcribed as fixtures under
+ * tests/golden/ (see tests/golden/make_golden.py).
+ *
+ * Records and field blocks use the product ABI layouts (include/ingot_gpu.h)
+ * so results can be compared byte-for-byte.
+ */
+#ifndef INGOT_ORACLE_H
+#define INGOT_ORACLE_H
+
+#include <stdint.h>
+#include "../include/ingot_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Parse one frame as `chain`; fills *rec (required) and *fields (optional). */
+void oracle_parse_one(const uint8_t* frame, uint32_t len, int chain,
+                      ingot_rec* rec, ingot_fields* fields);
+
+/* Batch form.  off == NULL selects the strided layout (frame i at i*stride);
+ * len == NULL means every frame is `stride` bytes long.  fields may be NULL.
+ * nthreads <= 1 runs on the calling thread; otherwise a static contiguous
+ * partition over nthreads pthreads.  Returns 0, or -1 on bad arguments. */
+int oracle_parse_batch(const uint8_t* arena, const uint64_t* off,
+                       const uint16_t* len, uint32_t stride, uint64_t n,
+                       int chain, ingot_rec* rec, ingot_fields* fields,
+                       int nthreads);
+
+/* Generic big-endian bitfield getter (ingot-macros/src/packet/bitfield.rs
+ * BE get paths): the n_bits (<= 64) starting at bit first_bit, MSB first. */
+uint64_t oracle_be_bits(const uint8_t* hdr, uint32_t first_bit, uint32_t n_bits);
+
+/* IpProtocol::class (ingot/src/ip.rs:40-54): 0 = None, 1 = FragmentHeader,
+ * 2 = Rfc6564. */
+int oracle_v6eh_class(uint8_t proto);
+
+/* Header-level parse (ValidX::parse); see ingot_oracle.c. */
+int oracle_parse_header(int kind, const uint8_t* s, uint32_t n, uint32_t* used,
+                        uint32_t* hint_out);
+
+/* Toeplitz (RSS) hash of `n` input bytes with a key of >= n+4 bytes. */
+uint32_t oracle_toeplitz(const uint8_t* key, uint32_t key_len,
+                         const uint8_t* data, uint32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

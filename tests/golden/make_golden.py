@@ -1,0 +1,347 @@
+"""Write tests/golden/kats.json — the reference's known-answer vectors as data.
+
+Every frame below is transcribed byte-for-byte from a test or bench of
+oxidecomputer/ingot @ 2025-08-08 (file:line given per vector), and every
+expected value is one the reference asserts there (or, marked "by
+construction", a value the reference's frame literally carries, e.g. the
+bench frames that it only `unwrap()`s).  "derived" vectors wrap a reference
+header-level vector in the minimal chain prefix/suffix needed to run it
+through a chain parser; their expected values follow from the same asserts.
+
+The reference is Rust and cannot run here (no cargo/rustc), so these
+fixtures are what pins the CPU oracle (tests/test_oracle_golden.py) and,
+through it, the GPU path.
+
+    python tests/golden/make_golden.py   # rewrites kats.json
+"""
+from __future__ import annotations
+
+import json
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+
+BROADCAST = [0xFF] * 6
+MAC_ABCDEF = [0x0A, 0x0B, 0x0C, 0x0D, 0x0E, 0x0F]
+
+
+def hexs(b) -> str:
+    return bytes(b).hex()
+
+
+# ---------------------------------------------------------------------------
+# Frames transcribed from the reference
+# ---------------------------------------------------------------------------
+
+# ingot-examples/benches/packet.rs:15-34  (pkt_body_v4, 50 B)
+PKT_BODY_V4 = (
+    [0x00] * 6 + [0xFF] * 6 + [0x08, 0x00]
+    + [0x45, 0x00, 0x00, 28 + 8, 0x00, 0x00, 0x00, 0x00, 0xF0, 0x11, 0x00, 0x00,
+       192, 168, 0, 1, 192, 168, 0, 255]
+    + [0x00, 0x80, 0x17, 0xC1, 0x00, 0x08, 0x00, 0x00]
+    + [0x00, 0x01, 0x02, 0x03, 0x04, 0x05, 0x06, 0x07]
+)
+# ingot-examples/benches/packet.rs:36-57  (pkt_body_v6, 70 B)
+PKT_BODY_V6 = (
+    [0x00] * 6 + [0xFF] * 6 + [0x86, 0xDD]
+    + [0x60, 0x00, 0x00, 0x00, 0x00, 0x10, 0x11, 0xF0]
+    + [0x00] * 15 + [0x01] + [0x00] * 15 + [0x01]
+    + [0x00, 0x80, 0x17, 0xC1, 0x00, 0x08, 0x00, 0x00]
+    + [0x00, 0x01, 0x02, 0x03, 0x04, 0x05, 0x06, 0x07]
+)
+# ingot-examples/benches/packet.rs:59-128 (opte_in_pkt); opte_out_pkt = last 50 B (:129)
+V6_FD02 = [0xFD, 0x00, 0x00, 0x00, 0x00, 0xF7, 0x01, 0x01, 0, 0, 0, 0, 0, 0, 0, 0x02]
+V6_FD01 = [0xFD, 0x00, 0x00, 0x00, 0x00, 0xF7, 0x01, 0x01, 0, 0, 0, 0, 0, 0, 0, 0x01]
+INNER_ETH_V4 = [0xAA, 0x00, 0x04, 0x00, 0xFF, 0x10, 0xAA, 0x00, 0x04, 0x00, 0xFF, 0x01,
+                0x08, 0x00]
+INNER_V4 = [0x45, 0x00, 0x00, 28 + 8, 0x00, 0x00, 0x00, 0x00, 0xF0, 0x11, 0x00, 0x00,
+            8, 8, 8, 8, 192, 168, 0, 5]
+INNER_UDP = [0x00, 0x80, 0x00, 53, 0x00, 0x08, 0x00, 0x00]
+INNER_BODY = [0x00, 0x01, 0x02, 0x03, 0x04, 0x05, 0x06, 0x07]
+OPTE_IN = (
+    [0xA8, 0x40, 0x25, 0x77, 0x77, 0x76, 0xA8, 0x40, 0x25, 0x77, 0x77, 0x77, 0x86, 0xDD]
+    + [0x60, 0x00, 0x00, 0x00, 0x00, 0x10, 0x11, 0xF0] + V6_FD02 + V6_FD01
+    + [0x1E, 0x61, 0x17, 0xC1, 0x00, 0x14, 0x00, 0x00]
+    + [0x01, 0x00, 0x65, 0x58, 0x00, 0x04, 0xD2, 0x00, 0x01, 0x29, 0x00, 0x00]
+    + INNER_ETH_V4 + INNER_V4 + INNER_UDP + INNER_BODY
+)
+OPTE_OUT = OPTE_IN[len(OPTE_IN) - 50:]
+
+# ingot-examples/src/tests.rs:310-329 (would_be_valid, 42 B)
+WOULD_BE_VALID = INNER_ETH_V4 + INNER_V4 + INNER_UDP
+# ingot-examples/src/tests.rs:352-372 (would_be_unwanted: protocol 0x59 OSPF)
+WOULD_BE_UNWANTED = (
+    INNER_ETH_V4
+    + [0x45, 0x00, 0x00, 28 + 8, 0x00, 0x00, 0x00, 0x00, 0xF0, 0x59, 0x00, 0x00,
+       8, 8, 8, 8, 192, 168, 0, 5]
+    + [0x00, 0x80, 0x00, 53, 0x00, 0x08, 0x00, 0x00]
+)
+# ingot-examples/src/tests.rs:280-291 (ARP, early accept)
+ARP_PKT = ([0xA8, 0x40, 0x25, 0x77, 0x77, 0x76, 0xA8, 0x40, 0x25, 0x77, 0x77, 0x77, 0x08, 0x06]
+           + list(range(8)))
+
+# ingot/src/tests.rs:298-330 (v6 -> HBH -> Fragment -> Experiment(253) -> UDP)
+V6_EH_CHAIN = (
+    [0x6A, 0x61, 0xE2, 0x40, 0x00, 0x10, 0x00, 0xF0] + V6_FD02 + V6_FD01
+    + [44, 0x00] + [0x00] * 6
+    + [253, 0, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00]
+    + [0x11, 0x04] + [0x00] * 38
+)
+# ingot/src/tests.rs:227-238 (bitset_fields_do_not_disturb_neighbours)
+V6_BITSET = [0x6A, 0x61, 0xE2, 0x40, 0x00, 0x10, 0x11, 0xF0] + V6_FD02 + V6_FD01
+
+# ingot/src/tests.rs:78-99 (TestFunFields)
+FUN_FIELDS = [
+    0x01, 0xA1, 0x23, 0x45,
+    0x45, 0x23, 0xA1, 0xFF,
+    0b1000_0000, 0b1_100_0000, 0b10_11_1110, 0b1001_1010,
+    0b1_101_0101, 0b0101_0101, 0b0101_0101, 0b0101_010_0,
+    0b0000_0001, 0b1_000_0001, 0b01_10_0110, 0b1011_1110,
+    0b1_101_0101, 0b0101_0101, 0b0101_0101, 0b0101_010_0,
+    0b0000_0000, 0b1_000_0000, 0b00_00_0000, 0b0000_0000,
+    0x01, 0xDE, 0x01, 0xDE,
+]
+
+
+def eth(dst, src, et):
+    return list(dst) + list(src) + [et >> 8, et & 0xFF]
+
+
+def u16(v):
+    return [v >> 8, v & 0xFF]
+
+
+def chain_frames():
+    out = []
+
+    # ingot-examples/src/tests.rs:22-54 parse_header_chain_with_narrowing:
+    # 42 zero bytes, then eth src/dst/ethertype, ipv4 protocol/src/dst set.
+    f = [0] * 42
+    f[0:14] = eth(BROADCAST, MAC_ABCDEF, 0x0800)
+    f[14 + 9] = 17
+    f[14 + 12:14 + 16] = [192, 168, 0, 1]
+    f[14 + 16:14 + 20] = [192, 168, 0, 255]
+    out.append(dict(
+        name="parse_header_chain_with_narrowing", source="ingot-examples/src/tests.rs:22-54",
+        chain="UdpParser", frame=hexs(f),
+        expect=dict(ok=True, l3="ipv4", l4="udp", remainder=0,
+                    fields=dict(eth_source=hexs(MAC_ABCDEF), v4_ihl=0, v4_hop_limit=0)),
+        note="ihl=0 is accepted: options = (0*4).saturating_sub(20) = 0 (ip.rs:91)"))
+
+    # ingot-examples/src/tests.rs:56-118 variable_len_fields_in_header_chain
+    f = [0] * 54
+    f[0:14] = eth(BROADCAST, MAC_ABCDEF, 0x0800)
+    f[14] = 0x08  # set_ihl(8); version left 0 by the zeroed buffer
+    f[14 + 9] = 17
+    f[14 + 12:14 + 16] = [192, 168, 0, 1]
+    f[14 + 16:14 + 20] = [192, 168, 0, 255]
+    f[34:46] = list(range(12))
+    f[46:54] = u16(6082) + u16(6081) + u16(0) + u16(0xFFFF)
+    out.append(dict(
+        name="variable_len_fields_in_header_chain", source="ingot-examples/src/tests.rs:56-118",
+        chain="UdpParser", frame=hexs(f),
+        expect=dict(ok=True, l3="ipv4", l4="udp", remainder=0, fields=dict(
+            eth_source=hexs(MAC_ABCDEF), eth_destination=hexs(BROADCAST),
+            eth_ethertype=0x0800, v4_protocol=17, v4_source=hexs([192, 168, 0, 1]),
+            v4_destination=hexs([192, 168, 0, 255]), v4_ihl=8,
+            v4_options=hexs(range(12)), l4_source=6082, l4_destination=6081,
+            udp_length=0, udp_checksum=0xFFFF))))
+
+    # ingot-examples/src/tests.rs:120-187 parse_header_chain_multichunk — the
+    # four chunks concatenated into one slice (values asserted :158-184).
+    e = eth(BROADCAST, MAC_ABCDEF, 0x86DD)
+    v6 = [0] * 40
+    v6[6] = 17
+    v6[8:24] = [0] * 15 + [1]  # Ipv6Addr::LOCALHOST
+    udp = u16(6082) + u16(6081) + u16(128) + u16(0xFFFF)
+    f = e + v6 + udp + [0xAA] * 128
+    out.append(dict(
+        name="parse_header_chain_multichunk_values", source="ingot-examples/src/tests.rs:120-187",
+        chain="UdpParser", frame=hexs(f), derived="chunks concatenated (parse_read is out of scope)",
+        expect=dict(ok=True, l3="ipv6", l4="udp", remainder=128, remainder_hex=hexs([0xAA] * 128),
+                    fields=dict(eth_source=hexs(MAC_ABCDEF), eth_destination=hexs(BROADCAST),
+                                eth_ethertype=0x86DD, v6_next_header=17, v6_version=0,
+                                v6_source=hexs([0] * 15 + [1]), v6_destination=hexs([0] * 16),
+                                l4_source=6082, l4_destination=6081, udp_length=128,
+                                udp_checksum=0xFFFF),
+                    l4_proto=17)))
+
+    # ingot-examples/src/tests.rs:307-379 parse_reports_error_location
+    for cut, label in ((4, "inner_eth"), (14, "inner_l3"), (len(WOULD_BE_VALID) - 1, "inner_ulp")):
+        out.append(dict(
+            name=f"parse_reports_error_location_trunc{cut}",
+            source="ingot-examples/src/tests.rs:331-349", chain="GenericUlp",
+            frame=hexs(WOULD_BE_VALID[:cut]),
+            expect=dict(ok=False, error="TooSmall", label=label)))
+    out.append(dict(
+        name="parse_reports_error_location_unwanted", source="ingot-examples/src/tests.rs:351-378",
+        chain="GenericUlp", frame=hexs(WOULD_BE_UNWANTED),
+        expect=dict(ok=False, error="Unwanted", label="inner_ulp")))
+    out.append(dict(
+        name="would_be_valid_full", source="ingot-examples/src/tests.rs:310-329", chain="GenericUlp",
+        frame=hexs(WOULD_BE_VALID), derived="the untruncated frame of the error-location test",
+        expect=dict(ok=True, l3="ipv4", l4="udp", remainder=0, fields=dict(
+            v4_source=hexs([8, 8, 8, 8]), v4_destination=hexs([192, 168, 0, 5]),
+            l4_source=0x80, l4_destination=53, udp_length=8), note="by construction")))
+
+    # ingot-examples/src/tests.rs:381-424 straddle_failure, single-chunk half:
+    # pkt[..16] with no further chunks -> TooSmall at inner_l3 (:419-423).
+    out.append(dict(
+        name="straddle_failure_single_chunk", source="ingot-examples/src/tests.rs:416-423",
+        chain="GenericUlp", frame=hexs(WOULD_BE_VALID[:16]),
+        expect=dict(ok=False, error="TooSmall", label="inner_l3")))
+
+    # ingot-examples/src/tests.rs:277-305 chunks_present_on_early_accept
+    out.append(dict(
+        name="chunks_present_on_early_accept", source="ingot-examples/src/tests.rs:277-298",
+        chain="GenericUlp", frame=hexs(ARP_PKT),
+        expect=dict(ok=True, accepted=True, l3="none", l4="none", remainder=8)))
+
+    # ingot-examples/benches/packet.rs frames (benches unwrap() => Ok)
+    out.append(dict(
+        name="bench_parse_stack_v4", source="ingot-examples/benches/packet.rs:15-34,136-138",
+        chain="UdpParser", frame=hexs(PKT_BODY_V4),
+        expect=dict(ok=True, l3="ipv4", l4="udp", remainder=8, fields=dict(
+            eth_destination=hexs([0] * 6), eth_source=hexs([0xFF] * 6), v4_version=4, v4_ihl=5,
+            v4_total_len=36, v4_hop_limit=0xF0, v4_protocol=17,
+            v4_source=hexs([192, 168, 0, 1]), v4_destination=hexs([192, 168, 0, 255]),
+            l4_source=0x80, l4_destination=0x17C1, udp_length=8, udp_checksum=0),
+            note="by construction")))
+    out.append(dict(
+        name="bench_parse_stack_v6", source="ingot-examples/benches/packet.rs:36-57,146-148",
+        chain="UdpParser", frame=hexs(PKT_BODY_V6),
+        expect=dict(ok=True, l3="ipv6", l4="udp", remainder=8, fields=dict(
+            v6_version=6, v6_payload_len=16, v6_next_header=17, v6_hop_limit=0xF0,
+            v6_source=hexs([0] * 15 + [1]), v6_destination=hexs([0] * 15 + [1]),
+            l4_source=0x80, l4_destination=0x17C1), note="by construction")))
+    out.append(dict(
+        name="bench_parse_stack_opte_out", source="ingot-examples/benches/packet.rs:129,167-169",
+        chain="GenericUlp", frame=hexs(OPTE_OUT),
+        expect=dict(ok=True, l3="ipv4", l4="udp", remainder=8, fields=dict(
+            v4_source=hexs([8, 8, 8, 8]), l4_destination=53), note="by construction")))
+    out.append(dict(
+        name="bench_opte_in_outer_as_udp_parser", source="ingot-examples/benches/packet.rs:59-128",
+        chain="UdpParser", frame=hexs(OPTE_IN), derived="outer Eth/v6/UDP of the OPTE frame",
+        expect=dict(ok=True, l3="ipv6", l4="udp", remainder=len(OPTE_IN) - 62, fields=dict(
+            v6_source=hexs(V6_FD02), v6_destination=hexs(V6_FD01), l4_source=0x1E61,
+            l4_destination=0x17C1, udp_length=0x14), note="by construction")))
+
+    # ingot/src/tests.rs:296-369 v6_repeat_extension_headers, as a chain:
+    # Ethernet(IPv6) + the v6/EH bytes (payload_len 16 ignored) + UDP header.
+    f = eth(BROADCAST, MAC_ABCDEF, 0x86DD) + V6_EH_CHAIN + u16(1) + u16(2) + u16(8) + u16(0)
+    out.append(dict(
+        name="v6_repeat_extension_headers_chain", source="ingot/src/tests.rs:296-369",
+        chain="UdpParser", frame=hexs(f), derived="Ethernet prefix + UDP suffix",
+        expect=dict(ok=True, l3="ipv6", l4="udp", remainder=0, l4_proto=17, n_v6ext=3,
+                    v6_ext_len=56,
+                    ehs=[dict(kind="rfc6564", next_header=44, ext_len=0),
+                         dict(kind="fragment", next_header=253),
+                         dict(kind="rfc6564", next_header=17, ext_len=4)],
+                    fields=dict(v6_version=6, v6_dscp=41, v6_ecn=2, v6_flow_label=123456,
+                                v6_payload_len=16, v6_next_header=0))))
+    # ingot/src/tests.rs:223-294 bitset_fields_do_not_disturb_neighbours, as a chain.
+    f = eth(BROADCAST, MAC_ABCDEF, 0x86DD) + V6_BITSET + u16(7) + u16(9) + u16(8) + u16(0)
+    out.append(dict(
+        name="bitset_fields_do_not_disturb_neighbours_chain", source="ingot/src/tests.rs:223-294",
+        chain="UdpParser", frame=hexs(f), derived="Ethernet prefix + UDP suffix",
+        expect=dict(ok=True, l3="ipv6", l4="udp", remainder=0, fields=dict(
+            v6_version=6, v6_dscp=41, v6_ecn=2, v6_ecn_raw=2, v6_flow_label=123456))))
+    # ingot/src/tests.rs:57-71 base_parse_and_type_conversion as a chain: a
+    # zeroed v6 header with next_header TCP and nothing after it -> the L4
+    # choice selects Tcp, which is TooSmall.
+    v6 = [0] * 40
+    v6[6] = 6
+    f = eth([0] * 6, [0] * 6, 0x86DD) + v6
+    out.append(dict(
+        name="base_parse_v6_tcp_then_truncated", source="ingot/src/tests.rs:57-71",
+        chain="GenericUlp", frame=hexs(f), derived="Ethernet(IPv6) prefix; chain continues to L4",
+        expect=dict(ok=False, error="TooSmall", label="inner_ulp", l3="ipv6", l4="tcp")))
+    # ingot/src/tests.rs:371-381 repeated_on_standard_header — TooSmall inside
+    # a RepeatedView propagates (util.rs:214).  Chain form: v6 -> HBH whose
+    # ext_len claims 16 more bytes than the frame has.
+    v6 = [0] * 40
+    v6[6] = 0
+    f = eth([0] * 6, [0] * 6, 0x86DD) + v6 + [17, 2] + [0] * 6
+    out.append(dict(
+        name="repeated_eh_truncated_propagates", source="ingot-types/src/util.rs:206-216",
+        chain="UdpParser", frame=hexs(f), derived="EH-chain form of ingot/src/tests.rs:371-381",
+        expect=dict(ok=False, error="TooSmall", label="l3", l3="ipv6")))
+    # roundtrip_emit_parse_unchanged (ingot/src/tests.rs:462-495): the Ipv6 repr
+    # emitted by the layout rules; parse must give it back (hint = NO_NH 59,
+    # so the L4 choice then rejects it).
+    v6 = ([0x60, 0x21, 0xE2, 0x40] + u16(77) + [0, 128] + [0] * 15 + [1] + [0] * 16
+          + [59, 0] + [0] * 6)
+    f = eth([0] * 6, [0] * 6, 0x86DD) + v6
+    out.append(dict(
+        name="roundtrip_emit_parse_unchanged_v6", source="ingot/src/tests.rs:462-495",
+        chain="GenericUlp", frame=hexs(f), derived="emitted bytes restated from the layout",
+        expect=dict(ok=False, error="Unwanted", label="inner_ulp", l3="ipv6", l4_proto=59,
+                    n_v6ext=1)))
+    return out
+
+
+def header_kats():
+    """Header-level vectors: (header kind, bytes, hint) -> (status, used, hint)."""
+    zero54 = [0] * 54
+    v6 = [0] * 40
+    v6[6] = 6
+    return [
+        dict(name="base_parse_ethernet", source="ingot/src/tests.rs:59-60", header="ethernet",
+             bytes=hexs(zero54), expect=dict(ok=True, used=14, hint=0)),
+        dict(name="base_parse_ipv6_tcp", source="ingot/src/tests.rs:62-65", header="ipv6",
+             bytes=hexs(v6), expect=dict(ok=True, used=40, hint=6)),
+        dict(name="v6_repeat_extension_headers", source="ingot/src/tests.rs:332-368",
+             header="ipv6", bytes=hexs(V6_EH_CHAIN), expect=dict(ok=True, used=96, hint=17)),
+        dict(name="bitset_fields_v6", source="ingot/src/tests.rs:240", header="ipv6",
+             bytes=hexs(V6_BITSET), expect=dict(ok=True, used=40, hint=17)),
+        dict(name="repeated_udp_24", source="ingot/src/tests.rs:373-376", header="repeated_udp",
+             bytes=hexs([0] * 24), expect=dict(ok=True, used=24)),
+        dict(name="repeated_udp_20", source="ingot/src/tests.rs:377-380", header="repeated_udp",
+             bytes=hexs([0] * 20), expect=dict(ok=False, error="TooSmall")),
+        dict(name="udp_roundtrip", source="ingot/src/tests.rs:462-468", header="udp",
+             bytes=hexs(u16(1234) + u16(5678) + u16(77) + u16(0xFFFF)),
+             expect=dict(ok=True, used=8)),
+        dict(name="ipv4_opts_bench", source="ingot/benches/modify.rs:67-77", header="ipv4",
+             bytes=hexs([0x49, 0x00, 0x00, 36, 0, 0, 0, 0, 0xF0, 0x11, 0, 0, 8, 8, 8, 8,
+                         192, 168, 0, 5] + list(range(16))),
+             expect=dict(ok=True, used=36, hint=17)),
+        dict(name="ipv4_no_opt_bench", source="ingot/benches/modify.rs:57-65", header="ipv4",
+             bytes=hexs(INNER_V4), expect=dict(ok=True, used=20, hint=17)),
+    ]
+
+
+def bitfield_kats():
+    # ingot/src/tests.rs:27-55 layout of TestFunFields (BE members only; the LE
+    # forms are out of scope: LE bitfields are unsupported, ingot/README.md:23).
+    return [dict(
+        name="unaligned_bitfield_read_write", source="ingot/src/tests.rs:73-118",
+        bytes=hexs(FUN_FIELDS),
+        fields=[
+            dict(name="fine", bit=0, bits=8, value=1),
+            dict(name="memcpy_be", bit=8, bits=24, value=10_560_325),
+            dict(name="still_fine", bit=56, bits=8, value=255),
+            dict(name="tricky_be0", bit=64, bits=9, value=257),
+            dict(name="tricky_be1", bit=73, bits=9, value=258),
+            dict(name="tricky_be2", bit=82, bits=14, value=16_026),
+            dict(name="trickier_be0", bit=96, bits=1, value=1),
+            dict(name="trickier_be1", bit=97, bits=30, value=0x2AAA_AAAA),
+            dict(name="trickier_be2", bit=127, bits=1, value=0),
+            dict(name="also_fine", bit=224, bits=32, value=31_326_686),
+        ])]
+
+
+def main() -> None:
+    doc = dict(
+        reference="oxidecomputer/ingot @ 2025-08-08",
+        generator="tests/golden/make_golden.py",
+        chain_kats=chain_frames(),
+        header_kats=header_kats(),
+        bitfield_kats=bitfield_kats(),
+    )
+    (HERE / "kats.json").write_text(json.dumps(doc, indent=1) + "\n")
+    print(f"wrote {len(doc['chain_kats'])} chain, {len(doc['header_kats'])} header, "
+          f"{len(doc['bitfield_kats'])} bitfield vectors")
+
+
+if __name__ == "__main__":
+    main()

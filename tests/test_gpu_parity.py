@@ -1,0 +1,251 @@
+"""Parity of the gfx950 path against the CPU oracle (bit-exact records and
+field blocks), through the C ABI.  Needs an MI355X: `pytest -m gpu`.
+
+* the reference's golden vectors (tests/golden/kats.json) through the device;
+* adversarial fuzz frames (every truncation / ihl / data_offset / EH / unknown
+  ethertype path), all three chains, records AND every getter;
+* each benchmark profile and layout at sizes the oracle finishes in seconds;
+* at full benchmark sizes, size-independent properties plus a sampled oracle
+  re-check of frames copied back from the device.
+"""
+import numpy as np
+import pytest
+
+import ingot_amd
+import oracle
+from ingot_amd import Chain, GenProfile, ParseError
+from tests.kat_check import check
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.fixture(scope="module")
+def ctx(torch):
+    return ingot_amd.Context(0)
+
+
+def host(t):
+    return None if t is None else t.cpu().numpy()
+
+
+def oracle_check(ctx, torch, arena, off, lens, chain, stride=0, n=None, fields=True):
+    """Run device records (+fields) and compare byte-for-byte with the oracle."""
+    if off is not None:
+        n = off.numel()
+        recs = ctx.parse(arena, off, lens, chain)
+    else:
+        recs = ctx.parse_strided(arena, stride, n, chain, lens=lens)
+    flds = ctx.fields(arena, off, lens, chain, stride=stride, n=n) if fields else None
+    torch.cuda.synchronize()
+    want = oracle.parse_batch(host(arena), host(off), host(lens), chain, stride=stride, n=n,
+                              fields=fields, nthreads=8)
+    w_rec = want[0] if fields else want
+    g_rec = ingot_amd.records_to_numpy(recs)
+    diff = np.nonzero((g_rec.view(np.uint8).reshape(n, 16) !=
+                       w_rec.view(np.uint8).reshape(n, 16)).any(axis=1))[0]
+    assert diff.size == 0, (f"{diff.size} record mismatches, first {diff[:5]}: "
+                            f"gpu {g_rec[diff[0]]} oracle {w_rec[diff[0]]}")
+    if fields:
+        g_f = ingot_amd.fields_to_numpy(flds)
+        fd = np.nonzero((g_f.view(np.uint8).reshape(n, 256) !=
+                         want[1].view(np.uint8).reshape(n, 256)).any(axis=1))[0]
+        assert fd.size == 0, (f"{fd.size} field mismatches, first {fd[:5]}: "
+                              f"gpu {g_f[fd[0]]} oracle {want[1][fd[0]]}")
+    return g_rec
+
+
+# ---------------------------------------------------------------------------
+# golden vectors
+# ---------------------------------------------------------------------------
+def test_golden_kats_on_device(ctx, torch, kats):
+    for chain in Chain:
+        group = [k for k in kats["chain_kats"] if Chain[k["chain"]] == chain]
+        if not group:
+            continue
+        frames = [bytes.fromhex(k["frame"]) for k in group]
+        recs, flds = ingot_amd.parse_frames(frames, chain)
+        for k, f, r, fl in zip(group, frames, recs, flds):
+            bad = check(k, r, fl)
+            assert not bad, f"{k['name']} ({k['source']}): {bad}"
+            orec, ofld = oracle.parse_one(f, chain)
+            assert r.tobytes() == orec.tobytes(), k["name"]
+            assert fl.tobytes() == ofld.tobytes(), k["name"]
+
+
+def test_reference_tests_read_alike(torch):
+    """ingot-examples/src/tests.rs:56-118 and :307-379, through the device."""
+    f = bytearray(54)
+    f[0:6] = b"\xff" * 6
+    f[6:12] = bytes([0xA, 0xB, 0xC, 0xD, 0xE, 0xF])
+    f[12:14] = b"\x08\x00"
+    f[14] = 0x08
+    f[23] = 17
+    f[26:30] = bytes([192, 168, 0, 1])
+    f[30:34] = bytes([192, 168, 0, 255])
+    f[34:46] = bytes(range(12))
+    f[46:54] = bytes([0x17, 0xC2, 0x17, 0xC1, 0, 0, 0xFF, 0xFF])
+    stack, hint, rest = ingot_amd.UdpParser.parse(bytes(f))
+    assert hint is None and rest == b""
+    assert stack.eth.source() == bytes([0xA, 0xB, 0xC, 0xD, 0xE, 0xF])
+    assert stack.eth.destination() == b"\xff" * 6
+    assert stack.eth.ethertype() == 0x0800
+    assert stack.l3.protocol() == 17
+    assert stack.l3.source() == bytes([192, 168, 0, 1])
+    assert stack.l3.ihl() == 8
+    assert stack.l3.options_ref() == bytes(range(12))
+    assert (stack.l4.source(), stack.l4.destination()) == (6082, 6081)
+    assert (stack.l4.length(), stack.l4.checksum()) == (0, 0xFFFF)
+
+    would_be_valid = bytes.fromhex(
+        "aa000400ff10aa000400ff010800" "45000024000000" "00f0110000080808" "08c0a80005"
+        "00800035" "00080000")
+    for cut, label in ((4, "inner_eth"), (14, "inner_l3"), (len(would_be_valid) - 1,
+                                                            "inner_ulp")):
+        with pytest.raises(ingot_amd.PacketParseError) as e:
+            ingot_amd.GenericUlp.parse_slice(would_be_valid[:cut])
+        assert e.value.error() == ParseError.TooSmall
+        assert e.value.header() == label
+
+
+# ---------------------------------------------------------------------------
+# fuzz + profiles
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("chain", list(Chain))
+def test_adversarial_fuzz_bit_exact(ctx, torch, chain):
+    arena, off, lens = ingot_amd.gen_frames(GenProfile.ADVERSARIAL, 300_000, seed=11)
+    g = oracle_check(ctx, torch, arena, off, lens, chain)
+    st = g["status"]
+    # the fuzz set must reach every reachable outcome
+    assert (st == 0).any()
+    assert (st == ParseError.TooSmall).any() and (st == ParseError.Unwanted).any()
+    assert (g["err_layer"][st != 0] == 0).any()
+
+
+@pytest.mark.parametrize("profile,chain", [
+    (GenProfile.MIXED, Chain.GenericUlp),
+    (GenProfile.MIXED, Chain.UdpParser),
+    (GenProfile.VLAN_V6EH, Chain.VlanUlp),
+    (GenProfile.VLAN_V6EH, Chain.GenericUlp),
+    (GenProfile.FLOWS, Chain.VlanUlp),
+])
+def test_profile_indexed_bit_exact(ctx, torch, profile, chain):
+    arena, off, lens = ingot_amd.gen_frames(profile, 200_000, seed=3)
+    g = oracle_check(ctx, torch, arena, off, lens, chain)
+    if chain != Chain.UdpParser and not (profile != GenProfile.MIXED and
+                                         chain == Chain.GenericUlp):
+        assert (g["status"] == 0).all()
+
+
+@pytest.mark.parametrize("stride,profile", [(64, GenProfile.V4UDP64), (64, GenProfile.ADVERSARIAL),
+                                            (128, GenProfile.MIXED), (2048, GenProfile.MIXED),
+                                            (48, GenProfile.ADVERSARIAL)])
+def test_strided_bit_exact(ctx, torch, stride, profile):
+    n = 100_003  # not a multiple of 64
+    arena, _, lens = ingot_amd.gen_frames(profile, n, seed=5, stride=stride)
+    for chain in Chain:
+        oracle_check(ctx, torch, arena, None, lens, chain, stride=stride, n=n,
+                     fields=chain == Chain.GenericUlp)
+
+
+def test_v4udp64_full_batch_exact(ctx, torch):
+    """Config 2 exactly: 1,048,576 x 64 B under UdpParser, every record checked."""
+    n = 1 << 20
+    arena, _, _ = ingot_amd.gen_frames(GenProfile.V4UDP64, n, stride=64)
+    g = oracle_check(ctx, torch, arena, None, None, Chain.UdpParser, stride=64, n=n,
+                     fields=False)
+    assert (g["status"] == 0).all()
+    assert (g["payload_off"] == 42).all() and (g["l4_kind"] == 2).all()
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 1000])
+def test_small_and_ragged_batches(ctx, torch, n):
+    arena, off, lens = ingot_amd.gen_frames(GenProfile.ADVERSARIAL, max(n, 1), seed=n + 1)
+    if n == 0:
+        off, lens = off[:0], lens[:0]
+        recs = ctx.parse(arena, off, lens, Chain.GenericUlp)
+        torch.cuda.synchronize()
+        assert recs.shape == (0, 16)
+        return
+    oracle_check(ctx, torch, arena, off, lens, Chain.GenericUlp)
+
+
+def test_window_boundary_and_long_chains(ctx, torch):
+    """Headers that end exactly at, or run far past, the 128-B LDS window
+    (long IPv4/TCP options, long EH chains) take the HBM path for the bytes
+    beyond the window; results must not change."""
+    frames = []
+    rng = np.random.default_rng(1)
+    for doff in range(5, 16):
+        for ihl in range(5, 16):
+            v4 = bytearray(ihl * 4)
+            v4[0] = 0x40 | ihl
+            v4[9] = 6
+            tcp = bytearray(doff * 4)
+            tcp[12] = doff << 4
+            f = bytes(12) + b"\x08\x00" + bytes(v4) + bytes(tcp)
+            for extra in (0, 1, 7):
+                frames.append(f + bytes(extra))
+            frames.append(f[:-1])
+    for n_eh in range(0, 12):
+        for ext in (0, 1, 3, 30):
+            v6 = bytearray(40)
+            v6[0] = 0x60
+            v6[6] = 0 if n_eh else 17
+            body = b""
+            for k in range(n_eh):
+                nh = 60 if k + 1 < n_eh else 17
+                body += bytes([nh, ext]) + rng.integers(0, 256, 6 + 8 * ext,
+                                                          dtype=np.uint8).tobytes()
+            f = bytes(12) + b"\x86\xdd" + bytes(v6) + body + bytes([0, 1, 0, 2, 0, 8, 0, 0])
+            frames.append(f)
+            frames.append(f[:-9])
+    # random misalignment
+    for chain in Chain:
+        recs, flds = ingot_amd.parse_frames(frames, chain)
+        for i, f in enumerate(frames):
+            orec, ofld = oracle.parse_one(f, chain)
+            assert recs[i].tobytes() == orec.tobytes(), (i, recs[i], orec)
+            assert flds[i].tobytes() == ofld.tobytes(), i
+
+
+# ---------------------------------------------------------------------------
+# full benchmark sizes: properties + sampled re-check
+# ---------------------------------------------------------------------------
+def test_config3_full_size_properties(ctx, torch):
+    """Config 3 at its full size: 16,777,216 mixed 64-1500 B frames (~13 GB)."""
+    n = 16 * (1 << 20)
+    arena, off, lens = ingot_amd.gen_frames(GenProfile.MIXED, n)
+    recs = ctx.parse(arena, off, lens, Chain.GenericUlp)
+    torch.cuda.synchronize()
+    r = recs.view(torch.int32).view(n, 4)
+    status = recs[:, 0]
+    assert int((status != 0).sum()) == 0
+    l3 = recs[:, 2].to(torch.int64)
+    frac_v6 = float((l3 == 2).double().mean())
+    assert 0.49 < frac_v6 < 0.51
+    payload = r[:, 3] & 0xFFFF
+    assert bool((payload.to(torch.int64) <= lens.to(torch.int64)).all())
+    # determinism: a second run is identical
+    recs2 = ctx.parse(arena, off, lens, Chain.GenericUlp)
+    torch.cuda.synchronize()
+    assert torch.equal(recs, recs2)
+    # sampled oracle re-check on the exact device bytes
+    idx = np.random.default_rng(0).choice(n, 4096, replace=False)
+    offs = host(off)[idx]
+    ls = host(lens)[idx]
+    frames = [host(arena[int(o):int(o) + int(ln)]).tobytes() for o, ln in zip(offs, ls)]
+    got = ingot_amd.records_to_numpy(recs[torch.as_tensor(idx, device=recs.device)])
+    for k, f in enumerate(frames):
+        orec, _ = oracle.parse_one(f, Chain.GenericUlp)
+        assert got[k].tobytes() == orec.tobytes(), idx[k]
+    del arena, off, lens, recs, recs2
+    torch.cuda.empty_cache()
