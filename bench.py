@@ -1,23 +1,31 @@
 #!/usr/bin/env python3
 """bench.py — device-resident L2/L3/L4 parse throughput on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
+                    [--streams S] [--record 16|8]
 
-A *step* is one pass of the parse path over one batch of synthetic frames
+A *step* is one launch of the parse path over one batch of synthetic frames
 already resident in HBM.  At N=1 the default workload is BASELINE.json
 configs[1] (C2): 1,048,576 x 64-B Eth/IPv4/UDP frames in 64-B slots, parsed as
-ingot's `UdpParser`.  N>1 (torchrun, one rank per GPU): every rank parses its
-own shard of the same size (weak scaling; packets are independent, so there is
-no data-path collective; only C5's per-flow histogram is all-reduced over
-RCCL).  Rank 0 prints one JSON line.
+ingot's `UdpParser`, 16-B records.  N>1 (torchrun, one rank per GPU): every
+rank parses its own shard of the same size (weak scaling; packets are
+independent, so there is no data-path collective).  Rank 0 prints one JSON
+line.
 
-To measure HBM and not the 256 MiB Infinity Cache, each step reads a different
-one of R arena copies (R chosen so the rotating set is >= 512 MiB).
+Pipelining: consecutive batches are independent, so step k is launched on
+stream k % S (default S=2, a double-buffered pipeline like a NIC-ring
+consumer): the next batch's kernel ramps up while the previous one drains,
+hiding the ~1.5 us dependent-launch boundary.  Every step is still exactly
+one launch over one 1M-frame batch; `variants` reports S=1 and 8-B records.
 
-`roofline` = algorithmic bytes per launch (R_i = min(len,128) +
-max(0, H_i-128) + D, W_i = 16) / the parse kernel's mean duration, timed with
-HIP events around each launch on the launch stream.  `cpu_baseline` = the C
-restatement of ingot's parse (oracle/, "port") on the host cores, rank 0, N=1.
+To measure HBM and not the 256 MiB Infinity Cache, step k reads arena copy
+k % R and writes record buffer k % R (R copies >= 512 MiB in total).
+
+`roofline.achieved` = algorithmic bytes per launch (R_i =
+min(len,128) + max(0, H_i-128) + D, W_i = record bytes) / (timed region / K),
+i.e. the HBM rate the device sustains on this path, from HIP events on the
+launch streams.  `cpu_baseline` = the C restatement of ingot's parse
+(oracle/, "port") on the host cores, rank 0, N=1.
 """
 from __future__ import annotations
 
@@ -34,17 +42,20 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 METRIC = "Mpkt/s device-resident L2/L3/L4 parse, 64–1500 B frames; % HBM roofline"
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md:36 (spec); 6.29 TB/s measured copy ceiling
-HBM_MEASURED_GBS = 6290.0
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md:36 (spec)
+HBM_MEASURED_GBS = 6290.0  # MI355X_MICROARCH.md:36 (measured float4 copy)
 
 CONFIGS = {
-    # name: (profile, frames per GPU, layout stride or None, chain, description)
+    # name: (profile, frames per GPU, slot stride or None (packed), chain, description)
     "c2": ("V4UDP64", 1 << 20, 64, "UdpParser",
            "C2: 1,048,576 x 64 B Eth/IPv4/UDP per GPU, 64-B slots, UdpParser"),
     "c3": ("MIXED", 1 << 24, None, "GenericUlp",
            "C3: 16,777,216 mixed 64-1500 B v4/v6 x TCP/UDP per GPU, packed, GenericUlp"),
+    "c3s": ("MIXED", 1 << 22, 2048, "GenericUlp",
+            "C3 frames in 2048-B ring slots (NIC-ring layout): 4,194,304 per GPU, GenericUlp"),
     "c4": ("VLAN_V6EH", 1 << 23, None, "VlanUlp",
-           "C4: 8,388,608 VLAN/QinQ + IPv6-EH mixed frames per GPU, packed, VlanUlp"),
+           "C4: 8,388,608 VLAN/QinQ + IPv6-EH mixed frames per GPU (64M over 8), packed, "
+           "VlanUlp"),
 }
 
 
@@ -52,21 +63,19 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def algorithmic_bytes(recs_np, lens_np, stride, descriptor_bytes):
-    """R_i = min(len_i,128) + max(0, H_i-128) + D ; W_i = 16.
-    H_i = header span the parse inspects = payload_off on Ok; on error the
-    consumed bytes plus the failing layer's fixed part is bounded by len."""
+def algorithmic_bytes(recs_np, lens_np, stride, descriptor_bytes, record_bytes):
+    """R_i = min(len_i,128) + max(0, H_i-128) + D ; W_i = record.
+    H_i = the header span the parse consumed (payload_off)."""
     lens = lens_np.astype(np.int64) if lens_np is not None else np.full(len(recs_np), stride)
     h = recs_np["payload_off"].astype(np.int64)
     r = np.minimum(lens, 128) + np.maximum(0, h - 128) + descriptor_bytes
-    return int(r.sum()), 16 * len(recs_np)
+    return int(r.sum()), record_bytes * len(recs_np)
 
 
 def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5):
     """Time the oracle on the host cores over the same frames (bounded)."""
     import oracle
 
-    lib = None
     try:  # -march=native build for this host, into a scratch dir
         d = Path(os.environ.get("TMPDIR", "/tmp")) / f"ingot_oracle_native_{os.getpid()}"
         lib = oracle.load(oracle.build(out_dir=d, native=True))
@@ -111,13 +120,64 @@ def _cpu_model():
     return "unknown"
 
 
+class Runner:
+    """Launches step k (arena k % R -> records k % R) on stream k % S."""
+
+    def __init__(self, torch, lib, ctx, chain, n, stride, arenas, off, lens, outs, streams,
+                 record_bytes):
+        self.torch, self.streams = torch, streams
+        reps = len(arenas)
+        h = ctx._h
+        optr = off.data_ptr() if off is not None else None
+        lptr = lens.data_ptr() if lens is not None else None
+        aptrs = [a.data_ptr() for a in arenas]
+        outptrs = [o.data_ptr() for o in outs]
+        sps = [s.cuda_stream for s in streams]
+        ns = len(sps)
+        c = int(chain)
+        if stride is not None:
+            fn = lib.ingot_gpu_parse_strided if record_bytes == 16 else \
+                lib.ingot_gpu_parse_strided_compact
+            self.launch = lambda k: fn(h, aptrs[k % reps], stride, lptr, n, c,
+                                       outptrs[k % reps], sps[k % ns])
+        else:
+            fn = lib.ingot_gpu_parse if record_bytes == 16 else lib.ingot_gpu_parse_compact
+            self.launch = lambda k: fn(h, aptrs[k % reps], optr, lptr, n, c,
+                                       outptrs[k % reps], sps[k % ns])
+
+    def run(self, steps):
+        """Time `steps` launches: fork all streams from streams[0], join back."""
+        torch = self.torch
+        s0 = self.streams[0]
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        w0 = time.perf_counter()
+        e0.record(s0)
+        for s in self.streams[1:]:
+            s.wait_event(e0)
+        for k in range(steps):
+            rc = self.launch(k)
+            if rc:
+                raise RuntimeError(f"parse launch failed: {rc}")
+        for s in self.streams[1:]:
+            ev = torch.cuda.Event()
+            ev.record(s)
+            s0.wait_event(ev)
+        e1.record(s0)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1), time.perf_counter() - w0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--streams", type=int, default=2)
+    ap.add_argument("--record", type=int, default=16, choices=(16, 8))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-variants", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=1.5)
     ap.add_argument("--rotate-mib", type=int, default=512,
                     help="minimum bytes of distinct arenas rotated across steps")
@@ -132,106 +192,91 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device(f"cuda:{local}")
+        dist.init_process_group("nccl", device_id=dev)
 
     prof_name, n, stride, chain_name, desc = CONFIGS[args.config]
     profile, chain = GenProfile[prof_name], Chain[chain_name]
     ctx = ingot_amd.Context(local)
-    stream = torch.cuda.current_stream(dev)
+    lib = ingot_amd.load_library()
 
-    # --- data: R distinct copies of this rank's shard (pure in (seed, index)) ---
+    # --- data: this rank's shard (pure in (seed, index)) + R copies ---
     first = rank * n
     arena, off, lens = ingot_amd.gen_frames(profile, n, first=first, stride=stride,
                                             device=local)
-    shard_bytes = arena.numel()
-    reps = max(1, -(-(args.rotate_mib << 20) // shard_bytes))
+    reps = max(1, -(-(args.rotate_mib << 20) // arena.numel()))
     arenas = [arena] + [arena.clone() for _ in range(reps - 1)]
     outs = [torch.empty((n, 16), dtype=torch.uint8, device=dev) for _ in range(reps)]
     torch.cuda.synchronize(dev)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
+                                                  for _ in range(max(3, args.streams - 1))]
 
-    lib = ingot_amd.load_library()
-    h, sp = ctx._h, stream.cuda_stream
-    optr = off.data_ptr() if off is not None else None
-    lptr = lens.data_ptr() if lens is not None else None
-    aptrs = [a.data_ptr() for a in arenas]
-    outptrs = [o.data_ptr() for o in outs]
+    def runner(nstreams, record):
+        return Runner(torch, lib, ctx, chain, n, stride, arenas, off, lens, outs,
+                      streams[:nstreams], record)
 
-    if stride is not None:
-        fn = lib.ingot_gpu_parse_strided
-
-        def launch(k):
-            return fn(h, aptrs[k % reps], stride, lptr, n, int(chain), outptrs[k % reps], sp)
-    else:
-        fn = lib.ingot_gpu_parse
-
-        def launch(k):
-            return fn(h, aptrs[k % reps], optr, lptr, n, int(chain), outptrs[k % reps], sp)
-
-    for k in range(args.warmup):
-        rc = launch(k)
-        if rc:
-            raise RuntimeError(f"parse launch failed: {rc}")
-    torch.cuda.synchronize(dev)
+    main_run = runner(args.streams, args.record)
+    main_run.run(args.warmup)
 
     # --- timed region: K steps, barrier + sync on both sides ---
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    t_start = torch.cuda.Event(enable_timing=True)
-    t_end = torch.cuda.Event(enable_timing=True)
-    w0 = time.perf_counter()
-    t_start.record(stream)
-    for k in range(args.steps):
-        launch(k)
-    t_end.record(stream)
-    torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - w0
+    ms_region, wall = main_run.run(args.steps)
     if world > 1:
         dist.barrier()
-    ms_region = t_start.elapsed_time(t_end)
-
-    # --- per-launch kernel durations (HIP events bracketing each launch) ---
-    nk = min(args.steps, 200)
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(2 * nk)]
-    for k in range(nk):
-        evs[2 * k].record(stream)
-        launch(k)
-        evs[2 * k + 1].record(stream)
-    torch.cuda.synchronize(dev)
-    kdur = sorted(evs[2 * k].elapsed_time(evs[2 * k + 1]) for k in range(nk))
-    kmean_ms = sum(kdur) / nk
-    kmed_ms = kdur[nk // 2]
-
-    ms_step = ms_region / args.steps
     t_sec = ms_region / 1e3
     if world > 1:
         tt = torch.tensor([t_sec], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_sec = float(tt.item())
-    total_pkts = n * args.steps * world
-    value = total_pkts / t_sec / 1e6
+    value = n * args.steps * world / t_sec / 1e6
+    ms_step = t_sec * 1e3 / args.steps
 
-    # algorithmic bytes from the records of this batch
-    recs_np = ingot_amd.records_to_numpy(outs[0])
+    # --- algorithmic bytes from this batch's records (16-B form) ---
+    recs = ctx.parse_strided(arenas[0], stride, n, chain, lens=lens) \
+        if stride is not None else ctx.parse(arenas[0], off, lens, chain)
+    torch.cuda.synchronize(dev)
+    recs_np = ingot_amd.records_to_numpy(recs)
     lens_np = lens.cpu().numpy() if lens is not None else None
-    rd, wr = algorithmic_bytes(recs_np, lens_np, stride or 0, 0 if stride else 10)
+    rd, wr = algorithmic_bytes(recs_np, lens_np, stride or 0, 0 if stride else 10, args.record)
     bytes_launch = rd + wr
-    achieved = bytes_launch / (kmean_ms / 1e3) / 1e9
+    launch_ms = ms_region / args.steps
+    achieved = bytes_launch / (launch_ms / 1e3) / 1e9
     ok_frac = float((recs_np["status"] == 0).mean())
 
-    result = None
+    # --- variants (outside the timed region; same data) ---
+    variants = {}
+    if not args.no_variants:
+        vsteps = min(args.steps, 1000)
+        for ns, rb in ((1, 16), (2, 8), (1, 8), (4, 16)):
+            if (ns, rb) == (args.streams, args.record):
+                continue
+            r = runner(ns, rb)
+            r.run(min(args.warmup, 50))
+            ms, _ = r.run(vsteps)
+            bpl = rd + rb * n
+            variants[f"streams{ns}_rec{rb}"] = {
+                "value": round(n * vsteps / (ms / 1e3) / 1e6, 2),
+                "us_per_step": round(ms * 1e3 / vsteps, 3),
+                "hbm_GBps": round(bpl / (ms / vsteps / 1e3) / 1e9, 1),
+            }
+
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            a_np = arenas[0].cpu().numpy()
-            o_np = off.cpu().numpy() if off is not None else None
-            cpu = cpu_baseline(a_np, o_np, lens_np, stride or 0, n, chain, args.cpu_budget)
+            m = min(n, 1 << 20)  # bounded sample: the first 1M frames of the batch
+            if off is not None:
+                o_np = off[:m].cpu().numpy()
+                end = int(o_np[-1]) + int(lens_np[m - 1])
+                a_np = arenas[0][:end + 64].cpu().numpy()
+            else:
+                o_np, a_np = None, arenas[0][:m * stride].cpu().numpy()
+            l_np = lens_np[:m] if lens_np is not None else None
+            cpu = cpu_baseline(a_np, o_np, l_np, stride or 0, m, chain, args.cpu_budget)
         result = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -250,6 +295,8 @@ def main():
                 "frames_per_gpu": n,
                 "chain": chain_name,
                 "layout": f"strided {stride} B" if stride else "packed, u64 offsets + u16 lengths",
+                "record_bytes": args.record,
+                "streams": args.streams,
                 "arena_copies_rotated": reps,
                 "parallelism": f"shard per GPU x{world} (no data-path collective)",
                 "ok_fraction": round(ok_frac, 6),
@@ -262,14 +309,14 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None,
                 "kernel": "k_parse (ingot_amd/csrc/parse.hip)",
-                "kernel_mean_us": round(kmean_ms * 1e3, 3),
-                "kernel_median_us": round(kmed_ms * 1e3, 3),
+                "launch_mean_us": round(launch_ms * 1e3, 3),
                 "algorithmic_bytes_per_launch": bytes_launch,
                 "read_bytes_per_launch": rd,
                 "write_bytes_per_launch": wr,
-                "read_frac": round(rd / (kmean_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                "read_frac": round(rd / (launch_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                 "frac_of_measured_copy_ceiling": round(achieved / HBM_MEASURED_GBS, 4),
             },
+            "variants": variants,
             "cpu_baseline": cpu,
             "wall_s_timed_region": round(wall, 4),
         }
@@ -277,7 +324,6 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    return result
 
 
 if __name__ == "__main__":

@@ -126,6 +126,26 @@ typedef struct ingot_rec {
     uint16_t ethertype;
 } ingot_rec;
 
+/* ---------------------------------------------------------------------------
+ * ingot_rec8 — the same result in 8 bytes (for record-bandwidth-bound
+ * callers).  Everything a caller needs to rebuild the layer views is kept;
+ * the dropped rec16 fields are derivable from it and the frame:
+ *   l3_off    = 14 + 4*n_vlan            (when l3_kind != NONE)
+ *   ethertype = be16(frame, 12 + 4*n_vlan)
+ *   err_layer = 0xff when status == Ok
+ *
+ *   b0: status (bits 0-3) | err_layer (bits 4-5, 0 when Ok) | l3_kind (bits 6-7)
+ *   b1: l4_kind (bits 0-2) | n_vlan (bits 3-4) | accepted (bit 5)
+ * ------------------------------------------------------------------------- */
+typedef struct ingot_rec8 {
+    uint8_t status_layer_l3;
+    uint8_t l4_vlan_flags;
+    uint8_t n_v6ext;
+    uint8_t l4_proto;
+    uint16_t l4_off;
+    uint16_t payload_off;
+} ingot_rec8;
+
 /* One IPv6 extension header as ingot's getters see it
  * (IpV6ExtFragment ip.rs:190-200, IpV6Ext6564 ip.rs:202-211). */
 #define INGOT_EH_FRAGMENT 1
@@ -216,6 +236,7 @@ typedef struct ingot_fields {
 
 #ifdef __cplusplus
 static_assert(sizeof(ingot_rec) == 16, "ingot_rec is 16 bytes");
+static_assert(sizeof(ingot_rec8) == 8, "ingot_rec8 is 8 bytes");
 static_assert(sizeof(ingot_v6eh) == 12, "ingot_v6eh is 12 bytes");
 static_assert(sizeof(ingot_fields) == 256, "ingot_fields is 256 bytes");
 #endif
@@ -265,6 +286,16 @@ int ingot_gpu_parse(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
 int ingot_gpu_parse_strided(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
                             uint32_t stride, const uint16_t* d_len, uint64_t n,
                             int chain, ingot_rec* d_out, void* stream);
+
+/* The two batch calls above with 8-byte ingot_rec8 records. */
+int ingot_gpu_parse_compact(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
+                            const uint64_t* d_off, const uint16_t* d_len,
+                            uint64_t n, int chain, ingot_rec8* d_out,
+                            void* stream);
+int ingot_gpu_parse_strided_compact(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
+                                    uint32_t stride, const uint16_t* d_len,
+                                    uint64_t n, int chain, ingot_rec8* d_out,
+                                    void* stream);
 
 /*
  * Parity mode: every getter of every parsed header (ingot_fields, 256 B per

@@ -26,6 +26,8 @@ from .abi import (  # noqa: F401  (re-exports)
     GEN_SEED,
     MAX_EH_FIELDS,
     REC_ACCEPTED,
+    REC8_BYTES,
+    REC8_DTYPE,
     REC_BYTES,
     REC_DTYPE,
     STATUS_OK,
@@ -33,9 +35,11 @@ from .abi import (  # noqa: F401  (re-exports)
     GenProfile,
     IngotFields,
     IngotRec,
+    IngotRec8,
     L3Kind,
     L4Kind,
     ParseError,
+    rec16_to_rec8,
 )
 
 __all__ = [
@@ -134,6 +138,29 @@ class Context:
                                                      _ptr(lens), n, int(chain), _ptr(out),
                                                      _stream(stream)),
                    "ingot_gpu_parse_strided")
+        return out
+
+    def parse_compact(self, arena, off, lens, chain: Chain, out=None, stream=None):
+        """As parse(), with 8-byte ingot_rec8 records: (n, 8) uint8 tensor."""
+        torch = _torch()
+        n = off.numel()
+        if out is None:
+            out = torch.empty((n, REC8_BYTES), dtype=torch.uint8, device=arena.device)
+        self._check_dev(arena, off, lens, out)
+        _lib.check(self._lib.ingot_gpu_parse_compact(self._h, _ptr(arena), _ptr(off), _ptr(lens),
+                                                     n, int(chain), _ptr(out), _stream(stream)),
+                   "ingot_gpu_parse_compact")
+        return out
+
+    def parse_strided_compact(self, arena, stride: int, n: int, chain: Chain, lens=None,
+                              out=None, stream=None):
+        torch = _torch()
+        if out is None:
+            out = torch.empty((n, REC8_BYTES), dtype=torch.uint8, device=arena.device)
+        self._check_dev(arena, lens, out)
+        _lib.check(self._lib.ingot_gpu_parse_strided_compact(
+            self._h, _ptr(arena), int(stride), _ptr(lens), n, int(chain), _ptr(out),
+            _stream(stream)), "ingot_gpu_parse_strided_compact")
         return out
 
     def fields(self, arena, off, lens, chain: Chain, stride: int = 0, n: Optional[int] = None,

@@ -82,6 +82,17 @@ class IngotRec(ctypes.Structure):
     ]
 
 
+class IngotRec8(ctypes.Structure):
+    _fields_ = [
+        ("status_layer_l3", ctypes.c_uint8),
+        ("l4_vlan_flags", ctypes.c_uint8),
+        ("n_v6ext", ctypes.c_uint8),
+        ("l4_proto", ctypes.c_uint8),
+        ("l4_off", ctypes.c_uint16),
+        ("payload_off", ctypes.c_uint16),
+    ]
+
+
 class IngotV6Eh(ctypes.Structure):
     _fields_ = [
         ("ident", ctypes.c_uint32),
@@ -160,12 +171,33 @@ class IngotFields(ctypes.Structure):
 
 
 assert ctypes.sizeof(IngotRec) == 16
+assert ctypes.sizeof(IngotRec8) == 8
 assert ctypes.sizeof(IngotV6Eh) == 12
 assert ctypes.sizeof(IngotFields) == 256
 
 REC_DTYPE = np.dtype(IngotRec)
 FIELDS_DTYPE = np.dtype(IngotFields)
+REC8_DTYPE = np.dtype(IngotRec8)
 REC_BYTES = REC_DTYPE.itemsize
+REC8_BYTES = REC8_DTYPE.itemsize
+
+
+def rec16_to_rec8(rec: np.ndarray) -> np.ndarray:
+    """The ingot_rec8 encoding of ingot_rec records (include/ingot_gpu.h)."""
+    out = np.zeros(rec.shape, dtype=REC8_DTYPE)
+    st = rec["status"].astype(np.uint32)
+    layer = np.where(st != 0, rec["err_layer"].astype(np.uint32) & 3, 0)
+    out["status_layer_l3"] = ((st & 15) | (layer << 4) | (rec["l3_kind"].astype(np.uint32) << 6)
+                              ).astype(np.uint8)
+    out["l4_vlan_flags"] = (rec["l4_kind"].astype(np.uint32) | (rec["n_vlan"].astype(np.uint32)
+                            << 3) | ((rec["flags"].astype(np.uint32) & 1) << 5)).astype(np.uint8)
+    out["n_v6ext"] = rec["n_v6ext"]
+    out["l4_proto"] = rec["l4_proto"]
+    out["l4_off"] = rec["l4_off"]
+    out["payload_off"] = rec["payload_off"]
+    return out
+
+
 FIELDS_BYTES = FIELDS_DTYPE.itemsize
 
 

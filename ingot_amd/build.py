@@ -68,9 +68,16 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         if force or _stale(obj, [src] + headers):
             jobs.append((src, obj))
     if jobs:
-        with cf.ThreadPoolExecutor(max_workers=min(len(jobs), 4)) as ex:
-            for f in [ex.submit(_compile, s, o) for s, o in jobs]:
-                f.result()
+        try:
+            with cf.ThreadPoolExecutor(max_workers=min(len(jobs), 4)) as ex:
+                for f in [ex.submit(_compile, s, o) for s, o in jobs]:
+                    f.result()
+        except Exception:
+            # never leave a stale library behind a failed build
+            LIB.unlink(missing_ok=True)
+            for _, o in jobs:
+                o.unlink(missing_ok=True)
+            raise
     if force or jobs or _stale(LIB, objs):
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB)]
         cmd += [str(o) for o in objs]

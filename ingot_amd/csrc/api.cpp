@@ -75,30 +75,58 @@ void ingot_gpu_ctx_destroy(ingot_gpu_ctx* ctx) { delete ctx; }
 
 int ingot_gpu_ctx_device(const ingot_gpu_ctx* ctx) { return ctx ? ctx->device : -1; }
 
-int ingot_gpu_parse(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
-                    const uint16_t* d_len, uint64_t n, int chain, ingot_rec* d_out,
-                    void* stream) {
+static int parse_indexed(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
+                  const uint16_t* d_len, uint64_t n, int chain, void* d_out, int mode,
+                  void* stream) {
     if (!ctx || !chain_ok(chain)) return INGOT_GPU_EINVAL;
     if (n == 0) return INGOT_GPU_SUCCESS;
     if (!d_arena || !d_off || !d_len || !d_out) return INGOT_GPU_EINVAL;
     if (int e = enter(ctx)) return e;
-    ingot_gpu::ParseArgs a{d_arena, d_off, d_len, 0, n, d_out, nullptr};
-    return from_hip(ingot_gpu::launch_parse(a, ingot_gpu::LAYOUT_INDEXED, chain, false,
+    ingot_gpu::ParseArgs a{d_arena, d_off, d_len, 0, n, d_out};
+    return from_hip(ingot_gpu::launch_parse(a, ingot_gpu::LAYOUT_INDEXED, chain, mode,
                                             ctx->max_blocks, (hipStream_t)stream));
 }
 
-int ingot_gpu_parse_strided(ingot_gpu_ctx* ctx, const uint8_t* d_arena, uint32_t stride,
-                            const uint16_t* d_len, uint64_t n, int chain, ingot_rec* d_out,
-                            void* stream) {
+static int parse_strided(ingot_gpu_ctx* ctx, const uint8_t* d_arena, uint32_t stride,
+                  const uint16_t* d_len, uint64_t n, int chain, void* d_out, int mode,
+                  void* stream) {
     if (!ctx || !chain_ok(chain)) return INGOT_GPU_EINVAL;
     if (n == 0) return INGOT_GPU_SUCCESS;
     if (!d_arena || !d_out) return INGOT_GPU_EINVAL;
     if (stride == 0 || stride % 16u != 0 || stride > 65535u) return INGOT_GPU_ERANGE;
     if (((uintptr_t)d_arena & 15u) != 0) return INGOT_GPU_EINVAL;
     if (int e = enter(ctx)) return e;
-    ingot_gpu::ParseArgs a{d_arena, nullptr, d_len, stride, n, d_out, nullptr};
-    return from_hip(ingot_gpu::launch_parse(a, ingot_gpu::LAYOUT_STRIDED, chain, false,
+    ingot_gpu::ParseArgs a{d_arena, nullptr, d_len, stride, n, d_out};
+    return from_hip(ingot_gpu::launch_parse(a, ingot_gpu::LAYOUT_STRIDED, chain, mode,
                                             ctx->max_blocks, (hipStream_t)stream));
+}
+
+int ingot_gpu_parse(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
+                    const uint16_t* d_len, uint64_t n, int chain, ingot_rec* d_out,
+                    void* stream) {
+    return parse_indexed(ctx, d_arena, d_off, d_len, n, chain, d_out, ingot_gpu::OUT_REC16,
+                         stream);
+}
+
+int ingot_gpu_parse_strided(ingot_gpu_ctx* ctx, const uint8_t* d_arena, uint32_t stride,
+                            const uint16_t* d_len, uint64_t n, int chain, ingot_rec* d_out,
+                            void* stream) {
+    return parse_strided(ctx, d_arena, stride, d_len, n, chain, d_out, ingot_gpu::OUT_REC16,
+                         stream);
+}
+
+int ingot_gpu_parse_compact(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
+                            const uint16_t* d_len, uint64_t n, int chain, ingot_rec8* d_out,
+                            void* stream) {
+    return parse_indexed(ctx, d_arena, d_off, d_len, n, chain, d_out, ingot_gpu::OUT_REC8,
+                         stream);
+}
+
+int ingot_gpu_parse_strided_compact(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
+                                    uint32_t stride, const uint16_t* d_len, uint64_t n,
+                                    int chain, ingot_rec8* d_out, void* stream) {
+    return parse_strided(ctx, d_arena, stride, d_len, n, chain, d_out, ingot_gpu::OUT_REC8,
+                         stream);
 }
 
 int ingot_gpu_fields(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
@@ -116,9 +144,9 @@ int ingot_gpu_fields(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t*
         return INGOT_GPU_EINVAL;
     }
     if (int e = enter(ctx)) return e;
-    ingot_gpu::ParseArgs a{d_arena, d_off, d_len, stride, n, nullptr, d_out};
-    return from_hip(
-        ingot_gpu::launch_parse(a, layout, chain, true, ctx->max_blocks, (hipStream_t)stream));
+    ingot_gpu::ParseArgs a{d_arena, d_off, d_len, stride, n, d_out};
+    return from_hip(ingot_gpu::launch_parse(a, layout, chain, ingot_gpu::OUT_FIELDS,
+                                            ctx->max_blocks, (hipStream_t)stream));
 }
 
 const char* ingot_gpu_strerror(int code) {

@@ -11,18 +11,20 @@ namespace ingot_gpu {
 
 enum LayoutKind { LAYOUT_STRIDED = 0, LAYOUT_INDEXED = 1 };
 
+// Output mode: 16-B ingot_rec, 8-B ingot_rec8, or 256-B ingot_fields.
+enum OutMode { OUT_REC16 = 0, OUT_REC8 = 1, OUT_FIELDS = 2 };
+
 struct ParseArgs {
     const uint8_t* arena;
     const uint64_t* off;   // LAYOUT_INDEXED
     const uint16_t* len;   // optional for LAYOUT_STRIDED
     uint32_t stride;       // LAYOUT_STRIDED
     uint64_t n;
-    ingot_rec* out;        // record mode
-    ingot_fields* fields;  // parity mode
+    void* out;             // n records of the OutMode's type
 };
 
-// max_blocks = 0 lets the launcher size the grid (persistent, LDS-limited).
-hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, bool fields,
+// max_blocks = 0 lets the launcher size the grid.
+hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, int mode,
                         uint32_t max_blocks, hipStream_t s);
 
 }  // namespace ingot_gpu

@@ -86,9 +86,19 @@ struct Frame {
             const uint32_t x = __builtin_amdgcn_alignbyte(d1, d0, b & 3u);  // bytes b.. little-endian
             v = __builtin_bswap32(x) >> (32u - 8u * n);
         } else {
-            v = 0;
-            for (uint32_t k = 0; k < n; ++k) v = (v << 8) | g[i + k];
+            v = beyond(i, n);
         }
+        return v;
+    }
+
+    // Bytes past the staged window (long option / EH chains), read straight
+    // from HBM by the lanes that need them.  Byte loads: measured faster on
+    // config 3 than aligned 16-B loads + lane selects (566 vs 659 us/step),
+    // since scattered per-lane 16-B requests cost 16x the texture-path work
+    // for the same one DRAM sector.
+    __device__ __forceinline__ uint32_t beyond(uint32_t i, uint32_t n) const {
+        uint32_t v = 0;
+        for (uint32_t k = 0; k < n; ++k) v = (v << 8) | g[i + k];
         return v;
     }
 
@@ -102,6 +112,17 @@ struct Rec {
     uint32_t status, err_layer, l3_kind, l4_kind, n_vlan, n_v6ext, l4_proto, flags;
     uint32_t l3_off, l4_off, payload_off, ethertype;
 };
+
+__device__ __forceinline__ uint2 pack8(const Rec& r) {
+    // ingot_rec8 (include/ingot_gpu.h)
+    const uint32_t layer = r.status ? (r.err_layer & 3u) : 0u;
+    uint2 o;
+    o.x = (r.status & 15u) | (layer << 4) | (r.l3_kind << 6) |
+          ((r.l4_kind | (r.n_vlan << 3) | ((r.flags & 1u) << 5)) << 8) | (r.n_v6ext << 16) |
+          (r.l4_proto << 24);
+    o.y = (r.l4_off & 0xffffu) | (r.payload_off << 16);
+    return o;
+}
 
 __device__ __forceinline__ uint4 pack(const Rec& r) {
     uint4 o;
@@ -362,7 +383,7 @@ __device__ __forceinline__ void walk(const FR& f, Rec& r, ingot_fields* F) {
 // ---------------------------------------------------------------------------
 // Kernel.
 // ---------------------------------------------------------------------------
-template <uint32_t NCH, int LAYOUT, int CHAIN, bool FIELDS>
+template <uint32_t NCH, int LAYOUT, int CHAIN, int MODE>
 __global__ __launch_bounds__(BLOCK) void k_parse(ParseArgs a) {
     constexpr uint32_t WIN = NCH * 16u;
     constexpr uint32_t WAVE_DW = WAVE * NCH * 4u;  // dwords per wave image
@@ -416,8 +437,8 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ParseArgs a) {
 
         Frame<NCH> fr{(const lds_u32*)wimg, lane, sh, take, len, a.arena + off};
         Rec r;
-        if constexpr (FIELDS) {
-            ingot_fields* F = a.fields + (valid ? i : 0);
+        if constexpr (MODE == OUT_FIELDS) {
+            ingot_fields* F = static_cast<ingot_fields*>(a.out) + (valid ? i : 0);
             if (valid) {
                 uint4* z = reinterpret_cast<uint4*>(F);
 #pragma unroll
@@ -425,63 +446,88 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ParseArgs a) {
                 walk<CHAIN, true>(fr, r, F);
                 reinterpret_cast<uint4*>(F)[0] = pack(r);
             }
+        } else if constexpr (MODE == OUT_REC8) {
+            walk<CHAIN, false>(fr, r, nullptr);
+            if (valid) static_cast<uint2*>(a.out)[i] = pack8(r);
         } else {
             walk<CHAIN, false>(fr, r, nullptr);
-            if (valid) reinterpret_cast<uint4*>(a.out)[i] = pack(r);
+            if (valid) static_cast<uint4*>(a.out)[i] = pack(r);
         }
         // The next tile's LDS-DMA overwrites this image: every lane's reads
         // above have returned (their values were consumed by the store).
     }
 }
 
-template <uint32_t NCH, int LAYOUT, bool FIELDS>
+template <uint32_t NCH, int LAYOUT, int MODE>
 hipError_t launch_chain(const ParseArgs& a, int chain, uint32_t grid, hipStream_t s) {
     switch (chain) {
     case INGOT_CHAIN_UDP_PARSER:
-        hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_UDP_PARSER, FIELDS>), dim3(grid),
+        hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_UDP_PARSER, MODE>), dim3(grid),
                            dim3(BLOCK), 0, s, a);
         break;
     case INGOT_CHAIN_GENERIC_ULP:
-        hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_GENERIC_ULP, FIELDS>), dim3(grid),
+        hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_GENERIC_ULP, MODE>), dim3(grid),
                            dim3(BLOCK), 0, s, a);
         break;
     default:
-        hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_VLAN_ULP, FIELDS>), dim3(grid),
+        hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_VLAN_ULP, MODE>), dim3(grid),
                            dim3(BLOCK), 0, s, a);
         break;
     }
     return hipGetLastError();
 }
 
-uint32_t grid_for(uint64_t n, uint32_t lds_bytes_per_block, uint32_t max_blocks) {
+template <uint32_t NCH, int LAYOUT>
+hipError_t launch_mode(const ParseArgs& a, int chain, int mode, uint32_t grid, hipStream_t s) {
+    switch (mode) {
+    case OUT_REC8: return launch_chain<NCH, LAYOUT, OUT_REC8>(a, chain, grid, s);
+    case OUT_FIELDS: return launch_chain<NCH, LAYOUT, OUT_FIELDS>(a, chain, grid, s);
+    default: return launch_chain<NCH, LAYOUT, OUT_REC16>(a, chain, grid, s);
+    }
+}
+
+// Grid: one 64-packet tile per wave (4 waves per block) up to `cap` blocks;
+// larger batches grid-stride.  Measured on MI355X at config-2 size: one tile
+// per wave beats 2 tiles per wave by ~2.5% (tools/microbench.py).
+uint32_t grid_for(uint64_t n, uint32_t max_blocks) {
     const uint64_t tiles = (n + WAVE - 1) / WAVE;
     const uint64_t want = (tiles + WAVES - 1) / WAVES;
-    uint32_t per_cu = 163840u / (lds_bytes_per_block ? lds_bytes_per_block : 1u);
-    if (per_cu > 8u) per_cu = 8u;
-    if (per_cu < 1u) per_cu = 1u;
-    uint64_t cap = max_blocks ? max_blocks : 256ull * per_cu;
-    uint64_t g = want < cap ? want : cap;
+    const uint64_t cap = max_blocks ? max_blocks : 65536ull;
+    const uint64_t g = want < cap ? want : cap;
     return (uint32_t)(g ? g : 1);
 }
 
 }  // namespace
 
-hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, bool fields,
+hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, int mode,
                         uint32_t max_blocks, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
+    const uint32_t g = grid_for(a.n, max_blocks);
+    // Staged window (16-B chunks per frame), measured on MI355X:
+    //  * packed frames (random alignment): 5 chunks = 2 DRAM sectors; larger
+    //    windows over-fetch a third sector and cut occupancy (LDS), smaller
+    //    ones send too many lanes to HBM for the L4 header.  C3: 566 us/step at
+    //    5 chunks vs 758 at 9.
+    //  * slots (16-B aligned): 8 chunks = exactly 2 sectors; 4 chunks when the
+    //    slot is <= 64 B.
+    // INGOT_GPU_WIN_INDEXED / INGOT_GPU_WIN_STRIDED override (4, 5, 6, 8, 9).
+    static const int win_i = [] {
+        const char* w = getenv("INGOT_GPU_WIN_INDEXED");
+        return w ? atoi(w) : 5;
+    }();
+    static const int win_s = [] {
+        const char* w = getenv("INGOT_GPU_WIN_STRIDED");
+        return w ? atoi(w) : 8;
+    }();
     if (layout_kind == LAYOUT_STRIDED) {
-        if (a.stride <= 64u) {
-            const uint32_t g = grid_for(a.n, WAVES * WAVE * 4u * 16u, max_blocks);
-            return fields ? launch_chain<4, LAYOUT_STRIDED, true>(a, chain, g, s)
-                          : launch_chain<4, LAYOUT_STRIDED, false>(a, chain, g, s);
-        }
-        const uint32_t g = grid_for(a.n, WAVES * WAVE * 8u * 16u, max_blocks);
-        return fields ? launch_chain<8, LAYOUT_STRIDED, true>(a, chain, g, s)
-                      : launch_chain<8, LAYOUT_STRIDED, false>(a, chain, g, s);
+        if (a.stride <= 64u || win_s == 4) return launch_mode<4, LAYOUT_STRIDED>(a, chain, mode, g, s);
+        if (win_s == 5) return launch_mode<5, LAYOUT_STRIDED>(a, chain, mode, g, s);
+        return launch_mode<8, LAYOUT_STRIDED>(a, chain, mode, g, s);
     }
-    const uint32_t g = grid_for(a.n, WAVES * WAVE * 9u * 16u, max_blocks);
-    return fields ? launch_chain<9, LAYOUT_INDEXED, true>(a, chain, g, s)
-                  : launch_chain<9, LAYOUT_INDEXED, false>(a, chain, g, s);
+    if (win_i == 4) return launch_mode<4, LAYOUT_INDEXED>(a, chain, mode, g, s);
+    if (win_i == 6) return launch_mode<6, LAYOUT_INDEXED>(a, chain, mode, g, s);
+    if (win_i == 9) return launch_mode<9, LAYOUT_INDEXED>(a, chain, mode, g, s);
+    return launch_mode<5, LAYOUT_INDEXED>(a, chain, mode, g, s);
 }
 
 }  // namespace ingot_gpu

@@ -10,7 +10,8 @@ import pytest
 
 import ingot_amd
 from ingot_amd import _lib
-from ingot_amd.abi import CHAIN_LABELS, FIELDS_DTYPE, REC_DTYPE, Chain, IngotFields, IngotRec
+from ingot_amd.abi import (CHAIN_LABELS, FIELDS_DTYPE, REC8_DTYPE, REC_DTYPE, Chain, IngotFields,
+                           IngotRec, IngotRec8)
 
 ROOT = Path(__file__).resolve().parent.parent
 
@@ -49,6 +50,7 @@ def test_layouts_match_c(tmp_path):
     """Compile a probe against include/ingot_gpu.h and compare every offset."""
     fields = [f[0] for f in IngotFields._fields_]
     rec_fields = [f[0] for f in IngotRec._fields_]
+    rec8_fields = [f[0] for f in IngotRec8._fields_]
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "ingot_gpu.h"',
              "int main(void){",
              'printf("rec %zu\\n", sizeof(ingot_rec));',
@@ -57,6 +59,9 @@ def test_layouts_match_c(tmp_path):
         lines.append(f'printf("rec.{f} %zu\\n", offsetof(ingot_rec, {f}));')
     for f in fields:
         lines.append(f'printf("fields.{f} %zu\\n", offsetof(ingot_fields, {f}));')
+    for f in rec8_fields:
+        lines.append(f'printf("rec8.{f} %zu\\n", offsetof(ingot_rec8, {f}));')
+    lines.append('printf("rec8 %zu\\n", sizeof(ingot_rec8));')
     lines.append("return 0;}")
     src = tmp_path / "probe.c"
     src.write_text("\n".join(lines))
@@ -69,6 +74,9 @@ def test_layouts_match_c(tmp_path):
     assert int(got["fields"]) == FIELDS_DTYPE.itemsize == 256
     for f in rec_fields:
         assert int(got[f"rec.{f}"]) == getattr(IngotRec, f).offset, f
+    assert int(got["rec8"]) == REC8_DTYPE.itemsize == 8
+    for f in rec8_fields:
+        assert int(got[f"rec8.{f}"]) == getattr(IngotRec8, f).offset, f
     for f in fields:
         assert int(got[f"fields.{f}"]) == getattr(IngotFields, f).offset, f
 
@@ -95,6 +103,8 @@ def test_argument_validation_without_gpu(lib):
     assert lib.ingot_gpu_parse(null, None, None, None, 10, 0, None, None) == -1
     assert lib.ingot_gpu_parse_strided(null, None, 64, None, 10, 0, None, None) == -1
     assert lib.ingot_gpu_fields(null, None, None, None, 64, 10, 0, None, None) == -1
+    assert lib.ingot_gpu_parse_compact(null, None, None, None, 10, 0, None, None) == -1
+    assert lib.ingot_gpu_parse_strided_compact(null, None, 64, None, 10, 0, None, None) == -1
     assert lib.ingot_pktgen_fill(0, 1, 0, 1, None, 0, None, None, 0, None) == -1
     assert lib.ingot_gpu_strerror(-1) == b"invalid argument"
 

@@ -166,6 +166,27 @@ def test_v4udp64_full_batch_exact(ctx, torch):
     assert (g["payload_off"] == 42).all() and (g["l4_kind"] == 2).all()
 
 
+@pytest.mark.parametrize("layout", ["indexed", "strided"])
+def test_compact_records_bit_exact(ctx, torch, layout):
+    """ingot_rec8 == the documented encoding of the oracle's ingot_rec."""
+    n = 150_001
+    for chain in Chain:
+        if layout == "indexed":
+            arena, off, lens = ingot_amd.gen_frames(GenProfile.ADVERSARIAL, n, seed=21)
+            got = ctx.parse_compact(arena, off, lens, chain)
+            want = oracle.parse_batch(host(arena), host(off), host(lens), chain, nthreads=8)
+        else:
+            arena, _, lens = ingot_amd.gen_frames(GenProfile.VLAN_V6EH, n, seed=22, stride=128)
+            got = ctx.parse_strided_compact(arena, 128, n, chain, lens=lens)
+            want = oracle.parse_batch(host(arena), None, host(lens), chain, stride=128, n=n,
+                                      nthreads=8)
+        torch.cuda.synchronize()
+        w8 = ingot_amd.rec16_to_rec8(want)
+        g = got.cpu().numpy().reshape(n, 8)
+        bad = np.nonzero((g != w8.view(np.uint8).reshape(n, 8)).any(axis=1))[0]
+        assert bad.size == 0, (chain, bad[:5])
+
+
 @pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 1000])
 def test_small_and_ragged_batches(ctx, torch, n):
     arena, off, lens = ingot_amd.gen_frames(GenProfile.ADVERSARIAL, max(n, 1), seed=n + 1)
