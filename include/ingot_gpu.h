@@ -261,6 +261,22 @@ void ingot_gpu_ctx_destroy(ingot_gpu_ctx* ctx);
 int ingot_gpu_ctx_device(const ingot_gpu_ctx* ctx);
 
 /*
+ * Tuning knobs (results never depend on them).  Defaults are the measured
+ * best on MI355X; value 0 restores the default.
+ *   INGOT_TUNE_WINDOW_INDEXED  16-B chunks staged in LDS per packed frame:
+ *                              2,3,4,5,6,8,9, or 100 = no staging (default 3)
+ *   INGOT_TUNE_WINDOW_STRIDED  16-B chunks staged per slot: 2,3,4,5,8 or 100
+ *                              (default 4 for slots <= 64 B, else 3)
+ *   INGOT_TUNE_MAX_BLOCKS      grid cap in 256-thread blocks (0 = one
+ *                              64-packet tile per wave)
+ */
+#define INGOT_TUNE_WINDOW_INDEXED 1
+#define INGOT_TUNE_WINDOW_STRIDED 2
+#define INGOT_TUNE_MAX_BLOCKS 3
+int ingot_gpu_ctx_set_tuning(ingot_gpu_ctx* ctx, int key, int value);
+int ingot_gpu_ctx_get_tuning(const ingot_gpu_ctx* ctx, int key);
+
+/*
  * Batched `<Chain>::parse_slice` over frames in a device arena.
  *
  *   d_arena   device pointer to the packet bytes

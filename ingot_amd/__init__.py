@@ -105,6 +105,14 @@ class Context:
 
     __del__ = close
 
+    def set_tuning(self, key: int, value: int) -> None:
+        """INGOT_TUNE_* knobs (window sizes, grid cap); never change results."""
+        _lib.check(self._lib.ingot_gpu_ctx_set_tuning(self._h, int(key), int(value)),
+                   "ingot_gpu_ctx_set_tuning")
+
+    def get_tuning(self, key: int) -> int:
+        return int(self._lib.ingot_gpu_ctx_get_tuning(self._h, int(key)))
+
     def _check_dev(self, *tensors) -> None:
         for t in tensors:
             if t is not None and (not t.is_cuda or t.device.index != self.device):

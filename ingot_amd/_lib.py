@@ -21,6 +21,8 @@ SIGNATURES = {
     "ingot_gpu_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "ingot_gpu_ctx_destroy": (None, [ctypes.c_void_p]),
     "ingot_gpu_ctx_device": (ctypes.c_int, [ctypes.c_void_p]),
+    "ingot_gpu_ctx_set_tuning": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "ingot_gpu_ctx_get_tuning": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ingot_gpu_parse": (
         ctypes.c_int,
         [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, c_u64, ctypes.c_int, c_u8p, ctypes.c_void_p],

@@ -64,6 +64,11 @@ class L4Kind(enum.IntEnum):
 REC_ACCEPTED = 0x01
 MAX_EH_FIELDS = 4
 
+# ingot_gpu_ctx_set_tuning keys
+TUNE_WINDOW_INDEXED = 1
+TUNE_WINDOW_STRIDED = 2
+TUNE_MAX_BLOCKS = 3
+
 
 class IngotRec(ctypes.Structure):
     _fields_ = [

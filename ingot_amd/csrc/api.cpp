@@ -16,7 +16,7 @@
 
 struct ingot_gpu_ctx {
     int device;
-    uint32_t max_blocks;  // 0 = automatic grid sizing (INGOT_GPU_MAX_BLOCKS overrides)
+    ingot_gpu::Tuning tuning;
 };
 
 namespace {
@@ -43,6 +43,37 @@ int enter(const ingot_gpu_ctx* ctx) {
     return INGOT_GPU_SUCCESS;
 }
 
+int stride_ok(const uint8_t* d_arena, uint32_t stride) {
+    if (stride == 0 || stride % 16u != 0 || stride > 65535u) return INGOT_GPU_ERANGE;
+    if (((uintptr_t)d_arena & 15u) != 0) return INGOT_GPU_EINVAL;
+    return INGOT_GPU_SUCCESS;
+}
+
+int parse_indexed(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
+                  const uint16_t* d_len, uint64_t n, int chain, void* d_out, int mode,
+                  void* stream) {
+    if (!ctx || !chain_ok(chain)) return INGOT_GPU_EINVAL;
+    if (n == 0) return INGOT_GPU_SUCCESS;
+    if (!d_arena || !d_off || !d_len || !d_out) return INGOT_GPU_EINVAL;
+    if (int e = enter(ctx)) return e;
+    ingot_gpu::ParseArgs a{d_arena, d_off, d_len, 0, n, d_out};
+    return from_hip(ingot_gpu::launch_parse(a, ingot_gpu::LAYOUT_INDEXED, chain, mode,
+                                            ctx->tuning, (hipStream_t)stream));
+}
+
+int parse_strided(ingot_gpu_ctx* ctx, const uint8_t* d_arena, uint32_t stride,
+                  const uint16_t* d_len, uint64_t n, int chain, void* d_out, int mode,
+                  void* stream) {
+    if (!ctx || !chain_ok(chain)) return INGOT_GPU_EINVAL;
+    if (n == 0) return INGOT_GPU_SUCCESS;
+    if (!d_arena || !d_out) return INGOT_GPU_EINVAL;
+    if (int e = stride_ok(d_arena, stride)) return e;
+    if (int e = enter(ctx)) return e;
+    ingot_gpu::ParseArgs a{d_arena, nullptr, d_len, stride, n, d_out};
+    return from_hip(ingot_gpu::launch_parse(a, ingot_gpu::LAYOUT_STRIDED, chain, mode,
+                                            ctx->tuning, (hipStream_t)stream));
+}
+
 }  // namespace
 
 extern "C" {
@@ -64,9 +95,8 @@ int ingot_gpu_ctx_create(int device, ingot_gpu_ctx** out) {
     // Code objects are built for gfx950 only.
     if (prop.gcnArchName[0] && std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         return INGOT_GPU_ENODEV;
-    ingot_gpu_ctx* c = new (std::nothrow) ingot_gpu_ctx{device, 0};
+    ingot_gpu_ctx* c = new (std::nothrow) ingot_gpu_ctx{device, {}};
     if (!c) return INGOT_GPU_ENOMEM;
-    if (const char* mb = std::getenv("INGOT_GPU_MAX_BLOCKS")) c->max_blocks = (uint32_t)std::atoi(mb);
     *out = c;
     return INGOT_GPU_SUCCESS;
 }
@@ -75,30 +105,24 @@ void ingot_gpu_ctx_destroy(ingot_gpu_ctx* ctx) { delete ctx; }
 
 int ingot_gpu_ctx_device(const ingot_gpu_ctx* ctx) { return ctx ? ctx->device : -1; }
 
-static int parse_indexed(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
-                  const uint16_t* d_len, uint64_t n, int chain, void* d_out, int mode,
-                  void* stream) {
-    if (!ctx || !chain_ok(chain)) return INGOT_GPU_EINVAL;
-    if (n == 0) return INGOT_GPU_SUCCESS;
-    if (!d_arena || !d_off || !d_len || !d_out) return INGOT_GPU_EINVAL;
-    if (int e = enter(ctx)) return e;
-    ingot_gpu::ParseArgs a{d_arena, d_off, d_len, 0, n, d_out};
-    return from_hip(ingot_gpu::launch_parse(a, ingot_gpu::LAYOUT_INDEXED, chain, mode,
-                                            ctx->max_blocks, (hipStream_t)stream));
+int ingot_gpu_ctx_set_tuning(ingot_gpu_ctx* ctx, int key, int value) {
+    if (!ctx || !ingot_gpu::tuning_valid(key, value)) return INGOT_GPU_EINVAL;
+    switch (key) {
+    case INGOT_TUNE_WINDOW_INDEXED: ctx->tuning.window_indexed = value; break;
+    case INGOT_TUNE_WINDOW_STRIDED: ctx->tuning.window_strided = value; break;
+    default: ctx->tuning.max_blocks = (uint32_t)value; break;
+    }
+    return INGOT_GPU_SUCCESS;
 }
 
-static int parse_strided(ingot_gpu_ctx* ctx, const uint8_t* d_arena, uint32_t stride,
-                  const uint16_t* d_len, uint64_t n, int chain, void* d_out, int mode,
-                  void* stream) {
-    if (!ctx || !chain_ok(chain)) return INGOT_GPU_EINVAL;
-    if (n == 0) return INGOT_GPU_SUCCESS;
-    if (!d_arena || !d_out) return INGOT_GPU_EINVAL;
-    if (stride == 0 || stride % 16u != 0 || stride > 65535u) return INGOT_GPU_ERANGE;
-    if (((uintptr_t)d_arena & 15u) != 0) return INGOT_GPU_EINVAL;
-    if (int e = enter(ctx)) return e;
-    ingot_gpu::ParseArgs a{d_arena, nullptr, d_len, stride, n, d_out};
-    return from_hip(ingot_gpu::launch_parse(a, ingot_gpu::LAYOUT_STRIDED, chain, mode,
-                                            ctx->max_blocks, (hipStream_t)stream));
+int ingot_gpu_ctx_get_tuning(const ingot_gpu_ctx* ctx, int key) {
+    if (!ctx) return INGOT_GPU_EINVAL;
+    switch (key) {
+    case INGOT_TUNE_WINDOW_INDEXED: return ctx->tuning.window_indexed;
+    case INGOT_TUNE_WINDOW_STRIDED: return ctx->tuning.window_strided;
+    case INGOT_TUNE_MAX_BLOCKS: return (int)ctx->tuning.max_blocks;
+    default: return INGOT_GPU_EINVAL;
+    }
 }
 
 int ingot_gpu_parse(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
@@ -132,21 +156,11 @@ int ingot_gpu_parse_strided_compact(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
 int ingot_gpu_fields(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
                      const uint16_t* d_len, uint32_t stride, uint64_t n, int chain,
                      ingot_fields* d_out, void* stream) {
-    if (!ctx || !chain_ok(chain)) return INGOT_GPU_EINVAL;
-    if (n == 0) return INGOT_GPU_SUCCESS;
-    if (!d_arena || !d_out) return INGOT_GPU_EINVAL;
-    int layout = ingot_gpu::LAYOUT_INDEXED;
-    if (!d_off) {
-        if (stride == 0 || stride % 16u != 0 || stride > 65535u) return INGOT_GPU_ERANGE;
-        if (((uintptr_t)d_arena & 15u) != 0) return INGOT_GPU_EINVAL;
-        layout = ingot_gpu::LAYOUT_STRIDED;
-    } else if (!d_len) {
-        return INGOT_GPU_EINVAL;
-    }
-    if (int e = enter(ctx)) return e;
-    ingot_gpu::ParseArgs a{d_arena, d_off, d_len, stride, n, d_out};
-    return from_hip(ingot_gpu::launch_parse(a, layout, chain, ingot_gpu::OUT_FIELDS,
-                                            ctx->max_blocks, (hipStream_t)stream));
+    if (d_off)
+        return parse_indexed(ctx, d_arena, d_off, d_len, n, chain, d_out, ingot_gpu::OUT_FIELDS,
+                             stream);
+    return parse_strided(ctx, d_arena, stride, d_len, n, chain, d_out, ingot_gpu::OUT_FIELDS,
+                         stream);
 }
 
 const char* ingot_gpu_strerror(int code) {

@@ -23,8 +23,15 @@ struct ParseArgs {
     void* out;             // n records of the OutMode's type
 };
 
-// max_blocks = 0 lets the launcher size the grid.
+// Per-context tuning (0 = measured default); see INGOT_TUNE_* in ingot_gpu.h.
+struct Tuning {
+    int window_indexed = 0;
+    int window_strided = 0;
+    uint32_t max_blocks = 0;
+};
+
 hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, int mode,
-                        uint32_t max_blocks, hipStream_t s);
+                        const Tuning& t, hipStream_t s);
+bool tuning_valid(int key, int value);
 
 }  // namespace ingot_gpu

@@ -388,6 +388,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ParseArgs a) {
     constexpr uint32_t WIN = NCH * 16u;
     constexpr uint32_t WAVE_DW = WAVE * NCH * 4u;  // dwords per wave image
     // +16 dwords: the second dword of a pair read may run past the last image.
+    // NCH = 0: no staging, every read goes to L2/HBM.
     __shared__ __attribute__((aligned(16))) uint32_t s_win[WAVES * WAVE_DW + 16];
 
     const uint32_t lane = threadIdx.x & (WAVE - 1u);
@@ -411,16 +412,17 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ParseArgs a) {
         }
         const uint64_t base = off & ~(uint64_t)15;
         const uint32_t sh = (uint32_t)(off & 15u);
-        const uint32_t take = len < WIN - sh ? len : WIN - sh;
+        const uint32_t take = NCH == 0 ? 0u : (len < WIN - sh ? len : WIN - sh);
         const uint32_t nch = (sh + take + 15u) >> 4;
 
         // Stage: instruction k, lane L fills LDS slot q = 64k + L, i.e.
         // packet p = q / NCH, swizzled chunk c.  (LDS-DMA: lane-linear image.)
 #pragma unroll
-        for (uint32_t k = 0; k < NCH; ++k) {
+        for (uint32_t k = 0; k < (NCH ? NCH : 1u) && NCH; ++k) {
             const uint32_t q = k * WAVE + lane;
-            const uint32_t pp = q / NCH;
-            const uint32_t c = (q - pp * NCH) ^ swz<NCH>(pp);
+            constexpr uint32_t NCH1 = NCH ? NCH : 1u;
+            const uint32_t pp = q / NCH1;
+            const uint32_t c = (q - pp * NCH1) ^ swz<NCH>(pp);
             const uint32_t np = (uint32_t)__shfl((int)nch, (int)pp);
             uint64_t bp;
             if constexpr (LAYOUT == LAYOUT_STRIDED) {
@@ -500,34 +502,50 @@ uint32_t grid_for(uint64_t n, uint32_t max_blocks) {
 }  // namespace
 
 hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, int mode,
-                        uint32_t max_blocks, hipStream_t s) {
+                        const Tuning& t, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
-    const uint32_t g = grid_for(a.n, max_blocks);
-    // Staged window (16-B chunks per frame), measured on MI355X:
-    //  * packed frames (random alignment): 5 chunks = 2 DRAM sectors; larger
-    //    windows over-fetch a third sector and cut occupancy (LDS), smaller
-    //    ones send too many lanes to HBM for the L4 header.  C3: 566 us/step at
-    //    5 chunks vs 758 at 9.
-    //  * slots (16-B aligned): 8 chunks = exactly 2 sectors; 4 chunks when the
-    //    slot is <= 64 B.
-    // INGOT_GPU_WIN_INDEXED / INGOT_GPU_WIN_STRIDED override (4, 5, 6, 8, 9).
-    static const int win_i = [] {
-        const char* w = getenv("INGOT_GPU_WIN_INDEXED");
-        return w ? atoi(w) : 5;
-    }();
-    static const int win_s = [] {
-        const char* w = getenv("INGOT_GPU_WIN_STRIDED");
-        return w ? atoi(w) : 8;
-    }();
+    const uint32_t g = grid_for(a.n, t.max_blocks);
+    // Staged window (16-B chunks per frame); defaults measured on MI355X with
+    // interleaved A/B in one process (tools/abtune.py):
+    //  * packed frames: 3 chunks (C3 595-598 us/step at 2-3 chunks, 614 at 4,
+    //    637 at 5, 838 at 9, 648 with no staging);
+    //  * slots > 64 B: 3 chunks (C3s 127 us vs 169 at 8); slots <= 64 B: the
+    //    whole 64-B slot (4 chunks; C2 is flat from 2 to 4 chunks).
+    // Small windows win: they fetch only the header lines and keep LDS per
+    // wave low; the rest of a long chain is read from L2/HBM on demand.
     if (layout_kind == LAYOUT_STRIDED) {
-        if (a.stride <= 64u || win_s == 4) return launch_mode<4, LAYOUT_STRIDED>(a, chain, mode, g, s);
-        if (win_s == 5) return launch_mode<5, LAYOUT_STRIDED>(a, chain, mode, g, s);
+        const int w = t.window_strided ? t.window_strided : (a.stride <= 64u ? 4 : 3);
+        if (w == 100) return launch_mode<0, LAYOUT_STRIDED>(a, chain, mode, g, s);
+        if (w == 2) return launch_mode<2, LAYOUT_STRIDED>(a, chain, mode, g, s);
+        if (w == 3) return launch_mode<3, LAYOUT_STRIDED>(a, chain, mode, g, s);
+        if (w == 4) return launch_mode<4, LAYOUT_STRIDED>(a, chain, mode, g, s);
+        if (w == 5) return launch_mode<5, LAYOUT_STRIDED>(a, chain, mode, g, s);
         return launch_mode<8, LAYOUT_STRIDED>(a, chain, mode, g, s);
     }
-    if (win_i == 4) return launch_mode<4, LAYOUT_INDEXED>(a, chain, mode, g, s);
-    if (win_i == 6) return launch_mode<6, LAYOUT_INDEXED>(a, chain, mode, g, s);
-    if (win_i == 9) return launch_mode<9, LAYOUT_INDEXED>(a, chain, mode, g, s);
-    return launch_mode<5, LAYOUT_INDEXED>(a, chain, mode, g, s);
+    switch (t.window_indexed ? t.window_indexed : 3) {
+    case 100: return launch_mode<0, LAYOUT_INDEXED>(a, chain, mode, g, s);
+    case 2: return launch_mode<2, LAYOUT_INDEXED>(a, chain, mode, g, s);
+    case 3: return launch_mode<3, LAYOUT_INDEXED>(a, chain, mode, g, s);
+    case 4: return launch_mode<4, LAYOUT_INDEXED>(a, chain, mode, g, s);
+    case 6: return launch_mode<6, LAYOUT_INDEXED>(a, chain, mode, g, s);
+    case 8: return launch_mode<8, LAYOUT_INDEXED>(a, chain, mode, g, s);
+    case 9: return launch_mode<9, LAYOUT_INDEXED>(a, chain, mode, g, s);
+    default: return launch_mode<5, LAYOUT_INDEXED>(a, chain, mode, g, s);
+    }
+}
+
+bool tuning_valid(int key, int value) {
+    switch (key) {
+    case INGOT_TUNE_WINDOW_INDEXED:
+        return value == 0 || (value >= 2 && value <= 6) || value == 8 || value == 9 ||
+               value == 100;
+    case INGOT_TUNE_WINDOW_STRIDED:
+        return value == 0 || (value >= 2 && value <= 5) || value == 8 || value == 100;
+    case INGOT_TUNE_MAX_BLOCKS:
+        return value >= 0;
+    default:
+        return false;
+    }
 }
 
 }  // namespace ingot_gpu

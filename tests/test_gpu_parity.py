@@ -187,6 +187,34 @@ def test_compact_records_bit_exact(ctx, torch, layout):
         assert bad.size == 0, (chain, bad[:5])
 
 
+def test_every_window_setting_is_bit_exact(torch):
+    """Tuning never changes results: every staged-window size (incl. no
+    staging, where every byte comes through the HBM path) on fuzz frames."""
+    from ingot_amd.abi import TUNE_WINDOW_INDEXED, TUNE_WINDOW_STRIDED
+
+    arena, off, lens = ingot_amd.gen_frames(GenProfile.ADVERSARIAL, 60_000, seed=31)
+    sarena, _, slens = ingot_amd.gen_frames(GenProfile.VLAN_V6EH, 40_000, seed=32, stride=256)
+    want_i = {c: oracle.parse_batch(host(arena), host(off), host(lens), c, fields=True,
+                                    nthreads=8) for c in Chain}
+    want_s = {c: oracle.parse_batch(host(sarena), None, host(slens), c, stride=256, n=40_000,
+                                    fields=True, nthreads=8) for c in Chain}
+    for w in (2, 3, 4, 5, 6, 8, 9, 100):
+        c = ingot_amd.Context(0)
+        c.set_tuning(TUNE_WINDOW_INDEXED, w)
+        if w != 6 and w != 9:
+            c.set_tuning(TUNE_WINDOW_STRIDED, w)
+        for chain in Chain:
+            r = c.parse(arena, off, lens, chain)
+            f = c.fields(arena, off, lens, chain)
+            rs = c.parse_strided(sarena, 256, 40_000, chain, lens=slens)
+            fs = c.fields(sarena, None, slens, chain, stride=256, n=40_000)
+            torch.cuda.synchronize()
+            assert r.cpu().numpy().tobytes() == want_i[chain][0].tobytes(), (w, chain)
+            assert f.cpu().numpy().tobytes() == want_i[chain][1].tobytes(), (w, chain)
+            assert rs.cpu().numpy().tobytes() == want_s[chain][0].tobytes(), (w, chain)
+            assert fs.cpu().numpy().tobytes() == want_s[chain][1].tobytes(), (w, chain)
+
+
 @pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 1000])
 def test_small_and_ragged_batches(ctx, torch, n):
     arena, off, lens = ingot_amd.gen_frames(GenProfile.ADVERSARIAL, max(n, 1), seed=n + 1)

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Measurement tool: interleaved A/B of tuning variants on one dataset, in one
+process (cdna_hip_programming.md §5.4 rule 24: separate invocations add
+cross-process/device variance that looks like a kernel property).
+
+    python tools/abtune.py --config c3 --var win_i=4 --var win_i=5 --var win_i=9
+    python tools/abtune.py --config c2 --var streams=1 --var streams=2 --var rec=8
+
+A variant is a comma list of key=value: win_i, win_s, blocks, streams, rec.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import statistics
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--var", action="append", default=[])
+    ap.add_argument("--steps", type=int, default=0)
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+
+    import torch
+
+    import bench
+    import ingot_amd
+    from ingot_amd import Chain, GenProfile
+    from ingot_amd.abi import TUNE_MAX_BLOCKS, TUNE_WINDOW_INDEXED, TUNE_WINDOW_STRIDED
+
+    prof, n, stride, chain_name, _ = bench.CONFIGS[args.config]
+    chain = Chain[chain_name]
+    arena, off, lens = ingot_amd.gen_frames(GenProfile[prof], n, stride=stride)
+    reps = max(1, -(-(512 << 20) // arena.numel()))
+    arenas = [arena] + [arena.clone() for _ in range(reps - 1)]
+    outs = [torch.empty((n, 16), dtype=torch.uint8, device="cuda") for _ in range(reps)]
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(3)]
+    lib = ingot_amd.load_library()
+    steps = args.steps or max(20, int(2e5 / max(1, n / 1e4)))
+    variants = args.var or ["win_i=5"]
+    runners = {}
+    for v in variants:
+        kv = dict(x.split("=") for x in v.split(",") if x)
+        ctx = ingot_amd.Context(0)
+        if "win_i" in kv:
+            ctx.set_tuning(TUNE_WINDOW_INDEXED, int(kv["win_i"]))
+        if "win_s" in kv:
+            ctx.set_tuning(TUNE_WINDOW_STRIDED, int(kv["win_s"]))
+        if "blocks" in kv:
+            ctx.set_tuning(TUNE_MAX_BLOCKS, int(kv["blocks"]))
+        ns, rb = int(kv.get("streams", 1)), int(kv.get("rec", 16))
+        runners[v] = (ctx, bench.Runner(torch, lib, ctx, chain, n, stride, arenas, off, lens,
+                                        outs, streams[:ns], rb))
+    res = {v: [] for v in variants}
+    for _ in range(args.rounds):
+        for v, (_, r) in runners.items():
+            r.run(5)
+            ms, _ = r.run(steps)
+            res[v].append(ms * 1e3 / steps)
+    summary = {}
+    for v, xs in res.items():
+        summary[v] = {"us_min": round(min(xs), 3), "us_median": round(statistics.median(xs), 3),
+                      "Gpkt_s_best": round(n / min(xs) / 1e3, 3), "all": [round(x, 2) for x in xs]}
+        print(f"{args.config} {v:28s} min {min(xs):10.2f} us  med {statistics.median(xs):10.2f} us"
+              f"  {n / min(xs) / 1e3:7.2f} Gpkt/s", flush=True)
+    if args.out:
+        Path(args.out).write_text(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Measure HBM traffic of the parse kernel from rocprofv3 PMC counters.
+
+Recipe (MI355X_MICROARCH.md §HBM, §rocprofv3 PMC slots): FETCH_SIZE and
+WRITE_SIZE in separate --pmc passes (they do not fit one pass); both are in
+KiB; on gfx950 FETCH_SIZE reports exactly half of the bytes of a wide
+coalesced streaming read, so it is doubled.  Per-dispatch values of the
+k_parse kernel are averaged and written to profiles/<tag>_pmc_<config>.json,
+which bench.py reports as `roofline.traffic`.
+
+    python tools/pmc_traffic.py --config c2 --tag r01
+(run on the GPU box; it launches rocprofv3 itself, the profiled program is
+python3 bench.py directly after `--`).
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def run_pass(counter: str, config: str, outdir: Path, steps: int) -> list[float]:
+    d = outdir / counter.lower()
+    d.mkdir(parents=True, exist_ok=True)
+    cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", str(d), "-o", "run",
+           "--", sys.executable, str(ROOT / "bench.py"), "--config", config, "--steps", str(steps),
+           "--warmup", "2", "--streams", "1", "--no-cpu-baseline", "--no-variants"]
+    env = dict(os.environ, TMPDIR="/tmp")
+    r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=900)
+    (d / "rocprof.log").write_text(r.stdout + "\n" + r.stderr)
+    if r.returncode != 0:
+        raise RuntimeError(f"rocprofv3 failed ({r.returncode}); see {d}/rocprof.log")
+    files = glob.glob(str(d / "**" / "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise RuntimeError(f"no counter_collection.csv under {d}")
+    vals = {}
+    with open(files[0]) as f:
+        for row in csv.DictReader(f):
+            if "k_parse" not in row.get("Kernel_Name", ""):
+                continue
+            if row.get("Counter_Name") != counter:
+                continue
+            key = row.get("Dispatch_Id") or row.get("Correlation_Id") or str(len(vals))
+            vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
+    return list(vals.values())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--tag", default="r01")
+    ap.add_argument("--steps", type=int, default=20)
+    args = ap.parse_args()
+    out = ROOT / "gpurun_out" / f"pmc_{args.config}"
+    fetch = run_pass("FETCH_SIZE", args.config, out, args.steps)
+    write = run_pass("WRITE_SIZE", args.config, out, args.steps)
+    # the first dispatches include the generator's and the algorithmic-bytes
+    # pass: keep the timed ones (all k_parse dispatches are the same launch)
+    f_kib = sorted(fetch)[len(fetch) // 2]
+    w_kib = sorted(write)[len(write) // 2]
+    res = {
+        "config": args.config,
+        "kernel": "k_parse",
+        "dispatches": [len(fetch), len(write)],
+        "FETCH_SIZE_KiB_median": f_kib,
+        "WRITE_SIZE_KiB_median": w_kib,
+        "fetch_bytes_corrected": f_kib * 1024 * 2,
+        "write_bytes": w_kib * 1024,
+        "traffic_bytes_per_launch": f_kib * 1024 * 2 + w_kib * 1024,
+        "correction": "FETCH_SIZE x2 on gfx950 (MI355X_MICROARCH.md:298)",
+    }
+    prof = ROOT / "profiles" / f"{args.tag}_pmc_{args.config}.json"
+    prof.write_text(json.dumps(res, indent=1) + "\n")
+    (ROOT / "gpurun_out" / prof.name).write_text(json.dumps(res, indent=1) + "\n")
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
