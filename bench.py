@@ -56,7 +56,11 @@ CONFIGS = {
     "c4": ("VLAN_V6EH", 1 << 23, None, "VlanUlp",
            "C4: 8,388,608 VLAN/QinQ + IPv6-EH mixed frames per GPU (64M over 8), packed, "
            "VlanUlp"),
+    "c5": ("FLOWS", 1 << 23, None, "VlanUlp",
+           "C5: C4 framing, 65,536 Zipf(1.1) flows; parse + RSS Toeplitz 5-tuple hash + "
+           "per-flow histogram (65,536 x u32) + RCCL all-reduce per step, 8,388,608 per GPU"),
 }
+FLOW_BINS = 1 << 16
 
 
 def log(*a):
@@ -147,25 +151,58 @@ class Runner:
 
     def run(self, steps):
         """Time `steps` launches: fork all streams from streams[0], join back."""
-        torch = self.torch
-        s0 = self.streams[0]
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        w0 = time.perf_counter()
-        e0.record(s0)
-        for s in self.streams[1:]:
-            s.wait_event(e0)
-        for k in range(steps):
-            rc = self.launch(k)
-            if rc:
-                raise RuntimeError(f"parse launch failed: {rc}")
-        for s in self.streams[1:]:
-            ev = torch.cuda.Event()
-            ev.record(s)
-            s0.wait_event(ev)
-        e1.record(s0)
-        torch.cuda.synchronize()
-        return e0.elapsed_time(e1), time.perf_counter() - w0
+        return _timed(self.torch, self.streams, self.launch, steps)
+
+
+class FlowRunner:
+    """Config 5 step: zero the histogram, parse + hash + histogram kernel,
+    then the RCCL all-reduce of the histogram (one stream: the reduce of step k
+    must see step k's counts)."""
+
+    def __init__(self, torch, lib, ctx, chain, n, arenas, off, lens, hists, flows, stream,
+                 reduce_fn):
+        self.torch, self.streams = torch, [stream]
+        reps = len(arenas)
+        h, sp, c = ctx._h, stream.cuda_stream, int(chain)
+        optr, lptr = off.data_ptr(), lens.data_ptr()
+        aptrs = [a.data_ptr() for a in arenas]
+
+        def launch(k):
+            hist = hists[k % reps]
+            hist.zero_()
+            rc = lib.ingot_gpu_flow_hist(h, aptrs[k % reps], optr, lptr, 0, n, c, None,
+                                         hist.numel(), flows[k % reps].data_ptr(), None,
+                                         hist.data_ptr(), sp)
+            reduce_fn(hist)
+            return rc
+
+        self.launch = launch
+
+    def run(self, steps):
+        return _timed(self.torch, self.streams, self.launch, steps)
+
+
+def _timed(torch, streams, launch, steps):
+    """Run `steps` launches between two HIP events on streams[0]; the other
+    streams fork from the start event and join before the end event."""
+    s0 = streams[0]
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    w0 = time.perf_counter()
+    e0.record(s0)
+    for s in streams[1:]:
+        s.wait_event(e0)
+    for k in range(steps):
+        rc = launch(k)
+        if rc:
+            raise RuntimeError(f"launch failed: {rc}")
+    for s in streams[1:]:
+        ev = torch.cuda.Event()
+        ev.record(s)
+        s0.wait_event(ev)
+    e1.record(s0)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1), time.perf_counter() - w0
 
 
 def main():
@@ -214,10 +251,22 @@ def main():
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
                                                   for _ in range(max(3, args.streams - 1))]
 
+    flows = args.config == "c5"
+    if flows:
+        from ingot_amd import dist as idist
+
+        hists = [torch.zeros(FLOW_BINS, dtype=torch.int32, device=dev) for _ in range(reps)]
+        flow_ids = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(reps)]
+
     def runner(nstreams, record):
+        if flows:
+            return FlowRunner(torch, lib, ctx, chain, n, arenas, off, lens, hists, flow_ids,
+                              streams[0], idist.reduce_histogram)
         return Runner(torch, lib, ctx, chain, n, stride, arenas, off, lens, outs,
                       streams[:nstreams], record)
 
+    if flows:
+        args.streams, args.no_variants = 1, True
     main_run = runner(args.streams, args.record)
     main_run.run(args.warmup)
 
@@ -243,6 +292,9 @@ def main():
     recs_np = ingot_amd.records_to_numpy(recs)
     lens_np = lens.cpu().numpy() if lens is not None else None
     rd, wr = algorithmic_bytes(recs_np, lens_np, stride or 0, 0 if stride else 10, args.record)
+    if flows:  # per-packet flow id (4 B) + the flow-id re-read of the histogram pass
+        wr = 4 * n + FLOW_BINS * 4
+        rd += 4 * n * (FLOW_BINS // min(FLOW_BINS, 16384))
     bytes_launch = rd + wr
     pipelined_gbs = bytes_launch / (ms_region / args.steps / 1e3) / 1e9
     # Roofline of the kernel itself: a single-stream pass (launches back to
@@ -315,7 +367,9 @@ def main():
                 "record_bytes": args.record,
                 "streams": args.streams,
                 "arena_copies_rotated": reps,
-                "parallelism": f"shard per GPU x{world} (no data-path collective)",
+                "parallelism": (f"shard per GPU x{world}; RCCL all-reduce (sum) of the "
+                                f"{FLOW_BINS} x u32 flow histogram every step" if flows else
+                                f"shard per GPU x{world} (no data-path collective)"),
                 "ok_fraction": round(ok_frac, 6),
             },
             "roofline": {

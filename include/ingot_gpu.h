@@ -323,6 +323,31 @@ int ingot_gpu_fields(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
                      uint32_t stride, uint64_t n, int chain,
                      ingot_fields* d_out, void* stream);
 
+/*
+ * Flow classification + per-flow histogram (config 5; build-defined, ingot
+ * has no flow hash).  For every packet that parses Ok as `chain` with an
+ * IPv4/IPv6 layer, the RSS Toeplitz hash of
+ *     source addr | destination addr | (source port | destination port)
+ * (ports only when the L4 layer is TCP or UDP; network byte order, the
+ * Microsoft RSS input order) with the 40-byte `key` (host memory; NULL =
+ * the standard Microsoft RSS key).  Outputs:
+ *   d_flow  (required, n x u32)  the packet's flow bin hash & (bins - 1), or
+ *           INGOT_FLOW_NONE for packets that are not counted;
+ *   d_hash  (optional, n x u32)  the full hash, 0 when not counted;
+ *   d_hist  (optional, bins x u32) d_hist[bin] += 1 per counted packet —
+ *           accumulated into (zero it to start a new histogram).
+ * bins is a power of two <= 2^24.  d_off == NULL selects the strided layout
+ * (as ingot_gpu_fields).  Two launches: parse + hash, then a contention-free
+ * histogram pass over d_flow (LDS-privatised bin ranges).
+ */
+#define INGOT_FLOW_KEY_BYTES 40
+#define INGOT_FLOW_NONE 0xffffffffu
+int ingot_gpu_flow_hist(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
+                        const uint64_t* d_off, const uint16_t* d_len,
+                        uint32_t stride, uint64_t n, int chain,
+                        const uint8_t* key, uint32_t bins, uint32_t* d_flow,
+                        uint32_t* d_hash, uint32_t* d_hist, void* stream);
+
 /* Error strings. */
 const char* ingot_gpu_strerror(int api_code);
 /* ParseError name as ingot prints it (error.rs:49-60): "Unwanted", ... ;

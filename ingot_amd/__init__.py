@@ -187,6 +187,30 @@ class Context:
         return out
 
 
+    def flow_hist(self, arena, off, lens, chain: Chain, hist=None, bins: Optional[int] = None,
+                  stride: int = 0, n: Optional[int] = None, key: Optional[bytes] = None,
+                  flow=None, hashes=None, stream=None):
+        """Flow classification (ingot_gpu_flow_hist).  Returns the per-packet
+        flow bins (n x int32; INGOT_FLOW_NONE = -1 when not counted); `hist`
+        (int32/uint32 cuda tensor of `bins` entries) is accumulated into if
+        given; optional full Toeplitz hashes into `hashes`.  key=None: the
+        standard RSS key."""
+        torch = _torch()
+        if n is None:
+            n = off.numel()
+        if bins is None:
+            bins = hist.numel() if hist is not None else 65536
+        if flow is None:
+            flow = torch.empty(n, dtype=torch.int32, device=arena.device)
+        self._check_dev(arena, off, lens, hist, hashes, flow)
+        kbuf = None if key is None else ctypes.create_string_buffer(bytes(key), 40)
+        _lib.check(self._lib.ingot_gpu_flow_hist(
+            self._h, _ptr(arena), _ptr(off), _ptr(lens), int(stride), n, int(chain),
+            ctypes.cast(kbuf, ctypes.c_void_p) if kbuf is not None else None, int(bins),
+            _ptr(flow), _ptr(hashes), _ptr(hist), _stream(stream)), "ingot_gpu_flow_hist")
+        return flow
+
+
 def records_to_numpy(t):
     """(n, 16) uint8 tensor/array -> numpy structured array of ingot_rec."""
     import numpy as np

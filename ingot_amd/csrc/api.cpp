@@ -163,6 +163,48 @@ int ingot_gpu_fields(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t*
                          stream);
 }
 
+int ingot_gpu_flow_hist(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
+                        const uint16_t* d_len, uint32_t stride, uint64_t n, int chain,
+                        const uint8_t* key, uint32_t bins, uint32_t* d_flow, uint32_t* d_hash,
+                        uint32_t* d_hist, void* stream) {
+    // The standard Microsoft RSS key (the one its published verification
+    // vectors use; tests/test_flows.py).
+    static const uint8_t kRssKey[INGOT_FLOW_KEY_BYTES] = {
+        0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67, 0x25, 0x3d, 0x43, 0xa3,
+        0x8f, 0xb0, 0xd0, 0xca, 0x2b, 0xcb, 0xae, 0x7b, 0x30, 0xb4, 0x77, 0xcb, 0x2d, 0xa3,
+        0x80, 0x30, 0xf2, 0x0c, 0x6a, 0x42, 0xb7, 0x3b, 0xbe, 0xac, 0x01, 0xfa};
+    if (!ctx || !chain_ok(chain)) return INGOT_GPU_EINVAL;
+    if (bins == 0 || (bins & (bins - 1)) != 0 || bins > (1u << 24)) return INGOT_GPU_ERANGE;
+    if (n == 0) return INGOT_GPU_SUCCESS;
+    if (!d_arena || !d_flow) return INGOT_GPU_EINVAL;
+    int layout = ingot_gpu::LAYOUT_INDEXED;
+    if (!d_off) {
+        if (int e = stride_ok(d_arena, stride)) return e;
+        layout = ingot_gpu::LAYOUT_STRIDED;
+    } else if (!d_len) {
+        return INGOT_GPU_EINVAL;
+    }
+    if (int e = enter(ctx)) return e;
+    const uint8_t* k = key ? key : kRssKey;
+    ingot_gpu::FlowArgs a{};
+    a.p = ingot_gpu::ParseArgs{d_arena, d_off, d_len, stride, n, nullptr};
+    a.flow = d_flow;
+    a.bin_mask = bins - 1u;
+    a.hash = d_hash;
+    for (uint32_t b = 0; b < ingot_gpu::FLOW_INPUT_BITS; ++b) {
+        uint32_t w = 0;
+        for (uint32_t j = 0; j < 32; ++j) {
+            const uint32_t bit = b + j;
+            w = (w << 1) | ((k[bit >> 3] >> (7u - (bit & 7u))) & 1u);
+        }
+        a.w[b] = w;
+    }
+    const hipStream_t s = (hipStream_t)stream;
+    if (int e = from_hip(ingot_gpu::launch_flows(a, layout, chain, ctx->tuning, s))) return e;
+    if (!d_hist) return INGOT_GPU_SUCCESS;
+    return from_hip(ingot_gpu::launch_flow_hist(d_flow, n, d_hist, bins, s));
+}
+
 const char* ingot_gpu_strerror(int code) {
     switch (code) {
     case INGOT_GPU_SUCCESS: return "success";

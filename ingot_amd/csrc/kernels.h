@@ -11,8 +11,13 @@ namespace ingot_gpu {
 
 enum LayoutKind { LAYOUT_STRIDED = 0, LAYOUT_INDEXED = 1 };
 
-// Output mode: 16-B ingot_rec, 8-B ingot_rec8, or 256-B ingot_fields.
-enum OutMode { OUT_REC16 = 0, OUT_REC8 = 1, OUT_FIELDS = 2 };
+// Output mode: 16-B ingot_rec, 8-B ingot_rec8, 256-B ingot_fields, or the
+// flow hash + histogram.
+enum OutMode { OUT_REC16 = 0, OUT_REC8 = 1, OUT_FIELDS = 2, OUT_FLOWS = 3 };
+
+// Toeplitz key windows: w[b] = the 32 key bits starting at input bit b, for
+// every bit of the longest input (IPv6 src|dst|ports = 36 bytes).
+constexpr uint32_t FLOW_INPUT_BITS = 36 * 8;
 
 struct ParseArgs {
     const uint8_t* arena;
@@ -23,6 +28,18 @@ struct ParseArgs {
     void* out;             // n records of the OutMode's type
 };
 
+struct FlowArgs {
+    ParseArgs p;
+    uint32_t* flow;  // per-packet bin or INGOT_FLOW_NONE
+    uint32_t bin_mask;
+    uint32_t* hash;  // optional
+    uint32_t w[FLOW_INPUT_BITS];
+};
+
+// Histogram pass over flow bins (flow.hip).
+hipError_t launch_flow_hist(const uint32_t* flow, uint64_t n, uint32_t* hist, uint32_t bins,
+                            hipStream_t s);
+
 // Per-context tuning (0 = measured default); see INGOT_TUNE_* in ingot_gpu.h.
 struct Tuning {
     int window_indexed = 0;
@@ -32,6 +49,8 @@ struct Tuning {
 
 hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, int mode,
                         const Tuning& t, hipStream_t s);
+hipError_t launch_flows(const FlowArgs& a, int layout_kind, int chain, const Tuning& t,
+                        hipStream_t s);
 bool tuning_valid(int key, int value);
 
 }  // namespace ingot_gpu

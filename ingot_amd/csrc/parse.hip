@@ -383,13 +383,73 @@ __device__ __forceinline__ void walk(const FR& f, Rec& r, ingot_fields* F) {
 // ---------------------------------------------------------------------------
 // Kernel.
 // ---------------------------------------------------------------------------
-template <uint32_t NCH, int LAYOUT, int CHAIN, int MODE>
-__global__ __launch_bounds__(BLOCK) void k_parse(ParseArgs a) {
+__device__ __forceinline__ const ParseArgs& base_args(const ParseArgs& a) { return a; }
+__device__ __forceinline__ const ParseArgs& base_args(const FlowArgs& a) { return a.p; }
+
+// RSS Toeplitz over one 32-bit input word (MSB first) whose first bit is
+// input bit B: XOR in the key window W[B + k] for every set bit k.  W is
+// lane-uniform (kernel argument), so only the data bits are per lane.
+// RSS Toeplitz with nibble tables in LDS: tab[p*16 + v] = XOR of the key
+// windows of the set bits of nibble value v at input nibble position p
+// (FLOW_INPUT_BITS/4 = 72 positions, 4.5 KiB per block, built once per block
+// from the 32-bit key windows).  A 32-bit input word = 8 LDS lookups.
+constexpr uint32_t FLOW_TAB = FLOW_INPUT_BITS / 4 * 16;
+
+__device__ __forceinline__ void build_flow_table(uint32_t* tab, const uint32_t* W) {
+    for (uint32_t e = threadIdx.x; e < FLOW_TAB; e += BLOCK) {
+        const uint32_t p = e >> 4, v = e & 15u;
+        uint32_t acc = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) acc ^= ((v >> (3u - k)) & 1u) ? W[4u * p + k] : 0u;
+        tab[e] = acc;
+    }
+}
+
+template <uint32_t NIB0>  // first nibble position of the word
+__device__ __forceinline__ uint32_t toeplitz_word(uint32_t word, const uint32_t* tab) {
+    uint32_t h = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) h ^= tab[(NIB0 + j) * 16u + ((word >> (28u - 4u * j)) & 15u)];
+    return h;
+}
+
+// Flow classification (ingot_gpu_flow_hist): hash of src|dst|ports.
+// Appending zero ports leaves a Toeplitz hash unchanged, so ICMP/other L4 use
+// the same word positions with a zero port word.
+template <class FR>
+__device__ __forceinline__ bool flow_hash(const FR& f, const Rec& r, const uint32_t* tab,
+                                          uint32_t& h) {
+    h = 0;
+    if (r.status != INGOT_OK || r.l3_kind == INGOT_L3_NONE) return false;
+    const bool ports = r.l4_kind == INGOT_L4_TCP || r.l4_kind == INGOT_L4_UDP;
+    const uint32_t pw = ports ? f.be(r.l4_off, 4) : 0u;
+    if (r.l3_kind == INGOT_L3_IPV4) {
+        h = toeplitz_word<0>(f.be(r.l3_off + 12u, 4), tab) ^
+            toeplitz_word<8>(f.be(r.l3_off + 16u, 4), tab) ^ toeplitz_word<16>(pw, tab);
+    } else {
+        const uint32_t a = r.l3_off + ipv6::SOURCE_BYTE;
+        h = toeplitz_word<0>(f.be(a, 4), tab) ^ toeplitz_word<8>(f.be(a + 4u, 4), tab) ^
+            toeplitz_word<16>(f.be(a + 8u, 4), tab) ^ toeplitz_word<24>(f.be(a + 12u, 4), tab) ^
+            toeplitz_word<32>(f.be(a + 16u, 4), tab) ^ toeplitz_word<40>(f.be(a + 20u, 4), tab) ^
+            toeplitz_word<48>(f.be(a + 24u, 4), tab) ^ toeplitz_word<56>(f.be(a + 28u, 4), tab) ^
+            toeplitz_word<64>(pw, tab);
+    }
+    return true;
+}
+
+template <uint32_t NCH, int LAYOUT, int CHAIN, int MODE, class ARGS>
+__global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
+    const ParseArgs& a = base_args(args);
     constexpr uint32_t WIN = NCH * 16u;
     constexpr uint32_t WAVE_DW = WAVE * NCH * 4u;  // dwords per wave image
     // +16 dwords: the second dword of a pair read may run past the last image.
     // NCH = 0: no staging, every read goes to L2/HBM.
     __shared__ __attribute__((aligned(16))) uint32_t s_win[WAVES * WAVE_DW + 16];
+    __shared__ uint32_t s_tab[MODE == OUT_FLOWS ? FLOW_TAB : 1];
+    if constexpr (MODE == OUT_FLOWS) {
+        build_flow_table(s_tab, args.w);
+        __syncthreads();
+    }
 
     const uint32_t lane = threadIdx.x & (WAVE - 1u);
     const uint32_t wave = threadIdx.x / WAVE;
@@ -451,6 +511,14 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ParseArgs a) {
         } else if constexpr (MODE == OUT_REC8) {
             walk<CHAIN, false>(fr, r, nullptr);
             if (valid) static_cast<uint2*>(a.out)[i] = pack8(r);
+        } else if constexpr (MODE == OUT_FLOWS) {
+            walk<CHAIN, false>(fr, r, nullptr);
+            uint32_t h;
+            const bool counted = valid && flow_hash(fr, r, s_tab, h);
+            if (valid) {
+                args.flow[i] = counted ? (h & args.bin_mask) : INGOT_FLOW_NONE;
+                if (args.hash) args.hash[i] = h;
+            }
         } else {
             walk<CHAIN, false>(fr, r, nullptr);
             if (valid) static_cast<uint4*>(a.out)[i] = pack(r);
@@ -460,19 +528,19 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ParseArgs a) {
     }
 }
 
-template <uint32_t NCH, int LAYOUT, int MODE>
-hipError_t launch_chain(const ParseArgs& a, int chain, uint32_t grid, hipStream_t s) {
+template <uint32_t NCH, int LAYOUT, int MODE, class ARGS>
+hipError_t launch_chain(const ARGS& a, int chain, uint32_t grid, hipStream_t s) {
     switch (chain) {
     case INGOT_CHAIN_UDP_PARSER:
-        hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_UDP_PARSER, MODE>), dim3(grid),
+        hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_UDP_PARSER, MODE, ARGS>), dim3(grid),
                            dim3(BLOCK), 0, s, a);
         break;
     case INGOT_CHAIN_GENERIC_ULP:
-        hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_GENERIC_ULP, MODE>), dim3(grid),
-                           dim3(BLOCK), 0, s, a);
+        hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_GENERIC_ULP, MODE, ARGS>),
+                           dim3(grid), dim3(BLOCK), 0, s, a);
         break;
     default:
-        hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_VLAN_ULP, MODE>), dim3(grid),
+        hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_VLAN_ULP, MODE, ARGS>), dim3(grid),
                            dim3(BLOCK), 0, s, a);
         break;
     }
@@ -531,6 +599,28 @@ hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, int mode
     case 8: return launch_mode<8, LAYOUT_INDEXED>(a, chain, mode, g, s);
     case 9: return launch_mode<9, LAYOUT_INDEXED>(a, chain, mode, g, s);
     default: return launch_mode<5, LAYOUT_INDEXED>(a, chain, mode, g, s);
+    }
+}
+
+// Flow mode needs the addresses (IPv6: 32 bytes past byte 22) and ports, so
+// its default window is 5 chunks; the same tuning knobs override it.
+hipError_t launch_flows(const FlowArgs& a, int layout_kind, int chain, const Tuning& t,
+                        hipStream_t s) {
+    if (a.p.n == 0) return hipSuccess;
+    const uint32_t g = grid_for(a.p.n, t.max_blocks);
+    if (layout_kind == LAYOUT_STRIDED) {
+        switch (t.window_strided ? t.window_strided : (a.p.stride <= 64u ? 4 : 5)) {
+        case 3: return launch_chain<3, LAYOUT_STRIDED, OUT_FLOWS>(a, chain, g, s);
+        case 4: return launch_chain<4, LAYOUT_STRIDED, OUT_FLOWS>(a, chain, g, s);
+        case 8: return launch_chain<8, LAYOUT_STRIDED, OUT_FLOWS>(a, chain, g, s);
+        default: return launch_chain<5, LAYOUT_STRIDED, OUT_FLOWS>(a, chain, g, s);
+        }
+    }
+    switch (t.window_indexed ? t.window_indexed : 5) {
+    case 3: return launch_chain<3, LAYOUT_INDEXED, OUT_FLOWS>(a, chain, g, s);
+    case 4: return launch_chain<4, LAYOUT_INDEXED, OUT_FLOWS>(a, chain, g, s);
+    case 6: return launch_chain<6, LAYOUT_INDEXED, OUT_FLOWS>(a, chain, g, s);
+    default: return launch_chain<5, LAYOUT_INDEXED, OUT_FLOWS>(a, chain, g, s);
     }
 }
 

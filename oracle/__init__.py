@@ -112,6 +112,39 @@ def toeplitz(key: bytes, data: bytes) -> int:
     return int(load().oracle_toeplitz(_p(k), len(key), _p(d), len(data)))
 
 
+RSS_KEY = bytes.fromhex("6d5a56da255b0ec24167253d43a38fb0d0ca2bcbae7b30b477cb2da38030f20c"
+                        "6a42b73bbeac01fa")
+
+
+def flow_hist(arena, off, lens, chain: Chain, stride: int = 0, n: int | None = None,
+              key: bytes = RSS_KEY, bins: int = 65536, hist: np.ndarray | None = None):
+    """-> (hist u32[bins] (accumulated), per-packet hash u32[n]); the per-packet
+    flow bins (INGOT_FLOW_NONE when not counted) are in `flow_hist.last_flows`."""
+    lib = load()
+    lib.oracle_flow_hist.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint32, ctypes.c_uint64,
+                                                             ctypes.c_int, ctypes.c_void_p,
+                                                             ctypes.c_void_p, ctypes.c_uint32,
+                                                             ctypes.c_void_p, ctypes.c_void_p]
+    lib.oracle_flow_hist.restype = ctypes.c_int
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    if off is not None:
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        n = len(off) if n is None else n
+    if lens is not None:
+        lens = np.ascontiguousarray(lens, dtype=np.uint16)
+    if hist is None:
+        hist = np.zeros(bins, dtype=np.uint32)
+    hashes = np.zeros(n, dtype=np.uint32)
+    flows = np.zeros(n, dtype=np.uint32)
+    k = np.frombuffer(bytes(key), dtype=np.uint8).copy()
+    rc = lib.oracle_flow_hist(_p(arena), _p(off), _p(lens), stride, n, int(chain), _p(k),
+                              _p(hist), bins, _p(hashes), _p(flows))
+    if rc != 0:
+        raise ValueError("oracle_flow_hist: bad arguments")
+    flow_hist.last_flows = flows
+    return hist, hashes
+
+
 HEADER_KINDS = {"ethernet": 0, "vlan": 1, "ipv4": 2, "ipv6": 3, "tcp": 4, "udp": 5, "icmp": 6,
                 "repeated_udp": 7}
 

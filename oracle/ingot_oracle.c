@@ -500,6 +500,7 @@ static void* run_job(void* arg) {
     for (uint64_t i = j->lo; i < j->hi; ++i) {
         uint64_t o = j->off ? j->off[i] : i * (uint64_t)j->stride;
         uint32_t l = j->len ? j->len[i] : j->stride;
+        if (!j->off && l > j->stride) l = j->stride; /* a slot holds one frame */
         oracle_parse_one(j->arena + o, l, j->chain, &j->rec[i], j->fields ? &j->fields[i] : 0);
     }
     return 0;
@@ -600,4 +601,48 @@ int oracle_parse_header(int kind, const uint8_t* s, uint32_t n, uint32_t* used,
         *hint_out = h;
     }
     return e;
+}
+
+/* ------------------------------------------------------------------------
+ * Flow classification (build-defined; ingot has no flow hash): Toeplitz over
+ * src | dst (| sport | dport for TCP/UDP) of frames that parse Ok with an L3.
+ * ---------------------------------------------------------------------- */
+int oracle_flow_hash(const uint8_t* frame, uint32_t len, int chain, const uint8_t* key,
+                     uint32_t* hash) {
+    ingot_rec r;
+    oracle_parse_one(frame, len, chain, &r, 0);
+    *hash = 0;
+    if (r.status != INGOT_OK || r.l3_kind == INGOT_L3_NONE) return 0;
+    uint8_t in[36];
+    uint32_t n = 0;
+    if (r.l3_kind == INGOT_L3_IPV4) {
+        memcpy(in, frame + r.l3_off + 12, 8);
+        n = 8;
+    } else {
+        memcpy(in, frame + r.l3_off + 8, 32);
+        n = 32;
+    }
+    if (r.l4_kind == INGOT_L4_TCP || r.l4_kind == INGOT_L4_UDP) {
+        memcpy(in + n, frame + r.l4_off, 4);
+        n += 4;
+    }
+    *hash = oracle_toeplitz(key, 40, in, n);
+    return 1;
+}
+
+int oracle_flow_hist(const uint8_t* arena, const uint64_t* off, const uint16_t* len,
+                     uint32_t stride, uint64_t n, int chain, const uint8_t* key, uint32_t* hist,
+                     uint32_t bins, uint32_t* hash_out, uint32_t* flow_out) {
+    if (!bins || (bins & (bins - 1))) return -1;
+    for (uint64_t i = 0; i < n; ++i) {
+        uint64_t o = off ? off[i] : i * (uint64_t)stride;
+        uint32_t l = len ? len[i] : stride;
+        if (!off && l > stride) l = stride;
+        uint32_t h = 0;
+        int counted = oracle_flow_hash(arena + o, l, chain, key, &h);
+        if (counted) hist[h & (bins - 1)] += 1;
+        if (hash_out) hash_out[i] = h;
+        if (flow_out) flow_out[i] = counted ? (h & (bins - 1)) : INGOT_FLOW_NONE;
+    }
+    return 0;
 }

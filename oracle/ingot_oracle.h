@@ -53,6 +53,16 @@ int oracle_parse_header(int kind, const uint8_t* s, uint32_t n, uint32_t* used,
 uint32_t oracle_toeplitz(const uint8_t* key, uint32_t key_len,
                          const uint8_t* data, uint32_t n);
 
+/* Flow classification (ingot_gpu_flow_hist semantics): returns 1 and the
+ * Toeplitz hash when the frame is counted, else 0 (*hash = 0). */
+int oracle_flow_hash(const uint8_t* frame, uint32_t len, int chain, const uint8_t* key,
+                     uint32_t* hash);
+/* Batch: hist[hash & (bins-1)] += 1 for counted frames (accumulates);
+ * hash_out / flow_out (bin or INGOT_FLOW_NONE) optional. */
+int oracle_flow_hist(const uint8_t* arena, const uint64_t* off, const uint16_t* len,
+                     uint32_t stride, uint64_t n, int chain, const uint8_t* key, uint32_t* hist,
+                     uint32_t bins, uint32_t* hash_out, uint32_t* flow_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -330,6 +330,29 @@ def bitfield_kats():
         ])]
 
 
+def rss_kats():
+    """Toeplitz/RSS verification suite (Microsoft, "Verifying the RSS Hash
+    Calculation", standard 40-byte key).  Not from ingot: the flow hash of
+    config 5 is build-defined, and these pin it.  Input order: src addr, dst
+    addr (, src port, dst port), network byte order."""
+    rows = [
+        ("161.142.100.80", 1766, "66.9.149.187", 2794, 0x323E8FC2, 0x51CCC178),
+        ("65.69.140.83", 4739, "199.92.111.2", 14230, 0xD718262A, 0xC626B0EA),
+        ("12.22.207.184", 38024, "24.19.198.95", 12898, 0xD2D0A5DE, 0x5C2B394A),
+        ("209.142.163.6", 2217, "38.27.205.30", 48228, 0x82989176, 0xAFC7327F),
+        ("202.188.127.2", 1303, "153.39.163.191", 44251, 0x5D1809C5, 0x10E828A2),
+        ("3ffe:2501:200:3::1", 1766, "3ffe:2501:200:1fff::7", 2794, 0x2CC18CD5, 0x40207D3D),
+        ("ff02::1", 4739, "3ffe:501:8::260:97ff:fe40:efab", 14230, 0x0F0C461C, 0xDDE51BBF),
+        ("fe80::200:f8ff:fe21:67cf", 38024, "3ffe:1900:4545:3:200:f8ff:fe21:67cf", 44251,
+         0x4B61E985, 0x02D1FEEF),
+    ]
+    return dict(
+        key="6d5a56da255b0ec24167253d43a38fb0d0ca2bcbae7b30b477cb2da38030f20c6a42b73bbeac01fa",
+        source="Microsoft RSS verification suite (standard key)",
+        vectors=[dict(dst=d, dport=dp, src=s, sport=sp, hash_addrs=h2, hash_ports=h4)
+                 for d, dp, s, sp, h2, h4 in rows])
+
+
 def main() -> None:
     doc = dict(
         reference="oxidecomputer/ingot @ 2025-08-08",
@@ -337,6 +360,7 @@ def main() -> None:
         chain_kats=chain_frames(),
         header_kats=header_kats(),
         bitfield_kats=bitfield_kats(),
+        rss_kats=rss_kats(),
     )
     (HERE / "kats.json").write_text(json.dumps(doc, indent=1) + "\n")
     print(f"wrote {len(doc['chain_kats'])} chain, {len(doc['header_kats'])} header, "

@@ -1,0 +1,73 @@
+"""The N>1 path on CPU: world_size-2 `gloo` process groups exercising the
+sharding, the max-over-ranks timing and the per-flow histogram all-reduce that
+bench.py runs over RCCL on GPUs (ingot_amd/dist.py)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+from ingot_amd import Chain, dist as idist
+from tests.frames import build_frames, pack
+
+N_PER_RANK = 1500
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        frames = build_frames(N_PER_RANK * world, seed=123)
+        first, n = idist.shard(rank, world, N_PER_RANK)
+        arena, off, lens = pack(frames[first:first + n])
+        hist, _ = oracle.flow_hist(arena, off, lens, Chain.VlanUlp, bins=4096)
+        t = torch.from_numpy(hist.astype(np.uint32).view(np.int32).copy())
+        idist.reduce_histogram(t)
+        slowest = idist.max_over_ranks(0.5 + rank)
+        if rank == 0:
+            q.put((t.numpy().view(np.uint32).copy(), slowest))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_and_split():
+    assert idist.shard(0, 4, 100) == (0, 100)
+    assert idist.shard(3, 4, 100) == (300, 100)
+    parts = [idist.split(1003, r, 4) for r in range(4)]
+    assert sum(n for _, n in parts) == 1003
+    assert all(parts[i][0] + parts[i][1] == parts[i + 1][0] for i in range(3))
+    with pytest.raises(ValueError):
+        idist.shard(4, 4, 1)
+
+
+@pytest.mark.parametrize("world", [2])
+def test_histogram_allreduce_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    hist, slowest = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    frames = build_frames(N_PER_RANK * world, seed=123)
+    arena, off, lens = pack(frames)
+    want, _ = oracle.flow_hist(arena, off, lens, Chain.VlanUlp, bins=4096)
+    assert (hist == want).all()
+    assert slowest == 0.5 + (world - 1)

@@ -1,0 +1,113 @@
+"""Flow classification (config 5): RSS Toeplitz hash of the parsed 5-tuple and
+the per-flow histogram.  Build-defined (ingot has no flow hash); the hash is
+pinned by Microsoft's published RSS verification vectors
+(tests/golden/kats.json "rss_kats"), the tuple extraction by the oracle."""
+import ipaddress
+
+import numpy as np
+import pytest
+
+import oracle
+from ingot_amd import Chain
+from tests.frames import build_frames, pack
+
+
+def test_rss_verification_vectors(kats):
+    rss = kats["rss_kats"]
+    key = bytes.fromhex(rss["key"])
+    assert key == oracle.RSS_KEY
+    for v in rss["vectors"]:
+        src = ipaddress.ip_address(v["src"]).packed
+        dst = ipaddress.ip_address(v["dst"]).packed
+        ports = v["sport"].to_bytes(2, "big") + v["dport"].to_bytes(2, "big")
+        assert oracle.toeplitz(key, src + dst) == v["hash_addrs"], v
+        assert oracle.toeplitz(key, src + dst + ports) == v["hash_ports"], v
+        # appending zero bytes never changes a Toeplitz hash (used by the kernel)
+        assert oracle.toeplitz(key, src + dst + bytes(4)) == v["hash_addrs"]
+
+
+def test_flow_hash_of_parsed_frames(kats):
+    v = kats["rss_kats"]["vectors"][0]
+    src = ipaddress.ip_address(v["src"]).packed
+    dst = ipaddress.ip_address(v["dst"]).packed
+    v4 = bytes([0x45, 0, 0, 0, 0, 0, 0, 0, 64, 6, 0, 0]) + src + dst
+    tcp = v["sport"].to_bytes(2, "big") + v["dport"].to_bytes(2, "big") + bytes(8) + \
+        bytes([0x50, 0]) + bytes(6)
+    frame = bytes(12) + b"\x08\x00" + v4 + tcp
+    hist, h = oracle.flow_hist(np.frombuffer(frame + bytes(8), np.uint8), np.array([0]),
+                               np.array([len(frame)]), Chain.GenericUlp, bins=1 << 16)
+    assert h[0] == v["hash_ports"] and hist[h[0] & 0xFFFF] == 1 and hist.sum() == 1
+    # ICMP: addresses only
+    v4i = bytes([0x45, 0, 0, 0, 0, 0, 0, 0, 64, 1, 0, 0]) + src + dst
+    fi = bytes(12) + b"\x08\x00" + v4i + bytes(8)
+    _, h = oracle.flow_hist(np.frombuffer(fi + bytes(8), np.uint8), np.array([0]),
+                            np.array([len(fi)]), Chain.GenericUlp)
+    assert h[0] == v["hash_addrs"]
+    # errors and ARP-accepted frames are not counted
+    for f in (frame[:30], bytes(12) + b"\x08\x06" + bytes(28)):
+        hist, h = oracle.flow_hist(np.frombuffer(f + bytes(8), np.uint8), np.array([0]),
+                                   np.array([len(f)]), Chain.GenericUlp)
+        assert hist.sum() == 0 and h[0] == 0
+
+
+def test_histogram_accumulates_and_matches_per_packet_hashes():
+    frames = build_frames(3000, seed=4)
+    arena, off, lens = pack(frames)
+    hist, h = oracle.flow_hist(arena, off, lens, Chain.GenericUlp, bins=1024)
+    counted = np.array([oracle.flow_hist(np.frombuffer(f + bytes(8), np.uint8), np.array([0]),
+                                         np.array([len(f)]), Chain.GenericUlp)[0].sum()
+                        for f in frames[:200]])
+    assert set(np.unique(counted)) <= {0, 1}
+    want = np.bincount(h[np.array([oracle.flow_hist(
+        np.frombuffer(f + bytes(8), np.uint8), np.array([0]), np.array([len(f)]),
+        Chain.GenericUlp)[0].sum() for f in frames]) == 1] & 1023, minlength=1024)
+    assert (hist == want).all()
+    hist2, _ = oracle.flow_hist(arena, off, lens, Chain.GenericUlp, bins=1024, hist=hist.copy())
+    assert (hist2 == 2 * hist).all()
+
+
+# ---------------------------------------------------------------------------
+# device
+# ---------------------------------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("profile,chain,stride", [
+    ("FLOWS", "VlanUlp", None), ("ADVERSARIAL", "GenericUlp", None),
+    ("MIXED", "UdpParser", None), ("VLAN_V6EH", "GenericUlp", 256), ("V4UDP64", "UdpParser", 64),
+])
+def test_flow_hist_bit_exact(profile, chain, stride):
+    import torch
+
+    import ingot_amd
+    from ingot_amd import GenProfile
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    n = 200_000
+    ctx = ingot_amd.Context(0)
+    arena, off, lens = ingot_amd.gen_frames(GenProfile[profile], n, seed=7, stride=stride)
+    hist = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")
+    hashes = torch.zeros(n, dtype=torch.int32, device="cuda")
+    flow = ctx.flow_hist(arena, off, lens, Chain[chain], hist=hist, stride=stride or 0, n=n,
+                         hashes=hashes)
+    torch.cuda.synchronize()
+    host = lambda t: None if t is None else t.cpu().numpy()  # noqa: E731
+    w_hist, w_hash = oracle.flow_hist(host(arena), host(off), host(lens), Chain[chain],
+                                      stride=stride or 0, n=n)
+    w_flow = oracle.flow_hist.last_flows
+    g_hash = hashes.cpu().numpy().view(np.uint32)
+    bad = np.nonzero(g_hash != w_hash)[0]
+    assert bad.size == 0, (bad[:5], g_hash[bad[:5]], w_hash[bad[:5]])
+    assert (flow.cpu().numpy().view(np.uint32) == w_flow).all()
+    assert (hist.cpu().numpy().view(np.uint32) == w_hist).all()
+    # accumulation across calls; a histogram-free call (flows only) and small bins
+    ctx.flow_hist(arena, off, lens, Chain[chain], hist=hist, stride=stride or 0, n=n)
+    torch.cuda.synchronize()
+    assert (hist.cpu().numpy().view(np.uint32) == 2 * w_hist).all()
+    h64 = torch.zeros(64, dtype=torch.int32, device="cuda")
+    ctx.flow_hist(arena, off, lens, Chain[chain], hist=h64, stride=stride or 0, n=n)
+    torch.cuda.synchronize()
+    w64 = np.bincount(w_hash[w_flow != 0xFFFFFFFF] & 63, minlength=64)
+    assert (h64.cpu().numpy() == w64).all()
+    if profile == "FLOWS":
+        # Zipf(1.1) head: the top bin holds a large share
+        assert w_hist.max() > 0.05 * w_hist.sum()
