@@ -1,0 +1,425 @@
+// ingot_amd.hpp — C++17 host-side mirror of ingot's parse interface, over the
+// C ABI in ingot_gpu.h.  Header-only; link libingot_gpu.so and amdhip64.
+//
+// The reference (Rust) exposes, per `#[derive(Parse)]` chain,
+//   Chain::parse(slice) -> Result<(Chain, Option<Hint>, Remainder), PacketParseError>
+// (ingot-macros/src/parse.rs:475-509, ingot-types/src/lib.rs:137-147, 208),
+// with one view per layer whose generated getters read the wire fields
+// (packet/mod.rs:1183-1479), and `PacketParseError{label, inner}`
+// (ingot-types/src/error.rs:119-171).  This header keeps those names and
+// meanings — UdpParser / GenericUlp (ingot-examples/src/packets.rs:18-24,
+// 54-60), ValidEthernet / ValidIpv4 / ValidIpv6 / ValidTcp / ValidUdp getters,
+// ParseError / PacketParseError — but every parse runs on the GPU: a
+// `gpu::BatchParser` uploads frames, runs the batched kernels and hands back
+// per-packet results.  `Chain::parse(bytes)` is the one-packet convenience
+// form (a batch of one), for tests that read like the reference's.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <optional>
+#include <tuple>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "ingot_gpu.h"
+
+namespace ingot {
+
+// ---------------------------------------------------------------------------
+// ingot_types::{ParseError, PacketParseError} (error.rs:21-44, 119-171)
+// ---------------------------------------------------------------------------
+namespace types {
+
+enum class ParseError : uint8_t {
+    Unwanted = INGOT_ERR_UNWANTED,
+    NeedsHint = INGOT_ERR_NEEDS_HINT,
+    TooSmall = INGOT_ERR_TOO_SMALL,
+    StraddledHeader = INGOT_ERR_STRADDLED_HEADER,
+    NoRemainingChunks = INGOT_ERR_NO_REMAINING_CHUNKS,
+    CannotAccept = INGOT_ERR_CANNOT_ACCEPT,
+    Reject = INGOT_ERR_REJECT,
+    IllegalValue = INGOT_ERR_ILLEGAL_VALUE,
+};
+
+inline const char* as_cstr(ParseError e) { return ingot_parse_error_name((int)e); }
+
+class PacketParseError {
+   public:
+    PacketParseError(const char* label, ParseError inner) : label_(label), inner_(inner) {}
+    const char* header() const { return label_; }  // the failing layer's label
+    ParseError error() const { return inner_; }
+    std::string to_string() const { return std::string(label_) + ": " + as_cstr(inner_); }
+
+   private:
+    const char* label_;
+    ParseError inner_;
+};
+
+// Result<T, PacketParseError>
+template <class T>
+class ParseResult {
+   public:
+    static ParseResult ok(T v) { return ParseResult(std::move(v)); }
+    static ParseResult err(PacketParseError e) { return ParseResult(e); }
+    bool is_ok() const { return value_.has_value(); }
+    bool is_err() const { return !is_ok(); }
+    T& unwrap() {
+        if (!value_) throw std::runtime_error("unwrap on Err: " + error_->to_string());
+        return *value_;
+    }
+    const PacketParseError& unwrap_err() const {
+        if (!error_) throw std::runtime_error("unwrap_err on Ok");
+        return *error_;
+    }
+
+   private:
+    explicit ParseResult(T v) : value_(std::move(v)) {}
+    explicit ParseResult(PacketParseError e) : error_(e) {}
+    std::optional<T> value_;
+    std::optional<PacketParseError> error_;
+};
+
+}  // namespace types
+
+using MacAddr6 = std::array<uint8_t, 6>;
+using Ipv4Addr = std::array<uint8_t, 4>;
+using Ipv6Addr = std::array<uint8_t, 16>;
+
+namespace ethernet {
+// ingot/src/ethernet.rs:9-20
+struct Ethertype {
+    uint16_t v;
+    static constexpr uint16_t IPV4 = 0x0800, ARP = 0x0806, ETHERNET = 0x6558, VLAN = 0x8100,
+                              IPV6 = 0x86dd, LLDP = 0x88cc, QINQ = 0x9100;
+};
+}  // namespace ethernet
+
+namespace ip {
+// ingot/src/ip.rs:20-38, 95-135
+struct IpProtocol {
+    static constexpr uint8_t ICMP = 1, IGMP = 2, TCP = 6, UDP = 17, ICMP_V6 = 58,
+                             IPV6_NO_NH = 59, IPV6_HOP_BY_HOP = 0, IPV6_ROUTE = 43,
+                             IPV6_FRAGMENT = 44, IPV6_DEST_OPTS = 60, IPV6_EXPERIMENT0 = 253,
+                             IPV6_EXPERIMENT1 = 254;
+};
+enum class Ecn : uint8_t { NotCapable = 0, Capable0 = 1, Capable1 = 2, CongestionExperienced = 3 };
+}  // namespace ip
+
+// ---------------------------------------------------------------------------
+// Layer views: the generated getters (values from the device field block).
+// ---------------------------------------------------------------------------
+namespace detail {
+template <size_t N>
+std::array<uint8_t, N> arr(const uint8_t* p) {
+    std::array<uint8_t, N> a{};
+    std::memcpy(a.data(), p, N);
+    return a;
+}
+}  // namespace detail
+
+class ValidEthernet {
+   public:
+    explicit ValidEthernet(const ingot_fields* f) : f_(f) {}
+    MacAddr6 destination() const { return detail::arr<6>(f_->eth_destination); }
+    MacAddr6 source() const { return detail::arr<6>(f_->eth_source); }
+    uint16_t ethertype() const { return f_->eth_ethertype; }
+
+   private:
+    const ingot_fields* f_;
+};
+
+class ValidVlanBody {
+   public:
+    ValidVlanBody(const ingot_fields* f, int i) : f_(f), i_(i) {}
+    uint8_t priority() const { return f_->vlan_priority[i_]; }
+    uint8_t dei() const { return f_->vlan_dei[i_]; }
+    uint16_t vid() const { return f_->vlan_vid[i_]; }
+    uint16_t ethertype() const { return f_->vlan_ethertype[i_]; }
+
+   private:
+    const ingot_fields* f_;
+    int i_;
+};
+
+class ValidIpv4 {
+   public:
+    ValidIpv4(const ingot_fields* f, const std::vector<uint8_t>* frame) : f_(f), frame_(frame) {}
+    uint8_t version() const { return f_->v4_version; }
+    uint8_t ihl() const { return f_->v4_ihl; }
+    uint8_t dscp() const { return f_->v4_dscp; }
+    ip::Ecn ecn() const { return (ip::Ecn)f_->v4_ecn; }
+    uint16_t total_len() const { return f_->v4_total_len; }
+    uint16_t identification() const { return f_->v4_identification; }
+    uint8_t flags() const { return f_->v4_flags; }
+    uint16_t fragment_offset() const { return f_->v4_fragment_offset; }
+    uint8_t hop_limit() const { return f_->v4_hop_limit; }
+    uint8_t protocol() const { return f_->v4_protocol; }
+    uint16_t checksum() const { return f_->v4_checksum; }
+    Ipv4Addr source() const { return detail::arr<4>(f_->v4_source); }
+    Ipv4Addr destination() const { return detail::arr<4>(f_->v4_destination); }
+    std::vector<uint8_t> options_ref() const {
+        auto b = frame_->begin() + f_->v4_options_off;
+        return std::vector<uint8_t>(b, b + f_->v4_options_len);
+    }
+    uint8_t next_layer() const { return f_->v4_protocol; }
+
+   private:
+    const ingot_fields* f_;
+    const std::vector<uint8_t>* frame_;
+};
+
+class ValidIpv6 {
+   public:
+    ValidIpv6(const ingot_fields* f, uint8_t hint) : f_(f), hint_(hint) {}
+    uint8_t version() const { return f_->v6_version; }
+    uint8_t dscp() const { return f_->v6_dscp; }
+    ip::Ecn ecn() const { return (ip::Ecn)f_->v6_ecn; }
+    uint32_t flow_label() const { return f_->v6_flow_label; }
+    uint16_t payload_len() const { return f_->v6_payload_len; }
+    uint8_t next_header() const { return f_->v6_next_header; }
+    uint8_t hop_limit() const { return f_->v6_hop_limit; }
+    Ipv6Addr source() const { return detail::arr<16>(f_->v6_source); }
+    Ipv6Addr destination() const { return detail::arr<16>(f_->v6_destination); }
+    // next_layer(): the last extension header's next_header (ip.rs:180-181)
+    uint8_t next_layer() const { return hint_; }
+    size_t extension_header_count() const { return f_->rec.n_v6ext; }
+    const ingot_v6eh& extension_header(size_t i) const { return f_->v6_eh[i]; }
+
+   private:
+    const ingot_fields* f_;
+    uint8_t hint_;
+};
+
+class ValidTcp {
+   public:
+    ValidTcp(const ingot_fields* f, const std::vector<uint8_t>* frame) : f_(f), frame_(frame) {}
+    uint16_t source() const { return f_->l4_source; }
+    uint16_t destination() const { return f_->l4_destination; }
+    uint32_t sequence() const { return f_->tcp_sequence; }
+    uint32_t acknowledgement() const { return f_->tcp_acknowledgement; }
+    uint8_t data_offset() const { return f_->tcp_data_offset; }
+    uint8_t flags() const { return f_->tcp_flags; }
+    uint16_t window_size() const { return f_->tcp_window_size; }
+    uint16_t checksum() const { return f_->tcp_checksum; }
+    uint16_t urgent_ptr() const { return f_->tcp_urgent_ptr; }
+    std::vector<uint8_t> options_ref() const {
+        auto b = frame_->begin() + f_->tcp_options_off;
+        return std::vector<uint8_t>(b, b + f_->tcp_options_len);
+    }
+
+   private:
+    const ingot_fields* f_;
+    const std::vector<uint8_t>* frame_;
+};
+
+class ValidUdp {
+   public:
+    explicit ValidUdp(const ingot_fields* f) : f_(f) {}
+    uint16_t source() const { return f_->l4_source; }
+    uint16_t destination() const { return f_->l4_destination; }
+    uint16_t length() const { return f_->udp_length; }
+    uint16_t checksum() const { return f_->udp_checksum; }
+
+   private:
+    const ingot_fields* f_;
+};
+
+// L3 choice (ingot-examples/src/choices.rs:17-21) and L4 / Ulp choices.
+struct L3 {
+    std::optional<ValidIpv4> ipv4;
+    std::optional<ValidIpv6> ipv6;
+};
+struct L4 {
+    std::optional<ValidTcp> tcp;
+    std::optional<ValidUdp> udp;
+    bool icmpv4 = false, icmpv6 = false;
+};
+
+// One parsed packet: owns its frame bytes and device field block so the views
+// stay valid.
+struct Packet {
+    std::vector<uint8_t> frame;
+    ingot_fields fields;
+};
+
+namespace gpu {
+
+inline void check(int rc, const char* what) {
+    if (rc != INGOT_GPU_SUCCESS)
+        throw std::runtime_error(std::string(what) + ": " + ingot_gpu_strerror(rc));
+}
+inline void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+class Context {
+   public:
+    explicit Context(int device = 0) { check(ingot_gpu_ctx_create(device, &h_), "ctx_create"); }
+    ~Context() { ingot_gpu_ctx_destroy(h_); }
+    Context(const Context&) = delete;
+    Context& operator=(const Context&) = delete;
+    ingot_gpu_ctx* get() const { return h_; }
+
+   private:
+    ingot_gpu_ctx* h_ = nullptr;
+};
+
+// Uploads host frames into a packed device arena, runs the records + field
+// kernels for `chain`, copies the per-packet field blocks back.
+inline std::vector<Packet> parse_batch(Context& ctx, const std::vector<std::vector<uint8_t>>& frames,
+                                       int chain) {
+    const size_t n = frames.size();
+    std::vector<uint64_t> off(n);
+    std::vector<uint16_t> len(n);
+    size_t total = 0;
+    for (size_t i = 0; i < n; ++i) {
+        if (frames[i].size() > 65535) throw std::length_error("frame longer than 65535 bytes");
+        off[i] = total;
+        len[i] = (uint16_t)frames[i].size();
+        total += (frames[i].size() + 15) / 16 * 16 + 16;
+    }
+    std::vector<uint8_t> arena(total + 64, 0);
+    for (size_t i = 0; i < n; ++i)
+        if (!frames[i].empty()) std::memcpy(arena.data() + off[i], frames[i].data(), frames[i].size());
+    uint8_t* d_arena = nullptr;
+    uint64_t* d_off = nullptr;
+    uint16_t* d_len = nullptr;
+    ingot_fields* d_f = nullptr;
+    hip_check(hipMalloc(&d_arena, arena.size()), "hipMalloc");
+    hip_check(hipMalloc(&d_off, n * 8 + 8), "hipMalloc");
+    hip_check(hipMalloc(&d_len, n * 2 + 8), "hipMalloc");
+    hip_check(hipMalloc(&d_f, n * sizeof(ingot_fields) + 256), "hipMalloc");
+    hip_check(hipMemcpy(d_arena, arena.data(), arena.size(), hipMemcpyHostToDevice), "H2D");
+    hip_check(hipMemcpy(d_off, off.data(), n * 8, hipMemcpyHostToDevice), "H2D");
+    hip_check(hipMemcpy(d_len, len.data(), n * 2, hipMemcpyHostToDevice), "H2D");
+    check(ingot_gpu_fields(ctx.get(), d_arena, d_off, d_len, 0, n, chain, d_f, nullptr),
+          "ingot_gpu_fields");
+    std::vector<Packet> out(n);
+    std::vector<ingot_fields> f(n);
+    hip_check(hipMemcpy(f.data(), d_f, n * sizeof(ingot_fields), hipMemcpyDeviceToHost), "D2H");
+    for (size_t i = 0; i < n; ++i) out[i] = Packet{frames[i], f[i]};
+    (void)hipFree(d_arena);
+    (void)hipFree(d_off);
+    (void)hipFree(d_len);
+    (void)hipFree(d_f);
+    return out;
+}
+
+inline Context& default_context() {
+    static Context ctx(0);
+    return ctx;
+}
+
+}  // namespace gpu
+
+namespace examples {
+
+template <class Chain>
+using Success = std::tuple<Chain, std::optional<uint8_t>, std::vector<uint8_t>>;
+
+namespace detail {
+inline types::PacketParseError error_of(int chain, const ingot_rec& r) {
+    return types::PacketParseError(ingot_chain_layer_label(chain, r.err_layer),
+                                   (types::ParseError)r.status);
+}
+inline L3 l3_of(const Packet& p) {
+    L3 l3;
+    if (p.fields.rec.l3_kind == INGOT_L3_IPV4) l3.ipv4.emplace(&p.fields, &p.frame);
+    if (p.fields.rec.l3_kind == INGOT_L3_IPV6) l3.ipv6.emplace(&p.fields, p.fields.rec.l4_proto);
+    return l3;
+}
+inline L4 l4_of(const Packet& p) {
+    L4 l4;
+    switch (p.fields.rec.l4_kind) {
+    case INGOT_L4_TCP: l4.tcp.emplace(&p.fields, &p.frame); break;
+    case INGOT_L4_UDP: l4.udp.emplace(&p.fields); break;
+    case INGOT_L4_ICMPV4: l4.icmpv4 = true; break;
+    case INGOT_L4_ICMPV6: l4.icmpv6 = true; break;
+    default: break;
+    }
+    return l4;
+}
+inline std::vector<uint8_t> remainder(const Packet& p) {
+    return std::vector<uint8_t>(p.frame.begin() + p.fields.rec.payload_off, p.frame.end());
+}
+}  // namespace detail
+
+// ingot-examples/src/packets.rs:18-24 — eth, l3: L3, l4: from L4 -> Udp.
+// The Packet is shared so the views outlive the temporary batch.
+struct UdpParser {
+    static constexpr int CHAIN = INGOT_CHAIN_UDP_PARSER;
+    std::shared_ptr<const Packet> pkt;
+    ValidEthernet eth;
+    L3 l3;
+    ValidUdp l4;
+
+    static std::vector<types::ParseResult<Success<UdpParser>>> parse_all(
+        const std::vector<std::vector<uint8_t>>& frames,
+        gpu::Context& ctx = gpu::default_context()) {
+        std::vector<types::ParseResult<Success<UdpParser>>> out;
+        for (auto& p : gpu::parse_batch(ctx, frames, CHAIN)) {
+            auto sp = std::make_shared<const Packet>(std::move(p));
+            if (sp->fields.rec.status != INGOT_OK) {
+                out.push_back(types::ParseResult<Success<UdpParser>>::err(
+                    detail::error_of(CHAIN, sp->fields.rec)));
+                continue;
+            }
+            UdpParser c{sp, ValidEthernet(&sp->fields), detail::l3_of(*sp),
+                        ValidUdp(&sp->fields)};
+            out.push_back(types::ParseResult<Success<UdpParser>>::ok(
+                Success<UdpParser>{c, std::nullopt, detail::remainder(*sp)}));
+        }
+        return out;
+    }
+    static types::ParseResult<Success<UdpParser>> parse(const std::vector<uint8_t>& frame) {
+        return std::move(parse_all({frame})[0]);
+    }
+};
+
+// ingot-examples/src/packets.rs:54-60 — inner_eth (control = exit_on_arp),
+// inner_l3: Option<L3>, inner_ulp: Option<Ulp>.
+struct GenericUlp {
+    static constexpr int CHAIN = INGOT_CHAIN_GENERIC_ULP;
+    std::shared_ptr<const Packet> pkt;
+    ValidEthernet inner_eth;
+    std::optional<L3> inner_l3;
+    std::optional<L4> inner_ulp;
+
+    static std::vector<types::ParseResult<Success<GenericUlp>>> parse_all(
+        const std::vector<std::vector<uint8_t>>& frames,
+        gpu::Context& ctx = gpu::default_context()) {
+        std::vector<types::ParseResult<Success<GenericUlp>>> out;
+        for (auto& p : gpu::parse_batch(ctx, frames, CHAIN)) {
+            auto sp = std::make_shared<const Packet>(std::move(p));
+            if (sp->fields.rec.status != INGOT_OK) {
+                out.push_back(types::ParseResult<Success<GenericUlp>>::err(
+                    detail::error_of(CHAIN, sp->fields.rec)));
+                continue;
+            }
+            GenericUlp c{sp, ValidEthernet(&sp->fields), std::nullopt, std::nullopt};
+            if (!(sp->fields.rec.flags & INGOT_REC_ACCEPTED)) {
+                c.inner_l3 = detail::l3_of(*sp);
+                c.inner_ulp = detail::l4_of(*sp);
+            }
+            out.push_back(types::ParseResult<Success<GenericUlp>>::ok(
+                Success<GenericUlp>{c, std::nullopt, detail::remainder(*sp)}));
+        }
+        return out;
+    }
+    static types::ParseResult<Success<GenericUlp>> parse(const std::vector<uint8_t>& frame) {
+        return std::move(parse_all({frame})[0]);
+    }
+    static types::ParseResult<Success<GenericUlp>> parse_slice(const std::vector<uint8_t>& frame) {
+        return parse(frame);
+    }
+};
+
+}  // namespace examples
+}  // namespace ingot

@@ -89,5 +89,32 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     return LIB
 
 
+CPP_TESTS = ROOT / "tests" / "cpp"
+
+
+def build_cpp_tests(verbose: bool = False) -> list[Path]:
+    """Compile the C++ mirror tests (tests/cpp/*.cpp) against the library."""
+    out_dir = CPP_TESTS / "build"
+    out_dir.mkdir(exist_ok=True)
+    outs = []
+    deps = _headers() + [ROOT / "include" / "ingot_amd.hpp", LIB]
+    for src in sorted(CPP_TESTS.glob("*.cpp")):
+        exe = out_dir / src.stem
+        outs.append(exe)
+        if not _stale(exe, [src] + deps):
+            continue
+        cmd = [hipcc(), "-std=c++17", "-O2", f"-I{ROOT / 'include'}", str(src),
+               f"-L{LIB.parent}", "-lingot_gpu", "-Wl,-rpath,$ORIGIN/../../../ingot_amd/lib",
+               "-o", str(exe)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            exe.unlink(missing_ok=True)
+            raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        if verbose:
+            print(f"built {exe}")
+    return outs
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv, verbose=True)
+    build_cpp_tests(verbose=True)

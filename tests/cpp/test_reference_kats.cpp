@@ -1,0 +1,256 @@
+// test_reference_kats.cpp — the reference's own chain-level tests, restated
+// against the C++ mirror (include/ingot_amd.hpp); every parse runs on the GPU.
+//
+// Each TEST follows one test of oxidecomputer/ingot @ 2025-08-08 (file:line in
+// its comment): the same frame construction and the same assertions.
+// Built by __graft_entry__.build() into tests/cpp/build/, run by
+// tests/test_cpp_mirror.py (pytest -m gpu).
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "ingot_amd.hpp"
+
+using namespace ingot;
+using namespace ingot::examples;
+using ingot::types::ParseError;
+
+static int g_failed = 0, g_run = 0;
+
+#define ASSERT_EQ(a, b)                                                                  \
+    do {                                                                                 \
+        if (!((a) == (b))) {                                                             \
+            std::fprintf(stderr, "  %s:%d: ASSERT_EQ(%s, %s) failed\n", __FILE__, __LINE__, \
+                         #a, #b);                                                        \
+            throw std::runtime_error("assertion");                                       \
+        }                                                                                \
+    } while (0)
+#define ASSERT_TRUE(a) ASSERT_EQ(!!(a), true)
+
+static std::vector<std::pair<const char*, std::function<void()>>>& registry() {
+    static std::vector<std::pair<const char*, std::function<void()>>> r;
+    return r;
+}
+struct Reg {
+    Reg(const char* n, std::function<void()> f) { registry().push_back({n, f}); }
+};
+#define TEST(name)                          \
+    static void name();                     \
+    static Reg reg_##name(#name, name);     \
+    static void name()
+
+static const MacAddr6 ABCDEF{0xa, 0xb, 0xc, 0xd, 0xe, 0xf};
+static const MacAddr6 BROADCAST{0xff, 0xff, 0xff, 0xff, 0xff, 0xff};
+
+static void put16(std::vector<uint8_t>& b, size_t at, uint16_t v) {
+    b[at] = (uint8_t)(v >> 8);
+    b[at + 1] = (uint8_t)v;
+}
+
+// ingot-examples/src/tests.rs:22-54
+TEST(parse_header_chain_with_narrowing) {
+    std::vector<uint8_t> buf2(14 + 20 + 8, 0);
+    for (int i = 0; i < 6; ++i) buf2[i] = BROADCAST[i], buf2[6 + i] = ABCDEF[i];
+    put16(buf2, 12, ethernet::Ethertype::IPV4);
+    buf2[14 + 9] = ip::IpProtocol::UDP;
+    const uint8_t src[4] = {192, 168, 0, 1}, dst[4] = {192, 168, 0, 255};
+    std::memcpy(&buf2[14 + 12], src, 4);
+    std::memcpy(&buf2[14 + 16], dst, 4);
+
+    auto [mystack, hint, rest] = UdpParser::parse(buf2).unwrap();
+    (void)hint;
+    ASSERT_TRUE(mystack.l3.ipv4.has_value());
+    (void)mystack.l3.ipv4->hop_limit();
+    ASSERT_EQ(mystack.eth.source(), ABCDEF);
+    ASSERT_EQ(rest.size(), 0u);
+}
+
+// ingot-examples/src/tests.rs:56-118
+TEST(variable_len_fields_in_header_chain) {
+    const size_t V4_EXTRA = 12;
+    std::vector<uint8_t> buf2(14 + 20 + V4_EXTRA + 8, 0);
+    for (int i = 0; i < 6; ++i) buf2[i] = BROADCAST[i], buf2[6 + i] = ABCDEF[i];
+    put16(buf2, 12, ethernet::Ethertype::IPV4);
+    buf2[14] = (uint8_t)(5 + V4_EXTRA / 4);  // set_ihl
+    buf2[14 + 9] = ip::IpProtocol::UDP;
+    const uint8_t src[4] = {192, 168, 0, 1}, dst[4] = {192, 168, 0, 255};
+    std::memcpy(&buf2[14 + 12], src, 4);
+    std::memcpy(&buf2[14 + 16], dst, 4);
+    for (size_t i = 0; i < V4_EXTRA; ++i) buf2[34 + i] = (uint8_t)i;
+    const size_t l = buf2.size();
+    put16(buf2, l - 8, 6082);
+    put16(buf2, l - 6, 6081);
+    put16(buf2, l - 4, 0);
+    put16(buf2, l - 2, 0xffff);
+
+    auto [mystack, hint, rest] = UdpParser::parse(buf2).unwrap();
+    (void)hint;
+    (void)rest;
+    ASSERT_EQ(mystack.eth.source(), ABCDEF);
+    ASSERT_EQ(mystack.eth.destination(), BROADCAST);
+    ASSERT_EQ(mystack.eth.ethertype(), ethernet::Ethertype::IPV4);
+    ASSERT_TRUE(mystack.l3.ipv4.has_value());
+    const auto& v4 = *mystack.l3.ipv4;
+    ASSERT_EQ(v4.protocol(), ip::IpProtocol::UDP);
+    ASSERT_EQ(v4.source(), (Ipv4Addr{192, 168, 0, 1}));
+    ASSERT_EQ(v4.destination(), (Ipv4Addr{192, 168, 0, 255}));
+    ASSERT_EQ(v4.ihl(), 8);
+    ASSERT_EQ(v4.options_ref(), (std::vector<uint8_t>{0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11}));
+    ASSERT_EQ(mystack.l4.source(), 6082);
+    ASSERT_EQ(mystack.l4.destination(), 6081);
+    ASSERT_EQ(mystack.l4.length(), 0);
+    ASSERT_EQ(mystack.l4.checksum(), 0xffff);
+}
+
+// ingot-examples/src/tests.rs:120-187 (values; chunks concatenated)
+TEST(parse_header_chain_multichunk_values) {
+    std::vector<uint8_t> f(14 + 40 + 8, 0);
+    for (int i = 0; i < 6; ++i) f[i] = BROADCAST[i], f[6 + i] = ABCDEF[i];
+    put16(f, 12, ethernet::Ethertype::IPV6);
+    f[14 + 6] = ip::IpProtocol::UDP;
+    f[14 + 8 + 15] = 1;  // Ipv6Addr::LOCALHOST
+    put16(f, 54, 6082);
+    put16(f, 56, 6081);
+    put16(f, 58, 128);
+    put16(f, 60, 0xffff);
+    f.insert(f.end(), 128, 0xaa);
+
+    auto [hdr, hint, rest] = UdpParser::parse(f).unwrap();
+    (void)hint;
+    ASSERT_EQ(hdr.eth.source(), ABCDEF);
+    ASSERT_EQ(hdr.eth.destination(), BROADCAST);
+    ASSERT_EQ(hdr.eth.ethertype(), ethernet::Ethertype::IPV6);
+    ASSERT_TRUE(hdr.l3.ipv6.has_value());
+    const auto& v6 = *hdr.l3.ipv6;
+    ASSERT_EQ(v6.next_header(), ip::IpProtocol::UDP);
+    ASSERT_EQ(v6.next_layer(), ip::IpProtocol::UDP);
+    Ipv6Addr lo{};
+    lo[15] = 1;
+    ASSERT_EQ(v6.source(), lo);
+    ASSERT_EQ(v6.destination(), Ipv6Addr{});
+    ASSERT_EQ(hdr.l4.source(), 6082);
+    ASSERT_EQ(hdr.l4.destination(), 6081);
+    ASSERT_EQ(hdr.l4.length(), 128);
+    ASSERT_EQ(hdr.l4.checksum(), 0xffff);
+    ASSERT_EQ(rest.size(), 128u);
+    for (auto b : rest) ASSERT_EQ(b, 0xaa);
+}
+
+static std::vector<uint8_t> would_be_valid() {
+    return {0xAA, 0x00, 0x04, 0x00, 0xFF, 0x10, 0xAA, 0x00, 0x04, 0x00, 0xFF, 0x01, 0x08, 0x00,
+            0x45, 0x00, 0x00, 28 + 8, 0x00, 0x00, 0x00, 0x00, 0xf0, 0x11, 0x00, 0x00,
+            8, 8, 8, 8, 192, 168, 0, 5,
+            0x00, 0x80, 0x00, 53, 0x00, 0x08, 0x00, 0x00};
+}
+
+// ingot-examples/src/tests.rs:307-379
+TEST(parse_reports_error_location) {
+    const auto v = would_be_valid();
+    auto cut = [&](size_t n) { return std::vector<uint8_t>(v.begin(), v.begin() + n); };
+    auto e = GenericUlp::parse_slice(cut(4)).unwrap_err();
+    ASSERT_EQ(e.error(), ParseError::TooSmall);
+    ASSERT_EQ(std::string(e.header()), "inner_eth");
+    e = GenericUlp::parse_slice(cut(14)).unwrap_err();
+    ASSERT_EQ(e.error(), ParseError::TooSmall);
+    ASSERT_EQ(std::string(e.header()), "inner_l3");
+    e = GenericUlp::parse_slice(cut(v.size() - 1)).unwrap_err();
+    ASSERT_EQ(e.error(), ParseError::TooSmall);
+    ASSERT_EQ(std::string(e.header()), "inner_ulp");
+
+    auto u = v;
+    u[14 + 9] = 0x59;  // OSPF
+    e = GenericUlp::parse_slice(u).unwrap_err();
+    ASSERT_EQ(e.error(), ParseError::Unwanted);
+    ASSERT_EQ(std::string(e.header()), "inner_ulp");
+}
+
+// ingot-examples/src/tests.rs:277-305 (single-slice half)
+TEST(chunks_present_on_early_accept) {
+    std::vector<uint8_t> pkt = {0xA8, 0x40, 0x25, 0x77, 0x77, 0x76, 0xA8, 0x40, 0x25, 0x77, 0x77,
+                                0x77, 0x08, 0x06, 0, 1, 2, 3, 4, 5, 6, 7};
+    auto [g, hint, b] = GenericUlp::parse(pkt).unwrap();
+    (void)hint;
+    ASSERT_TRUE(!g.inner_l3.has_value());
+    ASSERT_TRUE(!g.inner_ulp.has_value());
+    ASSERT_EQ(b.size(), 8u);
+}
+
+// ingot-examples/src/tests.rs:416-423 (single chunk of the straddle test)
+TEST(straddle_failure_single_chunk) {
+    const auto v = would_be_valid();
+    auto e = GenericUlp::parse_slice(std::vector<uint8_t>(v.begin(), v.begin() + 16)).unwrap_err();
+    ASSERT_EQ(e.error(), ParseError::TooSmall);
+    ASSERT_EQ(std::string(e.header()), "inner_l3");
+}
+
+// ingot/src/tests.rs:296-369, through a chain (Ethernet prefix, UDP suffix)
+TEST(v6_repeat_extension_headers) {
+    std::vector<uint8_t> f(14, 0);
+    put16(f, 12, ethernet::Ethertype::IPV6);
+    const uint8_t v6[] = {0x6A, 0x61, 0xe2, 0x40, 0x00, 0x10, 0x00, 0xf0,
+                          0xFD, 0, 0, 0, 0, 0xF7, 1, 1, 0, 0, 0, 0, 0, 0, 0, 2,
+                          0xFD, 0, 0, 0, 0, 0xF7, 1, 1, 0, 0, 0, 0, 0, 0, 0, 1,
+                          44, 0x00, 0, 0, 0, 0, 0, 0,
+                          253, 0, 0, 0, 0, 0, 0, 0,
+                          0x11, 0x04};
+    f.insert(f.end(), std::begin(v6), std::end(v6));
+    f.insert(f.end(), 38, 0);
+    const uint8_t udp[] = {0, 1, 0, 2, 0, 8, 0, 0};
+    f.insert(f.end(), std::begin(udp), std::end(udp));
+
+    auto [s, hint, rest] = UdpParser::parse(f).unwrap();
+    (void)hint;
+    (void)rest;
+    ASSERT_TRUE(s.l3.ipv6.has_value());
+    const auto& x = *s.l3.ipv6;
+    ASSERT_EQ(x.next_layer(), ip::IpProtocol::UDP);
+    ASSERT_EQ(x.extension_header_count(), 3u);
+    ASSERT_EQ(x.extension_header(0).kind, INGOT_EH_RFC6564);
+    ASSERT_EQ(x.extension_header(0).next_header, ip::IpProtocol::IPV6_FRAGMENT);
+    ASSERT_EQ(x.extension_header(0).ext_len, 0);
+    ASSERT_EQ(x.extension_header(1).kind, INGOT_EH_FRAGMENT);
+    ASSERT_EQ(x.extension_header(1).next_header, ip::IpProtocol::IPV6_EXPERIMENT0);
+    ASSERT_EQ(x.extension_header(2).kind, INGOT_EH_RFC6564);
+    ASSERT_EQ(x.extension_header(2).next_header, ip::IpProtocol::UDP);
+    ASSERT_EQ(x.extension_header(2).ext_len, 4);
+    // bitset_fields_do_not_disturb_neighbours (ingot/src/tests.rs:223-294)
+    ASSERT_EQ(x.version(), 6);
+    ASSERT_EQ(x.dscp(), 41);
+    ASSERT_EQ(x.ecn(), ip::Ecn::Capable1);
+    ASSERT_EQ(x.flow_label(), 123456u);
+}
+
+// ingot-examples/benches/packet.rs:15-34, 136-138 (batched: the bench loop)
+TEST(bench_parse_stack_v4_batch) {
+    std::vector<uint8_t> v4 = {0, 0, 0, 0, 0, 0, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0x08, 0x00,
+                               0x45, 0x00, 0x00, 28 + 8, 0, 0, 0, 0, 0xf0, 0x11, 0, 0,
+                               192, 168, 0, 1, 192, 168, 0, 255,
+                               0x00, 0x80, 0x17, 0xc1, 0x00, 0x08, 0x00, 0x00,
+                               0, 1, 2, 3, 4, 5, 6, 7};
+    std::vector<std::vector<uint8_t>> batch(1000, v4);
+    auto res = UdpParser::parse_all(batch);
+    ASSERT_EQ(res.size(), 1000u);
+    for (auto& r : res) {
+        auto& [s, hint, rest] = r.unwrap();
+        (void)hint;
+        ASSERT_EQ(s.l4.destination(), 0x17c1);
+        ASSERT_EQ(rest.size(), 8u);
+    }
+}
+
+int main() {
+    for (auto& [name, fn] : registry()) {
+        ++g_run;
+        try {
+            fn();
+            std::printf("ok   %s\n", name);
+        } catch (const std::exception& e) {
+            ++g_failed;
+            std::printf("FAIL %s: %s\n", name, e.what());
+        }
+    }
+    std::printf("%d run, %d failed\n", g_run, g_failed);
+    return g_failed ? 1 : 0;
+}

@@ -1,0 +1,33 @@
+"""The C++ host mirror (include/ingot_amd.hpp): the reference's chain tests
+restated in C++ (tests/cpp/test_reference_kats.cpp), run on the GPU."""
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def test_cpp_mirror_compiles():
+    from ingot_amd.build import build, build_cpp_tests
+
+    build()
+    exes = build_cpp_tests()
+    assert exes and all(e.exists() for e in exes)
+
+
+@pytest.mark.gpu
+def test_cpp_reference_kats_on_device():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    exe = ROOT / "tests" / "cpp" / "build" / "test_reference_kats"
+    if not exe.exists():
+        from ingot_amd.build import build_cpp_tests
+
+        build_cpp_tests()
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert " 0 failed" in r.stdout
