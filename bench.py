@@ -218,6 +218,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=1.5)
     ap.add_argument("--rotate-mib", type=int, default=512,
                     help="minimum bytes of distinct arenas rotated across steps")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="nccl = RCCL over xGMI (default); gloo only to rehearse N>1 on one GPU")
     args = ap.parse_args()
 
     import torch
@@ -226,14 +228,22 @@ def main():
     import ingot_amd
     from ingot_amd import Chain, GenProfile
 
+    from ingot_amd import dist as idist
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one GPU per rank; a --dist-backend gloo rehearsal may fold ranks onto
+    # fewer GPUs (e.g. the 1-GPU test box)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     prof_name, n, stride, chain_name, desc = CONFIGS[args.config]
     profile, chain = GenProfile[prof_name], Chain[chain_name]
@@ -241,7 +251,7 @@ def main():
     lib = ingot_amd.load_library()
 
     # --- data: this rank's shard (pure in (seed, index)) + R copies ---
-    first = rank * n
+    first, n = idist.shard(rank, world, n)
     arena, off, lens = ingot_amd.gen_frames(profile, n, first=first, stride=stride,
                                             device=local)
     reps = max(1, -(-(args.rotate_mib << 20) // arena.numel()))
@@ -253,8 +263,6 @@ def main():
 
     flows = args.config == "c5"
     if flows:
-        from ingot_amd import dist as idist
-
         hists = [torch.zeros(FLOW_BINS, dtype=torch.int32, device=dev) for _ in range(reps)]
         flow_ids = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(reps)]
 
@@ -277,11 +285,7 @@ def main():
     ms_region, wall = main_run.run(args.steps)
     if world > 1:
         dist.barrier()
-    t_sec = ms_region / 1e3
-    if world > 1:
-        tt = torch.tensor([t_sec], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_sec = float(tt.item())
+    t_sec = idist.max_over_ranks(ms_region / 1e3, device=dev)
     value = n * args.steps * world / t_sec / 1e6
     ms_step = t_sec * 1e3 / args.steps
 

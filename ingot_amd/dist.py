@@ -23,13 +23,26 @@ def split(n_total: int, rank: int, world: int) -> tuple[int, int]:
     return first, base + (1 if rank < extra else 0)
 
 
+def _active():
+    import torch.distributed as dist
+
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def _gloo() -> bool:
+    import torch.distributed as dist
+
+    return dist.get_backend() == "gloo"
+
+
 def max_over_ranks(value: float, device=None) -> float:
     import torch
     import torch.distributed as dist
 
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _active():
         return float(value)
-    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dev = None if _gloo() else device
+    t = torch.tensor([float(value)], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -42,8 +55,13 @@ def reduce_histogram(hist):
     import torch
     import torch.distributed as dist
 
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _active():
         return hist
     view = hist.view(torch.int32) if hist.dtype != torch.int32 else hist
-    dist.all_reduce(view, op=dist.ReduceOp.SUM)
+    if _gloo() and view.is_cuda:  # rehearsal backend: reduce through host memory
+        host = view.cpu()
+        dist.all_reduce(host, op=dist.ReduceOp.SUM)
+        view.copy_(host)
+    else:
+        dist.all_reduce(view, op=dist.ReduceOp.SUM)
     return hist
