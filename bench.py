@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py — device-resident L2/L3/L4 parse throughput on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c3s|c4|c5|c6]
                     [--streams S] [--record 16|8]
 
 A *step* is one launch of the parse path over one batch of synthetic frames
@@ -59,6 +59,10 @@ CONFIGS = {
     "c5": ("FLOWS", 1 << 23, None, "VlanUlp",
            "C5: C4 framing, 65,536 Zipf(1.1) flows; parse + RSS Toeplitz 5-tuple hash + "
            "per-flow histogram (65,536 x u32) + RCCL all-reduce per step, 8,388,608 per GPU"),
+    "c6": ("GENEVE", 1 << 23, None, "GeneveOverV6Tunnel",
+           "C6 (SURVEY 8f-1): 8,388,608 Geneve-over-IPv6 tunnel frames per GPU (OPTE inbound: "
+           "outer Eth/IPv6/UDP/Geneve+options, inner 64-1500 B Eth/v4|v6/TCP|UDP|ICMP, 2% ARP), "
+           "packed, GeneveOverV6Tunnel"),
 }
 FLOW_BINS = 1 << 16
 
@@ -275,6 +279,8 @@ def main():
 
     if flows:
         args.streams, args.no_variants = 1, True
+    if chain == Chain.GeneveOverV6Tunnel and args.record == 8:
+        ap.error("8-B records are not offered for the tunnel chain (include/ingot_gpu.h)")
     main_run = runner(args.streams, args.record)
     main_run.run(args.warmup)
 
@@ -327,6 +333,8 @@ def main():
         vsteps = min(args.steps, 1000)
         for ns, rb in ((1, 16), (2, 8), (1, 8), (4, 16)):
             if (ns, rb) == (args.streams, args.record):
+                continue
+            if rb == 8 and chain == Chain.GeneveOverV6Tunnel:
                 continue
             r = runner(ns, rb)
             r.run(min(args.warmup, 50))

@@ -71,12 +71,19 @@ enum ingot_status {
  *              no chain uses it): eth, 0..2 x VlanBody while the ethertype is
  *              0x8100/0x9100, L3, Ulp; no control.  Labels "eth", "vlan",
  *              "l3", "l4".  Parity for this chain is unpinned by the reference.
+ * GENEVE_OVER_V6  ingot-examples/src/packets.rs:27-40 (OPTE's inbound path)
+ *              outer_eth: Ethernet, outer_v6: from L3 -> Ipv6 (+EHs),
+ *              outer_udp: from L4 -> Udp, outer_encap: Geneve (+options,
+ *              geneve.rs:16-44), then GenericUlp's three layers (control =
+ *              exit_on_arp on inner_eth).  Labels "outer_eth", "outer_v6",
+ *              "outer_udp", "outer_encap", "inner_eth", "inner_l3", "inner_ulp".
  * ------------------------------------------------------------------------- */
 enum ingot_chain {
     INGOT_CHAIN_UDP_PARSER = 0,
     INGOT_CHAIN_GENERIC_ULP = 1,
     INGOT_CHAIN_VLAN_ULP = 2,
-    INGOT_CHAIN_COUNT = 3
+    INGOT_CHAIN_GENEVE_OVER_V6 = 3,
+    INGOT_CHAIN_COUNT = 4
 };
 
 enum ingot_l3_kind { INGOT_L3_NONE = 0, INGOT_L3_IPV4 = 1, INGOT_L3_IPV6 = 2 };
@@ -90,6 +97,7 @@ enum ingot_l4_kind {
 
 /* rec.flags */
 #define INGOT_REC_ACCEPTED 0x01u /* a parse control accepted early (parse.rs:221-254) */
+#define INGOT_REC_INNER 0x02u    /* tunnel chain: the walk reached inner_eth */
 
 /* ---------------------------------------------------------------------------
  * ingot_rec — the 16-byte per-packet result.
@@ -110,6 +118,14 @@ enum ingot_l4_kind {
  *                     last extension header's next_header, ip.rs:180-181,
  *                     util.rs:189-228).
  *   n_vlan/n_v6ext    VLAN tags / IPv6 extension headers fully parsed.
+ *
+ * GENEVE_OVER_V6: the fields describe the innermost layers reached.  While
+ * the walk is in the outer layers they describe outer_v6 / outer_udp; once
+ * inner_eth parses, flags |= INGOT_REC_INNER and l3/l4 kind, offsets,
+ * n_v6ext, l4_proto restart for the inner frame (ethertype = the inner one).
+ * The inner frame then starts at l3_off - 14 (inner L3 reached) or
+ * payload_off - 14 (walk ended at inner_eth); ingot_gpu_geneve_fields gives
+ * every outer offset and getter.
  * ------------------------------------------------------------------------- */
 typedef struct ingot_rec {
     uint8_t status;
@@ -234,11 +250,75 @@ typedef struct ingot_fields {
     uint8_t _pad1[52];                  /* 204 -> 256 */
 } ingot_fields;
 
+/* ---------------------------------------------------------------------------
+ * GENEVE_OVER_V6 parity mode: the outer layers' getters (128 B) after the
+ * inner frame's ingot_fields (whose eth_* / v4_* / v6_* / l4 fields are
+ * inner_eth / inner_l3 / inner_ulp).  Geneve getters follow geneve.rs:16-44:
+ * version u2, opt_len u6, flags = GeneveFlags::from_bits_truncate (bits 0xC0
+ * kept), protocol_type u16be, vni [u8;3] as a 24-bit BE integer, reserved
+ * u8.  Options (Repeated<GeneveOpt>, geneve.rs:80-102) are listed in order;
+ * the first INGOT_MAX_GENEVE_OPT_FIELDS are materialised, the count is exact.
+ * ------------------------------------------------------------------------- */
+#define INGOT_MAX_GENEVE_OPT_FIELDS 4
+
+typedef struct ingot_geneve_opt {
+    uint16_t opt_class;     /* class (u16be) */
+    uint16_t data_off;      /* frame offset of data (length*4 bytes) */
+    uint8_t option_type;    /* GeneveOptionType (is_critical = bit 7) */
+    uint8_t reserved;       /* u3 */
+    uint8_t length;         /* u5, in 4-byte words */
+    uint8_t _pad;
+} ingot_geneve_opt;
+
+typedef struct ingot_tunnel_fields {
+    uint8_t outer_eth_destination[6];   /*   0 */
+    uint8_t outer_eth_source[6];        /*   6 */
+    uint16_t outer_eth_ethertype;       /*  12 */
+    uint16_t outer_udp_off;             /*  14  frame offset of outer_udp */
+    uint8_t outer_v6_source[16];        /*  16 */
+    uint8_t outer_v6_destination[16];   /*  32 */
+    uint32_t outer_v6_flow_label;       /*  48 */
+    uint16_t outer_v6_payload_len;      /*  52 */
+    uint16_t outer_v6_ext_len;          /*  54  EH span bytes (from offset 54) */
+    uint8_t outer_v6_version;           /*  56 */
+    uint8_t outer_v6_dscp;              /*  57 */
+    uint8_t outer_v6_ecn_raw;           /*  58 */
+    uint8_t outer_v6_ecn;               /*  59 */
+    uint8_t outer_v6_next_header;       /*  60 */
+    uint8_t outer_v6_hop_limit;         /*  61 */
+    uint8_t outer_v6_n_ext;             /*  62 */
+    uint8_t outer_l4_proto;             /*  63  hint handed to the outer L4 choice */
+    uint16_t outer_udp_source;          /*  64 */
+    uint16_t outer_udp_destination;     /*  66 */
+    uint16_t outer_udp_length;          /*  68 */
+    uint16_t outer_udp_checksum;        /*  70 */
+    uint16_t geneve_off;                /*  72 */
+    uint16_t inner_eth_off;             /*  74 */
+    uint32_t geneve_vni;                /*  76 */
+    uint16_t geneve_protocol_type;      /*  80 */
+    uint8_t geneve_version;             /*  82 */
+    uint8_t geneve_opt_len;             /*  83 */
+    uint8_t geneve_flags;               /*  84 */
+    uint8_t geneve_reserved;            /*  85 */
+    uint8_t geneve_n_opts;              /*  86  (saturates at 255) */
+    uint8_t geneve_critical;            /*  87  any option_type.is_critical() */
+    ingot_geneve_opt geneve_opt[INGOT_MAX_GENEVE_OPT_FIELDS]; /* 88 (4 x 8) */
+    uint8_t _pad[8];                    /* 120 -> 128 */
+} ingot_tunnel_fields;
+
+typedef struct ingot_geneve_fields {
+    ingot_fields inner;                 /*   0  rec + inner layers */
+    ingot_tunnel_fields outer;          /* 256 */
+} ingot_geneve_fields;
+
 #ifdef __cplusplus
 static_assert(sizeof(ingot_rec) == 16, "ingot_rec is 16 bytes");
 static_assert(sizeof(ingot_rec8) == 8, "ingot_rec8 is 8 bytes");
 static_assert(sizeof(ingot_v6eh) == 12, "ingot_v6eh is 12 bytes");
 static_assert(sizeof(ingot_fields) == 256, "ingot_fields is 256 bytes");
+static_assert(sizeof(ingot_geneve_opt) == 8, "ingot_geneve_opt is 8 bytes");
+static_assert(sizeof(ingot_tunnel_fields) == 128, "ingot_tunnel_fields is 128 bytes");
+static_assert(sizeof(ingot_geneve_fields) == 384, "ingot_geneve_fields is 384 bytes");
 #endif
 
 /* API return codes (negative). */
@@ -303,7 +383,8 @@ int ingot_gpu_parse_strided(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
                             uint32_t stride, const uint16_t* d_len, uint64_t n,
                             int chain, ingot_rec* d_out, void* stream);
 
-/* The two batch calls above with 8-byte ingot_rec8 records. */
+/* The two batch calls above with 8-byte ingot_rec8 records.  Not for
+ * GENEVE_OVER_V6 (EINVAL): the inner offsets do not fit its derivation rules. */
 int ingot_gpu_parse_compact(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
                             const uint64_t* d_off, const uint16_t* d_len,
                             uint64_t n, int chain, ingot_rec8* d_out,
@@ -322,6 +403,17 @@ int ingot_gpu_fields(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
                      const uint64_t* d_off, const uint16_t* d_len,
                      uint32_t stride, uint64_t n, int chain,
                      ingot_fields* d_out, void* stream);
+/* (chain GENEVE_OVER_V6 is EINVAL here: use ingot_gpu_geneve_fields.) */
+
+/*
+ * Parity mode for GeneveOverV6Tunnel (384 B per packet): the inner frame's
+ * ingot_fields + the outer layers' ingot_tunnel_fields.  Same inputs as
+ * ingot_gpu_fields, chain implied.
+ */
+int ingot_gpu_geneve_fields(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
+                            const uint64_t* d_off, const uint16_t* d_len,
+                            uint32_t stride, uint64_t n,
+                            ingot_geneve_fields* d_out, void* stream);
 
 /*
  * Flow classification + per-flow histogram (config 5; build-defined, ingot

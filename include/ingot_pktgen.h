@@ -22,6 +22,14 @@
  *                          of those), IPv6 p .5 with EHs p .5.
  *   INGOT_GEN_FLOWS        C5: C4 framing; the 5-tuple is drawn from 65,536
  *                          flows with Zipf(1.1) popularity.
+ *   INGOT_GEN_GENEVE       C6 (GeneveOverV6Tunnel, OPTE inbound): outer Eth /
+ *                          IPv6 (HBH p .05) / UDP 6081 / Geneve with 0, 1
+ *                          (class 0x0129, p .8) or 2 options; inner Eth with
+ *                          ARP p .02, IPv4 p .68, IPv6 p .30; TCP p .75, UDP
+ *                          p .22, ICMP p .03; inner length U[64,1500].
+ *   INGOT_GEN_GENEVE_ADVERSARIAL  tunnel-shaped fuzz: outer ethertype / EHs /
+ *                          L4 / Geneve option spans perturbed, adversarial
+ *                          inner chain, lengths clustered at the chain's end.
  */
 #ifndef INGOT_PKTGEN_H
 #define INGOT_PKTGEN_H
@@ -37,7 +45,9 @@ enum ingot_gen_profile {
     INGOT_GEN_V4UDP64 = 2,
     INGOT_GEN_MIXED = 3,
     INGOT_GEN_VLAN_V6EH = 4,
-    INGOT_GEN_FLOWS = 5
+    INGOT_GEN_FLOWS = 5,
+    INGOT_GEN_GENEVE = 6,
+    INGOT_GEN_GENEVE_ADVERSARIAL = 7
 };
 
 #define INGOT_GEN_SEED 20250808ull

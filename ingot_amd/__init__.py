@@ -3,10 +3,11 @@ parse semantics.
 
 Host-side mirror of the reference's parse interface above the C ABI
 (include/ingot_gpu.h).  The batch API (`Context.parse*`) is the hot path; the
-per-packet classes `UdpParser`, `GenericUlp`, `VlanUlp` mirror ingot's
+per-packet classes `UdpParser`, `GenericUlp`, `VlanUlp`, `GeneveOverV6Tunnel` mirror ingot's
 `#[derive(Parse)]` chains (`Chain::parse(bytes) -> (headers, None, remainder)`
 raising `PacketParseError{label, inner}`) so tests read like the reference's
-own (ingot-examples/src/tests.rs).  Everything runs through the gfx950
+own (ingot-examples/src/tests.rs); `GeneveOverV6Tunnel` adds the outer
+layers (packets.rs:27-40).  Everything runs through the gfx950
 library; nothing here parses bytes on the CPU.
 
 Device memory, streams and torch.distributed come from PyTorch (plumbing).
@@ -24,6 +25,9 @@ from .abi import (  # noqa: F401  (re-exports)
     FIELDS_BYTES,
     FIELDS_DTYPE,
     GEN_SEED,
+    GENEVE_FIELDS_DTYPE,
+    MAX_GENEVE_OPT_FIELDS,
+    REC_INNER,
     MAX_EH_FIELDS,
     REC_ACCEPTED,
     REC8_BYTES,
@@ -44,7 +48,7 @@ from .abi import (  # noqa: F401  (re-exports)
 
 __all__ = [
     "Chain", "Context", "GenProfile", "PacketParseError", "ParseError", "UdpParser",
-    "GenericUlp", "VlanUlp", "gen_frames", "gen_lengths", "records_to_numpy",
+    "GenericUlp", "VlanUlp", "GeneveOverV6Tunnel", "gen_frames", "gen_lengths", "records_to_numpy",
     "fields_to_numpy", "load_library",
 ]
 
@@ -186,6 +190,21 @@ class Context:
                    "ingot_gpu_fields")
         return out
 
+    def geneve_fields(self, arena, off, lens, stride: int = 0, n: Optional[int] = None,
+                      out=None, stream=None):
+        """GeneveOverV6Tunnel parity mode: (n, 384) uint8 tensor of
+        ingot_geneve_fields (inner ingot_fields + outer ingot_tunnel_fields)."""
+        torch = _torch()
+        if n is None:
+            n = off.numel()
+        if out is None:
+            out = torch.empty((n, GENEVE_FIELDS_DTYPE.itemsize), dtype=torch.uint8,
+                              device=arena.device)
+        self._check_dev(arena, off, lens, out)
+        _lib.check(self._lib.ingot_gpu_geneve_fields(self._h, _ptr(arena), _ptr(off), _ptr(lens),
+                                                     int(stride), n, _ptr(out), _stream(stream)),
+                   "ingot_gpu_geneve_fields")
+        return out
 
     def flow_hist(self, arena, off, lens, chain: Chain, hist=None, bins: Optional[int] = None,
                   stride: int = 0, n: Optional[int] = None, key: Optional[bytes] = None,
@@ -224,6 +243,13 @@ def fields_to_numpy(t):
 
     a = t.cpu().numpy() if hasattr(t, "cpu") else np.asarray(t)
     return np.ascontiguousarray(a).view(FIELDS_DTYPE).reshape(-1)
+
+
+def geneve_fields_to_numpy(t):
+    import numpy as np
+
+    a = t.cpu().numpy() if hasattr(t, "cpu") else np.asarray(t)
+    return np.ascontiguousarray(a).view(GENEVE_FIELDS_DTYPE).reshape(-1)
 
 
 # ---------------------------------------------------------------------------
@@ -294,6 +320,100 @@ class EthernetView(_View):
 
     def ethertype(self) -> int:
         return int(self.f["eth_ethertype"])
+
+
+class OuterEthernetView(_View):
+    def destination(self) -> bytes:
+        return bytes(self.f["outer_eth_destination"])
+
+    def source(self) -> bytes:
+        return bytes(self.f["outer_eth_source"])
+
+    def ethertype(self) -> int:
+        return int(self.f["outer_eth_ethertype"])
+
+
+class OuterIpv6View(_View):
+    def __getattr__(self, name):
+        key = "outer_v6_" + name
+        if key in GENEVE_FIELDS_DTYPE["outer"].names:
+            v = self.f[key]
+            return (lambda: bytes(v)) if v.shape else (lambda: int(v))
+        raise AttributeError(name)
+
+    def v6ext_bytes(self) -> bytes:
+        return self.frame[self.off + 40:self.off + 40 + int(self.f["outer_v6_ext_len"])]
+
+    def next_layer(self) -> int:
+        return int(self.f["outer_l4_proto"])
+
+
+class OuterUdpView(_View):
+    def source(self) -> int:
+        return int(self.f["outer_udp_source"])
+
+    def destination(self) -> int:
+        return int(self.f["outer_udp_destination"])
+
+    def length(self) -> int:
+        return int(self.f["outer_udp_length"])
+
+    def checksum(self) -> int:
+        return int(self.f["outer_udp_checksum"])
+
+
+@dataclass
+class GeneveOpt:
+    """ingot::geneve::GeneveOpt (geneve.rs:80-102) with its data bytes."""
+
+    opt_class: int
+    option_type: int
+    reserved: int
+    length: int
+    data: bytes
+
+    def is_critical(self) -> bool:
+        return (self.option_type >> 7) == 1
+
+
+class GeneveView(_View):
+    """ingot::geneve::ValidGeneve getters (geneve.rs:16-44)."""
+
+    def version(self) -> int:
+        return int(self.f["geneve_version"])
+
+    def opt_len(self) -> int:
+        return int(self.f["geneve_opt_len"])
+
+    def flags(self) -> int:
+        return int(self.f["geneve_flags"])
+
+    def protocol_type(self) -> int:
+        return int(self.f["geneve_protocol_type"])
+
+    def vni(self) -> int:
+        return int(self.f["geneve_vni"])
+
+    def reserved(self) -> int:
+        return int(self.f["geneve_reserved"])
+
+    def options_ref(self) -> bytes:
+        return self.frame[self.off + 8:self.off + 8 + 4 * self.opt_len()]
+
+    def packet_length(self) -> int:
+        return 8 + 4 * self.opt_len()
+
+    def options(self) -> list:
+        """The first MAX_GENEVE_OPT_FIELDS options (n_options() is exact)."""
+        out = []
+        for g in self.f["geneve_opt"][:min(self.n_options(), MAX_GENEVE_OPT_FIELDS)]:
+            o, ln = int(g["data_off"]), int(g["length"])
+            out.append(GeneveOpt(int(g["opt_class"]), int(g["option_type"]), int(g["reserved"]),
+                                 ln, self.frame[o:o + 4 * ln]))
+        return out
+
+    def n_options(self) -> int:
+        return int(self.f["geneve_n_opts"])
 
 
 class VlanView(_View):
@@ -474,9 +594,12 @@ def parse_frames(frames: list, chain: Chain, device: int = 0):
     off = torch.tensor(offs_l, dtype=torch.int64, device=dev)
     lens = torch.tensor(lens_l, dtype=torch.int32, device=dev).to(torch.uint16)
     recs = ctx.parse(arena, off, lens, chain)
-    flds = ctx.fields(arena, off, lens, chain)
+    if chain == Chain.GeneveOverV6Tunnel:
+        flds = geneve_fields_to_numpy(ctx.geneve_fields(arena, off, lens))
+    else:
+        flds = fields_to_numpy(ctx.fields(arena, off, lens, chain))
     torch.cuda.synchronize(device)
-    return records_to_numpy(recs), fields_to_numpy(flds)
+    return records_to_numpy(recs), flds
 
 
 class _ChainParser:
@@ -500,7 +623,15 @@ class _ChainParser:
                                    ParseError(status))
         layers = {}
         eth_name, l3_name, l4_name = cls.names[0], cls.names[-2], cls.names[-1]
-        layers[eth_name] = EthernetView(frame, f, 0)
+        eth_off = 0
+        if cls.chain == Chain.GeneveOverV6Tunnel:
+            t, f = f["outer"], f["inner"]
+            eth_name, eth_off = "inner_eth", int(t["inner_eth_off"])
+            layers["outer_eth"] = OuterEthernetView(frame, t, 0)
+            layers["outer_v6"] = OuterIpv6View(frame, t, 14)
+            layers["outer_udp"] = OuterUdpView(frame, t, int(t["outer_udp_off"]))
+            layers["outer_encap"] = GeneveView(frame, t, int(t["geneve_off"]))
+        layers[eth_name] = EthernetView(frame, f, eth_off)
         if cls.chain == Chain.VlanUlp:
             tags = []
             for k in range(int(r["n_vlan"])):
@@ -545,3 +676,11 @@ class VlanUlp(_ChainParser):
 
     chain = Chain.VlanUlp
     names = ("eth", "vlan", "l3", "l4")
+
+
+class GeneveOverV6Tunnel(_ChainParser):
+    """ingot-examples/src/packets.rs:27-40 (OPTE's inbound path)."""
+
+    chain = Chain.GeneveOverV6Tunnel
+    names = ("outer_eth", "outer_v6", "outer_udp", "outer_encap", "inner_eth", "inner_l3",
+             "inner_ulp")

@@ -46,6 +46,10 @@ SIGNATURES = {
         [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, ctypes.c_uint32, c_u64, ctypes.c_int, c_u8p,
          ctypes.c_void_p],
     ),
+    "ingot_gpu_geneve_fields": (
+        ctypes.c_int,
+        [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, ctypes.c_uint32, c_u64, c_u8p, ctypes.c_void_p],
+    ),
     "ingot_gpu_flow_hist": (
         ctypes.c_int,
         [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, ctypes.c_uint32, c_u64, ctypes.c_int, c_u8p,

@@ -38,12 +38,15 @@ class Chain(enum.IntEnum):
     UdpParser = 0    # ingot-examples/src/packets.rs:18-24
     GenericUlp = 1   # ingot-examples/src/packets.rs:54-60
     VlanUlp = 2      # build-defined (VlanBody, ethernet.rs:57-65)
+    GeneveOverV6Tunnel = 3  # ingot-examples/src/packets.rs:27-40
 
 
 CHAIN_LABELS = {
     Chain.UdpParser: ("eth", "l3", "l4"),
     Chain.GenericUlp: ("inner_eth", "inner_l3", "inner_ulp"),
     Chain.VlanUlp: ("eth", "vlan", "l3", "l4"),
+    Chain.GeneveOverV6Tunnel: ("outer_eth", "outer_v6", "outer_udp", "outer_encap", "inner_eth",
+                               "inner_l3", "inner_ulp"),
 }
 
 
@@ -62,7 +65,9 @@ class L4Kind(enum.IntEnum):
 
 
 REC_ACCEPTED = 0x01
+REC_INNER = 0x02
 MAX_EH_FIELDS = 4
+MAX_GENEVE_OPT_FIELDS = 4
 
 # ingot_gpu_ctx_set_tuning keys
 TUNE_WINDOW_INDEXED = 1
@@ -175,14 +180,71 @@ class IngotFields(ctypes.Structure):
     ]
 
 
+class IngotGeneveOpt(ctypes.Structure):
+    _fields_ = [
+        ("opt_class", U16),
+        ("data_off", U16),
+        ("option_type", U8),
+        ("reserved", U8),
+        ("length", U8),
+        ("_pad", U8),
+    ]
+
+
+class IngotTunnelFields(ctypes.Structure):
+    _fields_ = [
+        ("outer_eth_destination", U8 * 6),
+        ("outer_eth_source", U8 * 6),
+        ("outer_eth_ethertype", U16),
+        ("outer_udp_off", U16),
+        ("outer_v6_source", U8 * 16),
+        ("outer_v6_destination", U8 * 16),
+        ("outer_v6_flow_label", U32),
+        ("outer_v6_payload_len", U16),
+        ("outer_v6_ext_len", U16),
+        ("outer_v6_version", U8),
+        ("outer_v6_dscp", U8),
+        ("outer_v6_ecn_raw", U8),
+        ("outer_v6_ecn", U8),
+        ("outer_v6_next_header", U8),
+        ("outer_v6_hop_limit", U8),
+        ("outer_v6_n_ext", U8),
+        ("outer_l4_proto", U8),
+        ("outer_udp_source", U16),
+        ("outer_udp_destination", U16),
+        ("outer_udp_length", U16),
+        ("outer_udp_checksum", U16),
+        ("geneve_off", U16),
+        ("inner_eth_off", U16),
+        ("geneve_vni", U32),
+        ("geneve_protocol_type", U16),
+        ("geneve_version", U8),
+        ("geneve_opt_len", U8),
+        ("geneve_flags", U8),
+        ("geneve_reserved", U8),
+        ("geneve_n_opts", U8),
+        ("geneve_critical", U8),
+        ("geneve_opt", IngotGeneveOpt * MAX_GENEVE_OPT_FIELDS),
+        ("_pad", U8 * 8),
+    ]
+
+
+class IngotGeneveFields(ctypes.Structure):
+    _fields_ = [("inner", IngotFields), ("outer", IngotTunnelFields)]
+
+
 assert ctypes.sizeof(IngotRec) == 16
 assert ctypes.sizeof(IngotRec8) == 8
 assert ctypes.sizeof(IngotV6Eh) == 12
 assert ctypes.sizeof(IngotFields) == 256
+assert ctypes.sizeof(IngotGeneveOpt) == 8
+assert ctypes.sizeof(IngotTunnelFields) == 128
+assert ctypes.sizeof(IngotGeneveFields) == 384
 
 REC_DTYPE = np.dtype(IngotRec)
 FIELDS_DTYPE = np.dtype(IngotFields)
 REC8_DTYPE = np.dtype(IngotRec8)
+GENEVE_FIELDS_DTYPE = np.dtype(IngotGeneveFields)
 REC_BYTES = REC_DTYPE.itemsize
 REC8_BYTES = REC8_DTYPE.itemsize
 
@@ -214,6 +276,8 @@ class GenProfile(enum.IntEnum):
     MIXED = 3
     VLAN_V6EH = 4
     FLOWS = 5
+    GENEVE = 6              # OPTE-style Geneve-over-IPv6 tunnel traffic
+    GENEVE_ADVERSARIAL = 7  # tunnel-shaped frames with every outer/inner defect
 
 
 GEN_SEED = 20250808

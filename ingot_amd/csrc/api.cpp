@@ -4,7 +4,7 @@
 // ingot's error surface: ParseError::as_cstr (ingot-types/src/error.rs:49-60)
 // and the per-layer labels a generated chain attaches to PacketParseError
 // (ingot-macros/src/parse.rs:36-50, field names from
-// ingot-examples/src/packets.rs:18-24, 54-60).
+// ingot-examples/src/packets.rs:18-40, 54-60).
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -29,6 +29,9 @@ const char* const kParseErrorNames[] = {
 const char* const kUdpParserLabels[] = {"eth", "l3", "l4"};
 const char* const kGenericUlpLabels[] = {"inner_eth", "inner_l3", "inner_ulp"};
 const char* const kVlanUlpLabels[] = {"eth", "vlan", "l3", "l4"};
+// ingot-examples/src/packets.rs:27-40
+const char* const kGeneveLabels[] = {"outer_eth", "outer_v6",  "outer_udp", "outer_encap",
+                                     "inner_eth", "inner_l3", "inner_ulp"};
 
 int chain_ok(int chain) { return chain >= 0 && chain < INGOT_CHAIN_COUNT; }
 
@@ -142,6 +145,7 @@ int ingot_gpu_parse_strided(ingot_gpu_ctx* ctx, const uint8_t* d_arena, uint32_t
 int ingot_gpu_parse_compact(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
                             const uint16_t* d_len, uint64_t n, int chain, ingot_rec8* d_out,
                             void* stream) {
+    if (chain == INGOT_CHAIN_GENEVE_OVER_V6) return INGOT_GPU_EINVAL;
     return parse_indexed(ctx, d_arena, d_off, d_len, n, chain, d_out, ingot_gpu::OUT_REC8,
                          stream);
 }
@@ -149,6 +153,7 @@ int ingot_gpu_parse_compact(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const ui
 int ingot_gpu_parse_strided_compact(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
                                     uint32_t stride, const uint16_t* d_len, uint64_t n,
                                     int chain, ingot_rec8* d_out, void* stream) {
+    if (chain == INGOT_CHAIN_GENEVE_OVER_V6) return INGOT_GPU_EINVAL;
     return parse_strided(ctx, d_arena, stride, d_len, n, chain, d_out, ingot_gpu::OUT_REC8,
                          stream);
 }
@@ -156,6 +161,18 @@ int ingot_gpu_parse_strided_compact(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
 int ingot_gpu_fields(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
                      const uint16_t* d_len, uint32_t stride, uint64_t n, int chain,
                      ingot_fields* d_out, void* stream) {
+    if (chain == INGOT_CHAIN_GENEVE_OVER_V6) return INGOT_GPU_EINVAL;  // 384-B blocks
+    if (d_off)
+        return parse_indexed(ctx, d_arena, d_off, d_len, n, chain, d_out, ingot_gpu::OUT_FIELDS,
+                             stream);
+    return parse_strided(ctx, d_arena, stride, d_len, n, chain, d_out, ingot_gpu::OUT_FIELDS,
+                         stream);
+}
+
+int ingot_gpu_geneve_fields(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
+                            const uint16_t* d_len, uint32_t stride, uint64_t n,
+                            ingot_geneve_fields* d_out, void* stream) {
+    const int chain = INGOT_CHAIN_GENEVE_OVER_V6;
     if (d_off)
         return parse_indexed(ctx, d_arena, d_off, d_len, n, chain, d_out, ingot_gpu::OUT_FIELDS,
                              stream);
@@ -227,6 +244,7 @@ int ingot_chain_layer_count(int chain) {
     case INGOT_CHAIN_UDP_PARSER: return 3;
     case INGOT_CHAIN_GENERIC_ULP: return 3;
     case INGOT_CHAIN_VLAN_ULP: return 4;
+    case INGOT_CHAIN_GENEVE_OVER_V6: return 7;
     default: return -1;
     }
 }
@@ -236,7 +254,8 @@ const char* ingot_chain_layer_label(int chain, int layer) {
     switch (chain) {
     case INGOT_CHAIN_UDP_PARSER: return kUdpParserLabels[layer];
     case INGOT_CHAIN_GENERIC_ULP: return kGenericUlpLabels[layer];
-    default: return kVlanUlpLabels[layer];
+    case INGOT_CHAIN_VLAN_ULP: return kVlanUlpLabels[layer];
+    default: return kGeneveLabels[layer];
     }
 }
 

@@ -87,6 +87,20 @@ constexpr uint32_t LEN = 8;
 constexpr Field ty{0, 8}, code{8, 8}, checksum{16, 16}, rest_of_hdr{32, 32};
 }  // namespace icmp
 
+// Geneve (ingot/src/geneve.rs:16-44) — 8 B + options (opt_len*4)
+namespace geneve {
+constexpr uint32_t LEN = 8;
+constexpr Field version{0, 2}, opt_len{2, 6}, flags{8, 8}, protocol_type{16, 16}, vni{32, 24},
+    reserved{56, 8};
+constexpr uint32_t FLAGS_KNOWN = 0xc0;  // GeneveFlags bits (geneve.rs:47-53)
+}  // namespace geneve
+
+// GeneveOpt (geneve.rs:80-102) — 4 B + data (length*4)
+namespace geneve_opt {
+constexpr uint32_t LEN = 4;
+constexpr Field opt_class{0, 16}, option_type{16, 8}, reserved{24, 3}, length{27, 5};
+}  // namespace geneve_opt
+
 // Protocol constants (ethernet.rs:12-20, ip.rs:20-38).
 constexpr uint32_t ET_IPV4 = 0x0800, ET_ARP = 0x0806, ET_VLAN = 0x8100, ET_IPV6 = 0x86dd,
                    ET_QINQ = 0x9100;

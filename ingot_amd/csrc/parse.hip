@@ -29,6 +29,8 @@
 // No MFMA: this is integer field extraction bounded by HBM bandwidth.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "../../include/ingot_gpu.h"
 #include "kernels.h"
 #include "layouts.h"
@@ -157,13 +159,66 @@ __device__ __forceinline__ void copy_bytes(const FR& f, uint32_t at, uint8_t* ds
     }
 }
 
+// IPv6 extension headers after the fixed header: `subparse(on_next_layer)`
+// with hint = next_header (mod.rs:1933-1938), i.e. RepeatedView::parse_choice
+// over the rest of the slice (util.rs:199-216): Unwanted (a non-EH class) ends
+// the chain, TooSmall is the header's error.  On return q is past the last EH
+// and h is its next_header.  false = TooSmall.
+template <bool FIELDS, class FR>
+__device__ __forceinline__ bool v6_ext_chain(const FR& f, uint32_t len, uint32_t& q, uint32_t& h,
+                                             uint32_t& n_eh, ingot_v6eh* eh) {
+    while (q < len) {
+        const uint32_t c = eh_class(h);
+        if (c == EH_NONE) break;  // Err(Unwanted) => break
+        uint32_t used, nh, x = 0;
+        if (c == EH_FRAGMENT) {
+            if (len - q < v6frag::LEN) return false;
+            nh = f.be(q, 1);
+            used = v6frag::LEN;
+        } else {
+            if (len - q < v6ext6564::FIXED) return false;
+            x = f.be(q, 2);
+            nh = x >> 8;
+            used = 8u + 8u * (x & 0xffu);  // 2 + (6 + ext_len*8), ip.rs:209
+            if (len - q < used) return false;
+        }
+        if constexpr (FIELDS) {
+            if (n_eh < INGOT_MAX_EH_FIELDS) {
+                ingot_v6eh* e = &eh[n_eh];
+                e->kind = (uint8_t)c;
+                e->off = (uint16_t)q;
+                e->next_header = (uint8_t)nh;
+                if (c == EH_FRAGMENT) {
+                    e->ext_len = (uint8_t)f.get(q, v6frag::reserved);
+                    e->frag_offset = (uint16_t)f.get(q, v6frag::fragment_offset);
+                    e->frag_res_more =
+                        (uint8_t)((f.get(q, v6frag::res) << 1) | f.get(q, v6frag::more_frags));
+                    e->ident = f.get(q, v6frag::ident);
+                } else {
+                    e->ext_len = (uint8_t)(x & 0xffu);
+                    e->frag_offset = 0;
+                    e->frag_res_more = 0;
+                    e->ident = 0;
+                }
+            }
+        }
+        ++n_eh;
+        q += used;
+        h = nh;
+    }
+    return true;
+}
+
 // ---------------------------------------------------------------------------
 // The chain walk: `<Chain>::parse_slice` for one frame.
 // Layer indices are the chain's PacketParseError labels (parse.rs:36-50).
+// F: the (inner) frame's getters; T: the tunnel's outer getters (FIELDS only).
 // ---------------------------------------------------------------------------
 template <int CHAIN, bool FIELDS, class FR>
-__device__ __forceinline__ void walk(const FR& f, Rec& r, ingot_fields* F) {
-    constexpr uint32_t L_L3 = CHAIN == INGOT_CHAIN_VLAN_ULP ? 2u : 1u;
+__device__ __forceinline__ void walk(const FR& f, Rec& r, ingot_fields* F,
+                                     ingot_tunnel_fields* T) {
+    constexpr bool TUN = CHAIN == INGOT_CHAIN_GENEVE_OVER_V6;
+    constexpr uint32_t L_L3 = CHAIN == INGOT_CHAIN_VLAN_ULP ? 2u : TUN ? 5u : 1u;
     constexpr uint32_t L_L4 = L_L3 + 1u;
     constexpr bool ULP = CHAIN != INGOT_CHAIN_UDP_PARSER;  // Ulp vs L4 choice
     const uint32_t len = f.len;
@@ -183,10 +238,160 @@ __device__ __forceinline__ void walk(const FR& f, Rec& r, ingot_fields* F) {
     uint32_t p = eth::LEN;
     r.payload_off = p;
     r.ethertype = et;
-    if constexpr (FIELDS) {
+    if constexpr (FIELDS && TUN) {
+        copy_bytes(f, 0, T->outer_eth_destination, 6);
+        copy_bytes(f, 6, T->outer_eth_source, 6);
+        T->outer_eth_ethertype = (uint16_t)et;
+    } else if constexpr (FIELDS) {
         copy_bytes(f, 0, F->eth_destination, 6);
         copy_bytes(f, 6, F->eth_source, 6);
         F->eth_ethertype = (uint16_t)et;
+    }
+
+    // GeneveOverV6Tunnel's outer layers (ingot-examples/src/packets.rs:27-40).
+    if constexpr (TUN) {
+        // -- layer 1 outer_v6: #[ingot(from = "L3<Q>")] Ipv6 — the L3 choice
+        // parses, then TryFrom keeps only the Ipv6 variant (choice.rs:153-187).
+        if (et == ET_IPV4) {
+            r.l3_kind = INGOT_L3_IPV4;
+            r.l3_off = p;
+            if (len - p < ipv4::LEN) FAIL(1u, INGOT_ERR_TOO_SMALL);
+            const uint32_t ihl = f.get(p, ipv4::ihl);
+            const uint32_t opt = ihl * 4u > 20u ? ihl * 4u - 20u : 0u;
+            if (len - p - ipv4::LEN < opt) FAIL(1u, INGOT_ERR_TOO_SMALL);
+            r.payload_off = p + ipv4::LEN + opt;
+            r.l4_proto = f.get(p, ipv4::protocol);
+            FAIL(1u, INGOT_ERR_UNWANTED);
+        }
+        if (et != ET_IPV6) FAIL(1u, INGOT_ERR_UNWANTED);
+        r.l3_kind = INGOT_L3_IPV6;
+        r.l3_off = p;
+        if (len - p < ipv6::LEN) FAIL(1u, INGOT_ERR_TOO_SMALL);
+        uint32_t h = f.get(p, ipv6::next_header);
+        uint32_t q = p + ipv6::LEN;
+        uint32_t n_eh = 0;
+        const bool eh_ok = v6_ext_chain<false>(f, len, q, h, n_eh, nullptr);
+        r.n_v6ext = n_eh > 255u ? 255u : n_eh;
+        if (!eh_ok) FAIL(1u, INGOT_ERR_TOO_SMALL);
+        if constexpr (FIELDS) {
+            T->outer_v6_version = (uint8_t)f.get(p, ipv6::version);
+            T->outer_v6_dscp = (uint8_t)f.get(p, ipv6::dscp);
+            T->outer_v6_ecn_raw = (uint8_t)f.get(p, ipv6::ecn);
+            T->outer_v6_ecn = ecn_from_network(T->outer_v6_ecn_raw);
+            T->outer_v6_flow_label = f.get(p, ipv6::flow_label);
+            T->outer_v6_payload_len = (uint16_t)f.get(p, ipv6::payload_len);
+            T->outer_v6_next_header = (uint8_t)f.get(p, ipv6::next_header);
+            T->outer_v6_hop_limit = (uint8_t)f.get(p, ipv6::hop_limit);
+            copy_bytes(f, p + ipv6::SOURCE_BYTE, T->outer_v6_source, 16);
+            copy_bytes(f, p + ipv6::DESTINATION_BYTE, T->outer_v6_destination, 16);
+            T->outer_v6_ext_len = (uint16_t)(q - p - ipv6::LEN);
+            T->outer_v6_n_ext = (uint8_t)r.n_v6ext;
+            T->outer_l4_proto = (uint8_t)h;
+        }
+        p = q;
+        r.payload_off = p;
+        r.l4_proto = h;
+
+        // -- layer 2 outer_udp: #[ingot(from = "L4<Q>")] Udp (TCP parses, then
+        // is Unwanted; anything else is Unwanted at the choice).
+        if (h == IPP_TCP) {
+            r.l4_kind = INGOT_L4_TCP;
+            r.l4_off = p;
+            if (len - p < tcp::LEN) FAIL(2u, INGOT_ERR_TOO_SMALL);
+            const uint32_t doff = f.get(p, tcp::data_offset);
+            const uint32_t opt = doff * 4u > 20u ? doff * 4u - 20u : 0u;
+            if (len - p - tcp::LEN < opt) FAIL(2u, INGOT_ERR_TOO_SMALL);
+            r.payload_off = p + tcp::LEN + opt;
+            FAIL(2u, INGOT_ERR_UNWANTED);
+        }
+        if (h != IPP_UDP) FAIL(2u, INGOT_ERR_UNWANTED);
+        r.l4_kind = INGOT_L4_UDP;
+        r.l4_off = p;
+        if (len - p < udp::LEN) FAIL(2u, INGOT_ERR_TOO_SMALL);
+        if constexpr (FIELDS) {
+            T->outer_udp_off = (uint16_t)p;
+            T->outer_udp_source = (uint16_t)f.get(p, udp::source);
+            T->outer_udp_destination = (uint16_t)f.get(p, udp::destination);
+            T->outer_udp_length = (uint16_t)f.get(p, udp::length);
+            T->outer_udp_checksum = (uint16_t)f.get(p, udp::checksum);
+        }
+        p += udp::LEN;
+        r.payload_off = p;
+
+        // -- layer 3 outer_encap: Geneve (geneve.rs:16-44): 8 B, then options
+        // split_at(opt_len*4) subparsed as Repeated<GeneveOpt>
+        // (mod.rs:1940-1957, util.rs:199-216); an option overrunning the span
+        // is TooSmall (GeneveOpt never returns Unwanted).
+        if (len - p < geneve::LEN) FAIL(3u, INGOT_ERR_TOO_SMALL);
+        const uint32_t g0 = f.be(p, 4);  // version | opt_len | flags | protocol_type
+        const uint32_t span = ((g0 >> 24) & 0x3fu) * 4u;
+        if (len - p - geneve::LEN < span) FAIL(3u, INGOT_ERR_TOO_SMALL);
+        uint32_t read = 0, n_opt = 0, crit = 0;
+        bool opt_bad = false;
+        while (read < span) {
+            const uint32_t o = p + geneve::LEN + read, rem = span - read;
+            if (rem < geneve_opt::LEN) { opt_bad = true; break; }
+            const uint32_t ow = f.be(o, 4);
+            const uint32_t data = (ow & 0x1fu) * 4u;
+            if (rem - geneve_opt::LEN < data) { opt_bad = true; break; }
+            if constexpr (FIELDS) {
+                if (n_opt < INGOT_MAX_GENEVE_OPT_FIELDS) {
+                    ingot_geneve_opt* g = &T->geneve_opt[n_opt];
+                    g->opt_class = (uint16_t)(ow >> 16);
+                    g->data_off = (uint16_t)(o + geneve_opt::LEN);
+                    g->option_type = (uint8_t)(ow >> 8);
+                    g->reserved = (uint8_t)((ow >> 5) & 7u);
+                    g->length = (uint8_t)(ow & 0x1fu);
+                }
+            }
+            crit |= (ow >> 15) & 1u;  // GeneveOptionType::is_critical (geneve.rs:72-76)
+            ++n_opt;
+            read += geneve_opt::LEN + data;
+        }
+        if (opt_bad) {
+            if constexpr (FIELDS) {
+                for (uint32_t k = 0; k < INGOT_MAX_GENEVE_OPT_FIELDS; ++k)
+                    T->geneve_opt[k] = ingot_geneve_opt{};
+            }
+            FAIL(3u, INGOT_ERR_TOO_SMALL);
+        }
+        if constexpr (FIELDS) {
+            const uint32_t g1 = f.be(p + 4u, 4);  // vni | reserved
+            T->geneve_off = (uint16_t)p;
+            T->geneve_version = (uint8_t)(g0 >> 30);
+            T->geneve_opt_len = (uint8_t)((g0 >> 24) & 0x3fu);
+            T->geneve_flags = (uint8_t)((g0 >> 16) & geneve::FLAGS_KNOWN);  // from_bits_truncate
+            T->geneve_protocol_type = (uint16_t)g0;
+            T->geneve_vni = g1 >> 8;
+            T->geneve_reserved = (uint8_t)g1;
+            T->geneve_n_opts = (uint8_t)(n_opt > 255u ? 255u : n_opt);
+            T->geneve_critical = (uint8_t)crit;
+        }
+        p += geneve::LEN + span;
+        r.payload_off = p;
+
+        // -- layer 4 inner_eth; from here the record describes the inner frame.
+        if (len - p < eth::LEN) FAIL(4u, INGOT_ERR_TOO_SMALL);
+        et = f.get(p, eth::ethertype);
+        if constexpr (FIELDS) {
+            T->inner_eth_off = (uint16_t)p;
+            copy_bytes(f, p, F->eth_destination, 6);
+            copy_bytes(f, p + 6u, F->eth_source, 6);
+            F->eth_ethertype = (uint16_t)et;
+        }
+        r.flags = INGOT_REC_INNER;
+        r.l3_kind = r.l4_kind = INGOT_L3_NONE;
+        r.l3_off = r.l4_off = 0;
+        r.n_v6ext = 0;
+        r.l4_proto = 0;
+        r.ethertype = et;
+        p += eth::LEN;
+        r.payload_off = p;
+        // control = exit_on_arp; the Option<> sled allows Accept here.
+        if (et == ET_ARP) {
+            r.flags |= INGOT_REC_ACCEPTED;
+            return;
+        }
     }
 
     // GenericUlp: control = exit_on_arp on inner_eth (packets.rs:45-51); the
@@ -249,53 +454,12 @@ __device__ __forceinline__ void walk(const FR& f, Rec& r, ingot_fields* F) {
         r.l3_kind = INGOT_L3_IPV6;
         r.l3_off = p;
         if (len - p < ipv6::LEN) FAIL(L_L3, INGOT_ERR_TOO_SMALL);
-        // subparse(on_next_layer): hint = next_header (mod.rs:1933-1938), then
-        // RepeatedView::parse_choice over the rest of the slice (util.rs:206-216).
         uint32_t h = f.get(p, ipv6::next_header);
         uint32_t q = p + ipv6::LEN;
         uint32_t n_eh = 0;
-        bool bad = false;
-        while (q < len) {
-            const uint32_t c = eh_class(h);
-            if (c == EH_NONE) break;  // Err(Unwanted) => break
-            uint32_t used, nh, x = 0;
-            if (c == EH_FRAGMENT) {
-                if (len - q < v6frag::LEN) { bad = true; break; }
-                nh = f.be(q, 1);
-                used = v6frag::LEN;
-            } else {
-                if (len - q < v6ext6564::FIXED) { bad = true; break; }
-                x = f.be(q, 2);
-                nh = x >> 8;
-                used = 8u + 8u * (x & 0xffu);  // 2 + (6 + ext_len*8), ip.rs:209
-                if (len - q < used) { bad = true; break; }
-            }
-            if constexpr (FIELDS) {
-                if (n_eh < INGOT_MAX_EH_FIELDS) {
-                    ingot_v6eh* e = &F->v6_eh[n_eh];
-                    e->kind = (uint8_t)c;
-                    e->off = (uint16_t)q;
-                    e->next_header = (uint8_t)nh;
-                    if (c == EH_FRAGMENT) {
-                        e->ext_len = (uint8_t)f.get(q, v6frag::reserved);
-                        e->frag_offset = (uint16_t)f.get(q, v6frag::fragment_offset);
-                        e->frag_res_more = (uint8_t)((f.get(q, v6frag::res) << 1) |
-                                                     f.get(q, v6frag::more_frags));
-                        e->ident = f.get(q, v6frag::ident);
-                    } else {
-                        e->ext_len = (uint8_t)(x & 0xffu);
-                        e->frag_offset = 0;
-                        e->frag_res_more = 0;
-                        e->ident = 0;
-                    }
-                }
-            }
-            ++n_eh;
-            q += used;
-            h = nh;
-        }
+        const bool eh_ok = v6_ext_chain<FIELDS>(f, len, q, h, n_eh, FIELDS ? F->v6_eh : nullptr);
         r.n_v6ext = n_eh > 255u ? 255u : n_eh;
-        if (bad) {
+        if (!eh_ok) {
             if constexpr (FIELDS) {
                 for (uint32_t k = 0; k < INGOT_MAX_EH_FIELDS; ++k) F->v6_eh[k] = ingot_v6eh{};
             }
@@ -440,6 +604,7 @@ __device__ __forceinline__ bool flow_hash(const FR& f, const Rec& r, const uint3
 template <uint32_t NCH, int LAYOUT, int CHAIN, int MODE, class ARGS>
 __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
     const ParseArgs& a = base_args(args);
+    constexpr bool TUN = CHAIN == INGOT_CHAIN_GENEVE_OVER_V6;
     constexpr uint32_t WIN = NCH * 16u;
     constexpr uint32_t WAVE_DW = WAVE * NCH * 4u;  // dwords per wave image
     // +16 dwords: the second dword of a pair read may run past the last image.
@@ -500,19 +665,29 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
         Frame<NCH> fr{(const lds_u32*)wimg, lane, sh, take, len, a.arena + off};
         Rec r;
         if constexpr (MODE == OUT_FIELDS) {
-            ingot_fields* F = static_cast<ingot_fields*>(a.out) + (valid ? i : 0);
+            // ingot_fields, or ingot_geneve_fields (inner + outer) for the tunnel.
+            using OutT = typename std::conditional<TUN, ingot_geneve_fields, ingot_fields>::type;
+            OutT* G = static_cast<OutT*>(a.out) + (valid ? i : 0);
             if (valid) {
-                uint4* z = reinterpret_cast<uint4*>(F);
+                uint4* z = reinterpret_cast<uint4*>(G);
 #pragma unroll
-                for (int k = 0; k < 16; ++k) z[k] = make_uint4(0, 0, 0, 0);
-                walk<CHAIN, true>(fr, r, F);
+                for (int k = 0; k < (int)(sizeof(OutT) / 16); ++k) z[k] = make_uint4(0, 0, 0, 0);
+                ingot_fields* F;
+                ingot_tunnel_fields* T = nullptr;
+                if constexpr (TUN) {
+                    F = &G->inner;
+                    T = &G->outer;
+                } else {
+                    F = G;
+                }
+                walk<CHAIN, true>(fr, r, F, T);
                 reinterpret_cast<uint4*>(F)[0] = pack(r);
             }
         } else if constexpr (MODE == OUT_REC8) {
-            walk<CHAIN, false>(fr, r, nullptr);
+            walk<CHAIN, false>(fr, r, nullptr, nullptr);
             if (valid) static_cast<uint2*>(a.out)[i] = pack8(r);
         } else if constexpr (MODE == OUT_FLOWS) {
-            walk<CHAIN, false>(fr, r, nullptr);
+            walk<CHAIN, false>(fr, r, nullptr, nullptr);
             uint32_t h;
             const bool counted = valid && flow_hash(fr, r, s_tab, h);
             if (valid) {
@@ -520,7 +695,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
                 if (args.hash) args.hash[i] = h;
             }
         } else {
-            walk<CHAIN, false>(fr, r, nullptr);
+            walk<CHAIN, false>(fr, r, nullptr, nullptr);
             if (valid) static_cast<uint4*>(a.out)[i] = pack(r);
         }
         // The next tile's LDS-DMA overwrites this image: every lane's reads
@@ -539,9 +714,17 @@ hipError_t launch_chain(const ARGS& a, int chain, uint32_t grid, hipStream_t s) 
         hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_GENERIC_ULP, MODE, ARGS>),
                            dim3(grid), dim3(BLOCK), 0, s, a);
         break;
-    default:
+    case INGOT_CHAIN_VLAN_ULP:
         hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_VLAN_ULP, MODE, ARGS>), dim3(grid),
                            dim3(BLOCK), 0, s, a);
+        break;
+    default:
+        if constexpr (MODE == OUT_REC8) {
+            return hipErrorInvalidValue;  // not offered for the tunnel (api.cpp)
+        } else {
+            hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_GENEVE_OVER_V6, MODE, ARGS>),
+                               dim3(grid), dim3(BLOCK), 0, s, a);
+        }
         break;
     }
     return hipGetLastError();
@@ -581,8 +764,11 @@ hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, int mode
     //    whole 64-B slot (4 chunks; C2 is flat from 2 to 4 chunks).
     // Small windows win: they fetch only the header lines and keep LDS per
     // wave low; the rest of a long chain is read from L2/HBM on demand.
+    // The tunnel's inner headers start ~88 B in: stage 8 chunks (128 B).
+    const bool tun = chain == INGOT_CHAIN_GENEVE_OVER_V6;
     if (layout_kind == LAYOUT_STRIDED) {
-        const int w = t.window_strided ? t.window_strided : (a.stride <= 64u ? 4 : 3);
+        const int w = t.window_strided ? t.window_strided
+                                       : tun ? 8 : (a.stride <= 64u ? 4 : 3);
         if (w == 100) return launch_mode<0, LAYOUT_STRIDED>(a, chain, mode, g, s);
         if (w == 2) return launch_mode<2, LAYOUT_STRIDED>(a, chain, mode, g, s);
         if (w == 3) return launch_mode<3, LAYOUT_STRIDED>(a, chain, mode, g, s);
@@ -590,7 +776,7 @@ hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, int mode
         if (w == 5) return launch_mode<5, LAYOUT_STRIDED>(a, chain, mode, g, s);
         return launch_mode<8, LAYOUT_STRIDED>(a, chain, mode, g, s);
     }
-    switch (t.window_indexed ? t.window_indexed : 3) {
+    switch (t.window_indexed ? t.window_indexed : tun ? 8 : 3) {
     case 100: return launch_mode<0, LAYOUT_INDEXED>(a, chain, mode, g, s);
     case 2: return launch_mode<2, LAYOUT_INDEXED>(a, chain, mode, g, s);
     case 3: return launch_mode<3, LAYOUT_INDEXED>(a, chain, mode, g, s);

@@ -14,7 +14,7 @@ from pathlib import Path
 
 import numpy as np
 
-from ingot_amd.abi import FIELDS_DTYPE, REC_DTYPE, Chain  # ABI layouts only
+from ingot_amd.abi import FIELDS_DTYPE, GENEVE_FIELDS_DTYPE, REC_DTYPE, Chain  # ABI layouts only
 
 HERE = Path(__file__).resolve().parent
 LIB_PATH = HERE / "build" / "libingot_oracle.so"
@@ -57,6 +57,10 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     lib.oracle_v6eh_class.restype = ctypes.c_int
     lib.oracle_toeplitz.argtypes = [vp, ctypes.c_uint32, vp, ctypes.c_uint32]
     lib.oracle_toeplitz.restype = ctypes.c_uint32
+    lib.oracle_parse_geneve.argtypes = [vp, ctypes.c_uint32, vp]
+    lib.oracle_parse_geneve.restype = None
+    lib.oracle_geneve_fields_batch.argtypes = [vp, vp, vp, ctypes.c_uint32, ctypes.c_uint64, vp]
+    lib.oracle_geneve_fields_batch.restype = ctypes.c_int
     if path is None:
         _lib = lib
     return lib
@@ -95,6 +99,33 @@ def parse_batch(arena: np.ndarray, off: np.ndarray | None, lens: np.ndarray | No
     if rc != 0:
         raise ValueError("oracle_parse_batch: bad arguments")
     return (rec, fld) if fields else rec
+
+
+def parse_geneve(frame: bytes):
+    """GeneveOverV6Tunnel -> ingot_geneve_fields (numpy structured scalar;
+    ["inner"]["rec"] is the record)."""
+    lib = load()
+    buf = np.frombuffer(bytes(frame) + b"\0" * 8, dtype=np.uint8).copy()
+    out = np.zeros(1, dtype=GENEVE_FIELDS_DTYPE)
+    lib.oracle_parse_geneve(_p(buf), len(frame), _p(out))
+    return out[0]
+
+
+def geneve_fields_batch(arena: np.ndarray, off: np.ndarray | None, lens: np.ndarray | None,
+                        stride: int = 0, n: int | None = None, lib: ctypes.CDLL | None = None):
+    lib = lib or load()
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    if off is not None:
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        n = len(off) if n is None else n
+    if lens is not None:
+        lens = np.ascontiguousarray(lens, dtype=np.uint16)
+    if n is None:
+        raise ValueError("n is required for the strided layout")
+    out = np.zeros(n, dtype=GENEVE_FIELDS_DTYPE)
+    if lib.oracle_geneve_fields_batch(_p(arena), _p(off), _p(lens), stride, n, _p(out)) != 0:
+        raise ValueError("oracle_geneve_fields_batch: bad arguments")
+    return out
 
 
 def be_bits(hdr: bytes, first_bit: int, n_bits: int) -> int:
@@ -146,7 +177,7 @@ def flow_hist(arena, off, lens, chain: Chain, stride: int = 0, n: int | None = N
 
 
 HEADER_KINDS = {"ethernet": 0, "vlan": 1, "ipv4": 2, "ipv6": 3, "tcp": 4, "udp": 5, "icmp": 6,
-                "repeated_udp": 7}
+                "repeated_udp": 7, "geneve": 8}
 
 
 def parse_header(kind: str, data: bytes):

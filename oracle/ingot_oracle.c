@@ -91,6 +91,16 @@ enum {
 /* Udp (udp.rs:8-15), IcmpV4/IcmpV6 (icmp.rs:42-50, 114-122) */
 #define UDP_LEN 8u
 #define ICMP_LEN 8u
+/* Geneve (geneve.rs:16-44): version u2, opt_len u6, flags u8,
+ * protocol_type u16be, vni [u8;3], reserved u8, options var_len */
+#define GENEVE_LEN 8u
+#define GENEVE_VERSION 0, 2
+#define GENEVE_OPT_LEN_F 2, 6
+/* GeneveOpt (geneve.rs:80-102): class u16be, option_type u8, reserved u3,
+ * length u5, data var_len */
+#define GENEVE_OPT_LEN 4u
+#define GOPT_RESERVED 24, 3
+#define GOPT_LENGTH 27, 5
 
 uint64_t oracle_be_bits(const uint8_t* hdr, uint32_t first_bit, uint32_t n_bits) {
     /* bitfield.rs:40-186: the covering bytes, read as a big-endian integer,
@@ -424,11 +434,144 @@ static int layer_eth(walk_t* w, uint32_t* et) {
     return PE_OK;
 }
 
-void oracle_parse_one(const uint8_t* frame, uint32_t len, int chain, ingot_rec* rec,
-                      ingot_fields* fields) {
+/* Geneve (geneve.rs:16-44) as its generated parse_choice (mod.rs:1846-1957):
+ * the 8-B fixed chunk (Accessor, else TooSmall), then `options`:
+ * var_len = opt_len*4 cut with split_at (else TooSmall) and subparsed as
+ * Repeated<GeneveOpt> with no hint = RepeatedView::parse_choice
+ * (util.rs:199-216) over exactly that span.  GeneveOpt (geneve.rs:80-102) is a
+ * 4-B chunk + data var_len length*4; it never returns Unwanted, so an option
+ * that overruns the span is TooSmall for the whole header. */
+static int parse_geneve(const uint8_t* s, uint32_t n, uint32_t frame_off, uint32_t* used,
+                        ingot_tunnel_fields* T) {
+    if (n < GENEVE_LEN) return PE_TOO_SMALL;
+    uint32_t span = (s[0] & 0x3fu) * 4u;
+    if (n - GENEVE_LEN < span) return PE_TOO_SMALL;
+    uint32_t read = 0, n_opt = 0, crit = 0;
+    while (read < span) {
+        const uint8_t* o = s + GENEVE_LEN + read;
+        uint32_t rem = span - read;
+        if (rem < GENEVE_OPT_LEN) goto small;
+        uint32_t data = BITS(o, GOPT_LENGTH) * 4u;
+        if (rem - GENEVE_OPT_LEN < data) goto small;
+        if (T && n_opt < INGOT_MAX_GENEVE_OPT_FIELDS) {
+            ingot_geneve_opt* g = &T->geneve_opt[n_opt];
+            g->opt_class = (uint16_t)be16(o);
+            g->option_type = o[2];
+            g->reserved = (uint8_t)BITS(o, GOPT_RESERVED);
+            g->length = (uint8_t)BITS(o, GOPT_LENGTH);
+            g->data_off = (uint16_t)(frame_off + GENEVE_LEN + read + GENEVE_OPT_LEN);
+        }
+        if (o[2] & 0x80u) crit = 1; /* GeneveOptionType::is_critical, geneve.rs:72-76 */
+        n_opt++;
+        read += GENEVE_OPT_LEN + data;
+    }
+    *used = GENEVE_LEN + span;
+    if (T) {
+        T->geneve_version = (uint8_t)BITS(s, GENEVE_VERSION);
+        T->geneve_opt_len = (uint8_t)BITS(s, GENEVE_OPT_LEN_F);
+        T->geneve_flags = (uint8_t)(s[1] & 0xc0u); /* GeneveFlags::from_bits_truncate */
+        T->geneve_protocol_type = (uint16_t)be16(s + 2);
+        T->geneve_vni = ((uint32_t)s[4] << 16) | ((uint32_t)s[5] << 8) | s[6];
+        T->geneve_reserved = s[7];
+        T->geneve_n_opts = (uint8_t)(n_opt > 255 ? 255 : n_opt);
+        T->geneve_critical = (uint8_t)crit;
+    }
+    return PE_OK;
+small:
+    if (T) memset(T->geneve_opt, 0, sizeof T->geneve_opt);
+    return PE_TOO_SMALL;
+}
+
+/* GeneveOverV6Tunnel (ingot-examples/src/packets.rs:27-40) after outer_eth:
+ *   outer_v6:    #[ingot(from = "L3<Q>")] Ipv6 — the L3 choice parses, then
+ *                TryFrom<ValidL3> keeps only the Ipv6 variant (choice.rs:153-187);
+ *   outer_udp:   #[ingot(from = "L4<Q>")] Udp, likewise;
+ *   outer_encap: Geneve (parse, no hint needed);
+ *   inner_eth:   control = exit_on_arp (packets.rs:45-51); the Option<> sled
+ *                after it allows Accept there (parse.rs:144-156, 221-254);
+ *   inner_l3: Option<L3>, inner_ulp: Option<Ulp>. */
+static void geneve_chain(walk_t* w, uint32_t et, ingot_fields* inner, ingot_tunnel_fields* T) {
+    ingot_rec* r = w->r;
+    const uint8_t* f = w->f;
+    uint32_t proto = 0, used = 0, iet = 0;
+    int e;
+    if (T) {
+        memcpy(T->outer_eth_destination, f, 6);
+        memcpy(T->outer_eth_source, f + 6, 6);
+        T->outer_eth_ethertype = (uint16_t)et;
+    }
+    if (layer_l3(w, 1, et, &proto) != PE_OK) return;
+    if (r->l3_kind != INGOT_L3_IPV6) {
+        fail(w, 1, PE_UNWANTED);
+        return;
+    }
+    if (T) {
+        const uint8_t* s = f + r->l3_off;
+        T->outer_v6_version = (uint8_t)BITS(s, V6_VERSION);
+        T->outer_v6_dscp = (uint8_t)BITS(s, V6_DSCP);
+        T->outer_v6_ecn_raw = (uint8_t)BITS(s, V6_ECN);
+        T->outer_v6_ecn = ecn_from_network(T->outer_v6_ecn_raw);
+        T->outer_v6_flow_label = BITS(s, V6_FLOW);
+        T->outer_v6_payload_len = (uint16_t)BITS(s, V6_PAYLOAD_LEN);
+        T->outer_v6_next_header = s[6];
+        T->outer_v6_hop_limit = s[7];
+        memcpy(T->outer_v6_source, s + 8, 16);
+        memcpy(T->outer_v6_destination, s + 24, 16);
+        T->outer_v6_ext_len = (uint16_t)(w->p - r->l3_off - V6_LEN);
+        T->outer_v6_n_ext = r->n_v6ext;
+        T->outer_l4_proto = (uint8_t)proto;
+    }
+    if (layer_l4(w, 2, proto, 0, 1) != PE_OK) return;
+    if (T) {
+        const uint8_t* s = f + r->l4_off;
+        T->outer_udp_off = r->l4_off;
+        T->outer_udp_source = (uint16_t)be16(s);
+        T->outer_udp_destination = (uint16_t)be16(s + 2);
+        T->outer_udp_length = (uint16_t)be16(s + 4);
+        T->outer_udp_checksum = (uint16_t)be16(s + 6);
+    }
+    e = parse_geneve(f + w->p, w->len - w->p, w->p, &used, T);
+    if (e != PE_OK) {
+        fail(w, 3, e);
+        return;
+    }
+    if (T) T->geneve_off = (uint16_t)w->p;
+    w->p += used;
+    r->payload_off = (uint16_t)w->p;
+
+    e = parse_eth(f + w->p, w->len - w->p, &used, &iet);
+    if (e != PE_OK) {
+        fail(w, 4, e);
+        return;
+    }
+    /* the record now describes the inner frame */
+    r->flags |= INGOT_REC_INNER;
+    r->l3_kind = r->l4_kind = 0;
+    r->l3_off = r->l4_off = 0;
+    r->n_v6ext = 0;
+    r->l4_proto = 0;
+    r->ethertype = (uint16_t)iet;
+    if (T) T->inner_eth_off = (uint16_t)w->p;
+    w->F = inner;
+    if (inner) fields_eth(inner, f + w->p);
+    w->p += used;
+    r->payload_off = (uint16_t)w->p;
+    if (iet == ET_ARP) {
+        r->flags |= INGOT_REC_ACCEPTED;
+        return;
+    }
+    if (layer_l3(w, 5, iet, &proto) != PE_OK) return;
+    layer_l4(w, 6, proto, 1, 0);
+}
+
+static void parse_one(const uint8_t* frame, uint32_t len, int chain, ingot_rec* rec,
+                      ingot_fields* fields, ingot_tunnel_fields* tunnel) {
     memset(rec, 0, sizeof *rec);
     if (fields) memset(fields, 0, sizeof *fields);
-    walk_t w = {frame, len, 0, rec, fields};
+    if (tunnel) memset(tunnel, 0, sizeof *tunnel);
+    const int tun = chain == INGOT_CHAIN_GENEVE_OVER_V6;
+    /* the tunnel's outer layers have no ingot_fields slots */
+    walk_t w = {frame, len, 0, rec, tun ? 0 : fields};
     uint32_t et = 0, proto = 0;
     rec->err_layer = 0xff;
 
@@ -472,6 +615,9 @@ void oracle_parse_one(const uint8_t* frame, uint32_t len, int chain, ingot_rec* 
         if (layer_l3(&w, 2, et, &proto) != PE_OK) goto out;
         layer_l4(&w, 3, proto, 1, 0);
         break;
+    case INGOT_CHAIN_GENEVE_OVER_V6:
+        geneve_chain(&w, et, fields, tunnel);
+        break;
     default:
         fail(&w, 0, PE_UNWANTED);
         break;
@@ -479,6 +625,28 @@ void oracle_parse_one(const uint8_t* frame, uint32_t len, int chain, ingot_rec* 
 out:
     if (rec->status == PE_OK) rec->err_layer = 0xff;
     if (fields) fields->rec = *rec;
+}
+
+void oracle_parse_one(const uint8_t* frame, uint32_t len, int chain, ingot_rec* rec,
+                      ingot_fields* fields) {
+    parse_one(frame, len, chain, rec, fields, 0);
+}
+
+void oracle_parse_geneve(const uint8_t* frame, uint32_t len, ingot_geneve_fields* out) {
+    parse_one(frame, len, INGOT_CHAIN_GENEVE_OVER_V6, &out->inner.rec, &out->inner,
+              &out->outer);
+}
+
+int oracle_geneve_fields_batch(const uint8_t* arena, const uint64_t* off, const uint16_t* len,
+                               uint32_t stride, uint64_t n, ingot_geneve_fields* out) {
+    if ((!arena && n) || (!out && n) || (!off && stride == 0 && n)) return -1;
+    for (uint64_t i = 0; i < n; ++i) {
+        uint64_t o = off ? off[i] : i * (uint64_t)stride;
+        uint32_t l = len ? len[i] : stride;
+        if (!off && l > stride) l = stride;
+        oracle_parse_geneve(arena + o, l, &out[i]);
+    }
+    return 0;
 }
 
 /* ------------------------------------------------------------------------
@@ -566,7 +734,7 @@ uint32_t oracle_toeplitz(const uint8_t* key, uint32_t key_len, const uint8_t* da
  * Header-level entry (single `ValidX::parse`), for the reference's
  * header-level known-answer tests.  kind: 0 Ethernet, 1 VlanBody, 2 Ipv4,
  * 3 Ipv6, 4 Tcp, 5 Udp, 6 IcmpV4/V6, 7 RepeatedView<Udp> (util.rs:189-228
- * over a fixed 8-B header with a unit hint).  Returns the status; *used and
+ * over a fixed 8-B header with a unit hint), 8 Geneve.  Returns the status; *used and
  * *hint_out (0xffffffff = None) on Ok.
  * ---------------------------------------------------------------------- */
 int oracle_parse_header(int kind, const uint8_t* s, uint32_t n, uint32_t* used,
@@ -594,6 +762,7 @@ int oracle_parse_header(int kind, const uint8_t* s, uint32_t n, uint32_t* used,
         u = read;
         break;
     }
+    case 8: e = parse_geneve(s, n, 0, &u, 0); break;
     default: return PE_UNWANTED;
     }
     if (e == PE_OK) {

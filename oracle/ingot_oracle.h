@@ -28,6 +28,13 @@ extern "C" {
 void oracle_parse_one(const uint8_t* frame, uint32_t len, int chain,
                       ingot_rec* rec, ingot_fields* fields);
 
+/* GeneveOverV6Tunnel with the outer layers' getters (inner.rec is the record);
+ * batch form single-threaded (layouts as oracle_parse_batch). */
+void oracle_parse_geneve(const uint8_t* frame, uint32_t len, ingot_geneve_fields* out);
+int oracle_geneve_fields_batch(const uint8_t* arena, const uint64_t* off,
+                               const uint16_t* len, uint32_t stride, uint64_t n,
+                               ingot_geneve_fields* out);
+
 /* Batch form.  off == NULL selects the strided layout (frame i at i*stride);
  * len == NULL means every frame is `stride` bytes long.  fields may be NULL.
  * nthreads <= 1 runs on the calling thread; otherwise a static contiguous

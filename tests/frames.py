@@ -55,3 +55,23 @@ def pack(frames):
     arena = np.frombuffer(b"".join(frames) + bytes(64), dtype=np.uint8).copy()
     return (arena, np.array(off, dtype=np.uint64),
             np.array([len(f) for f in frames], dtype=np.uint16))
+
+
+def geneve_outer(rng, opts=((0x0129, 0, b""),), hbh: bool = False, vni: int | None = None,
+                 flags: int = 0) -> bytes:
+    """Outer Ethernet / IPv6 (optional 8-B hop-by-hop EH) / UDP 6081 / Geneve
+    with `opts` = ((class, type, data), ...) as in RFC 8926 / geneve.rs:16-102."""
+    optb = b""
+    for cls, ty, data in opts:
+        assert len(data) % 4 == 0
+        optb += _u16(cls) + bytes([ty, len(data) // 4]) + data
+    vni = int(rng.integers(0, 1 << 24)) if vni is None else vni
+    gen = bytes([len(optb) // 4, flags]) + _u16(0x6558) + vni.to_bytes(3, "big") + b"\0" + optb
+    udp = _u16(int(rng.integers(49152, 65536))) + _u16(6081) + _u16(8 + len(gen)) + _u16(0)
+    ehb = bytes([17, 0]) + bytes(6) if hbh else b""
+    v6 = (bytes([0x60, 0, 0, 0]) + _u16(len(ehb) + len(udp) + len(gen)) +
+          bytes([0 if hbh else 17, 255]) + bytes([0xFD]) +
+          rng.integers(0, 256, 15, dtype=np.uint8).tobytes() + bytes([0xFD]) +
+          rng.integers(0, 256, 15, dtype=np.uint8).tobytes())
+    eth = rng.integers(0, 256, 12, dtype=np.uint8).tobytes() + _u16(0x86DD)
+    return eth + v6 + ehb + udp + gen

@@ -280,6 +280,108 @@ def chain_frames():
     return out
 
 
+def geneve_frames():
+    """GeneveOverV6Tunnel (ingot-examples/src/packets.rs:27-40) vectors."""
+    out = []
+    chain = "GeneveOverV6Tunnel"
+    outer_eth, outer_v6 = OPTE_IN[:14], OPTE_IN[14:54]
+    outer_udp, geneve = OPTE_IN[54:62], OPTE_IN[62:74]
+    inner = OPTE_IN[74:]
+    # ingot-examples/src/tests.rs:189-268 test_tunnelled_unconditionals (the
+    # same bytes are ingot-examples/benches/packet.rs:59-128 opte_in_pkt, which
+    # the bench parses with unwrap(), :159-164).
+    out.append(dict(
+        name="test_tunnelled_unconditionals", source="ingot-examples/src/tests.rs:189-268",
+        chain=chain, frame=hexs(OPTE_IN),
+        expect=dict(ok=True, l3="ipv4", l4="udp", inner=True, remainder=8,
+                    fields=dict(eth_ethertype=0x0800),
+                    outer_fields=dict(geneve_opt_len=1, geneve_n_opts=1,
+                                      **{"geneve_opt[0].opt_class": 0x0129}),
+                    note="options_ref().packet_length() == 4 -> opt_len 1; "
+                         "remainder 8 by construction (the inner body)")))
+    # ingot-examples/src/tests.rs:270-274: inner ethertype set to ARP ->
+    # exit_on_arp accepts; inner_l3 / inner_ulp are None.
+    arp = list(OPTE_IN)
+    arp[74 + 12:74 + 14] = [0x08, 0x06]
+    out.append(dict(
+        name="test_tunnelled_unconditionals_arp", source="ingot-examples/src/tests.rs:270-274",
+        chain=chain, frame=hexs(arp),
+        expect=dict(ok=True, accepted=True, inner=True, l3="none", l4="none",
+                    remainder=len(OPTE_IN) - 88, fields=dict(eth_ethertype=0x0806))))
+    # ingot/src/tests.rs:384-419 to_owned: the Geneve getters of g_opt (the same
+    # header bytes as the tunnel above).
+    out.append(dict(
+        name="to_owned_geneve_in_tunnel", source="ingot/src/tests.rs:384-419",
+        chain=chain, frame=hexs(OPTE_IN), derived="the test's g_opt is this frame's outer_encap",
+        expect=dict(ok=True, outer_fields={
+            "geneve_version": 0, "geneve_opt_len": 1, "geneve_flags": 0,
+            "geneve_protocol_type": 0x6558, "geneve_vni": 0x0004D2, "geneve_reserved": 0,
+            "geneve_opt[0].opt_class": 0x0129, "geneve_opt[0].option_type": 0,
+            "geneve_opt[0].reserved": 0, "geneve_opt[0].length": 0})))
+    # ingot/src/tests.rs:167-221 varlen_geneve: option type 0x47.
+    g47 = [0x01, 0x00, 0x65, 0x58, 0x00, 0x04, 0xD2, 0x00, 0x01, 0x29, 0x47, 0x00]
+    f = outer_eth + outer_v6 + outer_udp + g47 + inner
+    out.append(dict(
+        name="varlen_geneve_in_tunnel", source="ingot/src/tests.rs:167-221", chain=chain,
+        frame=hexs(f), derived="the test's g_opt as this tunnel's outer_encap",
+        expect=dict(ok=True, l3="ipv4", l4="udp", outer_fields={
+            "geneve_n_opts": 1, "geneve_opt[0].opt_class": 0x0129,
+            "geneve_opt[0].option_type": 0x47, "geneve_opt[0].reserved": 0,
+            "geneve_opt[0].length": 0})))
+    # ingot/src/tests.rs:503-527 easy_tuple_emit: (Udp{1234,5678,77,0xffff},
+    # Geneve{flags CRITICAL_OPTS, ETHERNET, vni 7777}) emitted, i.e. the
+    # layout's bytes; as outer_udp + outer_encap of a tunnel.
+    udp_g = u16(1234) + u16(5678) + u16(77) + u16(0xFFFF) + [0x00, 0x40, 0x65, 0x58,
+                                                             0x00, 0x1E, 0x61, 0x00]
+    f = outer_eth + outer_v6 + udp_g + inner
+    out.append(dict(
+        name="easy_tuple_emit_in_tunnel", source="ingot/src/tests.rs:503-527", chain=chain,
+        frame=hexs(f), derived="emitted bytes restated from the layout (geneve.rs:16-44)",
+        expect=dict(ok=True, l3="ipv4", l4="udp", outer_fields={
+            "outer_udp_source": 1234, "outer_udp_destination": 5678, "outer_udp_length": 77,
+            "outer_udp_checksum": 0xFFFF, "geneve_version": 0, "geneve_opt_len": 0,
+            "geneve_flags": 0x40, "geneve_protocol_type": 0x6558, "geneve_vni": 7777,
+            "geneve_reserved": 0, "geneve_n_opts": 0})))
+    # Derived from the layer rules on the reference frame: each truncation is
+    # TooSmall at the layer whose Accessor / split_at fails (accessor.rs:30-67,
+    # mod.rs:1867-1875); the from= conversions reject the other variants
+    # (choice.rs:153-187, parse.rs:196-200).
+    cuts = [(10, "outer_eth"), (14 + 39, "outer_v6"), (54 + 7, "outer_udp"),
+            (62 + 7, "outer_encap"), (62 + 11, "outer_encap"), (74 + 13, "inner_eth"),
+            (88 + 19, "inner_l3"), (108 + 7, "inner_ulp")]
+    for cut, label in cuts:
+        out.append(dict(
+            name=f"tunnel_truncated_{cut}", source="ingot-examples/src/tests.rs:189-268",
+            chain=chain, frame=hexs(OPTE_IN[:cut]), derived=f"reference frame cut to {cut} B",
+            expect=dict(ok=False, error="TooSmall", label=label)))
+    f = list(OPTE_IN)
+    f[12:14] = [0x08, 0x00]
+    out.append(dict(
+        name="tunnel_outer_ipv4_unwanted", source="ingot-examples/src/packets.rs:31-32",
+        chain=chain, frame=hexs(f), derived="outer ethertype IPv4: L3 parses, from= rejects",
+        expect=dict(ok=False, error="Unwanted", label="outer_v6", l3="ipv4")))
+    f = list(OPTE_IN)
+    f[20] = 6
+    out.append(dict(
+        name="tunnel_outer_tcp_unwanted", source="ingot-examples/src/packets.rs:33-34",
+        chain=chain, frame=hexs(f), derived="outer next_header TCP: L4 parses, from= rejects",
+        expect=dict(ok=False, error="Unwanted", label="outer_udp", l4="tcp")))
+    f = list(OPTE_IN)
+    f[62] = 0x02  # opt_len 2: 8 option bytes claimed, only the inner frame follows
+    f[62 + 11] = 0x02  # the option claims 8 data bytes inside a 4-byte span
+    out.append(dict(
+        name="tunnel_option_overruns_span", source="ingot-types/src/util.rs:206-216",
+        chain=chain, frame=hexs(f), derived="GeneveOpt data overrunning the options span",
+        expect=dict(ok=False, error="TooSmall", label="outer_encap")))
+    f = list(OPTE_IN)
+    f[63] = 0xFF
+    out.append(dict(
+        name="tunnel_geneve_flags_truncate", source="ingot/src/geneve.rs:47-63",
+        chain=chain, frame=hexs(f), derived="GeneveFlags::from_bits_truncate keeps 0xC0",
+        expect=dict(ok=True, outer_fields={"geneve_flags": 0xC0})))
+    return out
+
+
 def header_kats():
     """Header-level vectors: (header kind, bytes, hint) -> (status, used, hint)."""
     zero54 = [0] * 54
@@ -307,6 +409,16 @@ def header_kats():
              expect=dict(ok=True, used=36, hint=17)),
         dict(name="ipv4_no_opt_bench", source="ingot/benches/modify.rs:57-65", header="ipv4",
              bytes=hexs(INNER_V4), expect=dict(ok=True, used=20, hint=17)),
+        dict(name="varlen_geneve_no_opt", source="ingot/src/tests.rs:169-180, 202-203",
+             header="geneve", bytes=hexs([0x00, 0x00, 0x65, 0x58, 0x00, 0x04, 0xD2, 0x00]),
+             expect=dict(ok=True, used=8)),
+        dict(name="varlen_geneve_opt", source="ingot/src/tests.rs:182-206", header="geneve",
+             bytes=hexs([0x01, 0x00, 0x65, 0x58, 0x00, 0x04, 0xD2, 0x00, 0x01, 0x29, 0x47, 0x00]),
+             expect=dict(ok=True, used=12)),
+        dict(name="geneve_opts_bench", source="ingot/benches/modify.rs:38-56, 90-93",
+             header="geneve",
+             bytes=hexs([0x01, 0x00, 0x65, 0x58, 0x00, 0x04, 0xD2, 0x00, 0x01, 0x29, 0x00, 0x00]),
+             expect=dict(ok=True, used=12)),
     ]
 
 
@@ -357,7 +469,7 @@ def main() -> None:
     doc = dict(
         reference="oxidecomputer/ingot @ 2025-08-08",
         generator="tests/golden/make_golden.py",
-        chain_kats=chain_frames(),
+        chain_kats=chain_frames() + geneve_frames(),
         header_kats=header_kats(),
         bitfield_kats=bitfield_kats(),
         rss_kats=rss_kats(),

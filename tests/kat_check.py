@@ -5,7 +5,9 @@ Used for both the CPU oracle (test_oracle_golden.py) and the GPU path
 """
 from __future__ import annotations
 
-from ingot_amd.abi import CHAIN_LABELS, REC_ACCEPTED, Chain, L3Kind, L4Kind, ParseError
+import re
+
+from ingot_amd.abi import CHAIN_LABELS, REC_ACCEPTED, REC_INNER, Chain, L3Kind, L4Kind, ParseError
 
 L3_NAMES = {"none": L3Kind.NONE, "ipv4": L3Kind.IPV4, "ipv6": L3Kind.IPV6}
 L4_NAMES = {"none": L4Kind.NONE, "tcp": L4Kind.TCP, "udp": L4Kind.UDP,
@@ -21,9 +23,19 @@ def _field(f, name):
     return bytes(v).hex() if getattr(v, "shape", ()) else int(v)
 
 
+def _outer_field(t, name):
+    m = re.fullmatch(r"(\w+)\[(\d+)\]\.(\w+)", name)
+    v = t[m.group(1)][int(m.group(2))][m.group(3)] if m else t[name]
+    return bytes(v).hex() if getattr(v, "shape", ()) else int(v)
+
+
 def check(kat: dict, rec, fld) -> list[str]:
-    """Return a list of mismatches (empty = pass)."""
+    """Return a list of mismatches (empty = pass).  For the tunnel chain `fld`
+    may be an ingot_geneve_fields (inner + outer blocks)."""
     frame = bytes.fromhex(kat["frame"])
+    outer = None
+    if fld is not None and fld.dtype.names and "outer" in fld.dtype.names:
+        outer, fld = fld["outer"], fld["inner"]
     chain = Chain[kat["chain"]]
     e = kat["expect"]
     bad = []
@@ -46,6 +58,15 @@ def check(kat: dict, rec, fld) -> list[str]:
         got = (ParseError(status).name, CHAIN_LABELS[chain][int(rec["err_layer"])])
         if got != (e["error"], e["label"]):
             bad.append(f"expected {e['error']} at {e['label']}, got {got}")
+    if "inner" in e and bool(int(rec["flags"]) & REC_INNER) != e["inner"]:
+        bad.append(f"inner flag {int(rec['flags'])} != {e['inner']}")
+    if outer is not None:
+        for name, want in e.get("outer_fields", {}).items():
+            got = _outer_field(outer, name)
+            if got != want:
+                bad.append(f"outer {name}: {got} != {want}")
+    elif e.get("outer_fields") and fld is not None:
+        bad.append("outer fields expected but not provided")
     if "l3" in e and int(rec["l3_kind"]) != L3_NAMES[e["l3"]]:
         bad.append(f"l3_kind {int(rec['l3_kind'])} != {e['l3']}")
     if "l4" in e and int(rec["l4_kind"]) != L4_NAMES[e["l4"]]:

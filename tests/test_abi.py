@@ -9,7 +9,7 @@ from pathlib import Path
 import pytest
 
 import ingot_amd
-from ingot_amd import _lib
+from ingot_amd import _lib, abi
 from ingot_amd.abi import (CHAIN_LABELS, FIELDS_DTYPE, REC8_DTYPE, REC_DTYPE, Chain, IngotFields,
                            IngotRec, IngotRec8)
 
@@ -48,20 +48,16 @@ def test_every_declared_symbol_is_exported(lib):
 
 def test_layouts_match_c(tmp_path):
     """Compile a probe against include/ingot_gpu.h and compare every offset."""
-    fields = [f[0] for f in IngotFields._fields_]
-    rec_fields = [f[0] for f in IngotRec._fields_]
-    rec8_fields = [f[0] for f in IngotRec8._fields_]
+    structs = {"ingot_rec": IngotRec, "ingot_rec8": IngotRec8, "ingot_v6eh": abi.IngotV6Eh,
+               "ingot_fields": IngotFields, "ingot_geneve_opt": abi.IngotGeneveOpt,
+               "ingot_tunnel_fields": abi.IngotTunnelFields,
+               "ingot_geneve_fields": abi.IngotGeneveFields}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "ingot_gpu.h"',
-             "int main(void){",
-             'printf("rec %zu\\n", sizeof(ingot_rec));',
-             'printf("fields %zu\\n", sizeof(ingot_fields));']
-    for f in rec_fields:
-        lines.append(f'printf("rec.{f} %zu\\n", offsetof(ingot_rec, {f}));')
-    for f in fields:
-        lines.append(f'printf("fields.{f} %zu\\n", offsetof(ingot_fields, {f}));')
-    for f in rec8_fields:
-        lines.append(f'printf("rec8.{f} %zu\\n", offsetof(ingot_rec8, {f}));')
-    lines.append('printf("rec8 %zu\\n", sizeof(ingot_rec8));')
+             "int main(void){"]
+    for c, py in structs.items():
+        lines.append(f'printf("{c} %zu\\n", sizeof({c}));')
+        for f in (f[0] for f in py._fields_):
+            lines.append(f'printf("{c}.{f} %zu\\n", offsetof({c}, {f}));')
     lines.append("return 0;}")
     src = tmp_path / "probe.c"
     src.write_text("\n".join(lines))
@@ -70,15 +66,14 @@ def test_layouts_match_c(tmp_path):
                    check=True)
     got = dict(line.split() for line in subprocess.run([str(exe)], capture_output=True,
                                                        text=True).stdout.splitlines())
-    assert int(got["rec"]) == REC_DTYPE.itemsize == 16
-    assert int(got["fields"]) == FIELDS_DTYPE.itemsize == 256
-    for f in rec_fields:
-        assert int(got[f"rec.{f}"]) == getattr(IngotRec, f).offset, f
-    assert int(got["rec8"]) == REC8_DTYPE.itemsize == 8
-    for f in rec8_fields:
-        assert int(got[f"rec8.{f}"]) == getattr(IngotRec8, f).offset, f
-    for f in fields:
-        assert int(got[f"fields.{f}"]) == getattr(IngotFields, f).offset, f
+    sizes = {"ingot_rec": 16, "ingot_rec8": 8, "ingot_v6eh": 12, "ingot_fields": 256,
+             "ingot_geneve_opt": 8, "ingot_tunnel_fields": 128, "ingot_geneve_fields": 384}
+    for c, py in structs.items():
+        assert int(got[c]) == ctypes.sizeof(py) == sizes[c], c
+        for f in (f[0] for f in py._fields_):
+            assert int(got[f"{c}.{f}"]) == getattr(py, f).offset, (c, f)
+    assert REC_DTYPE.itemsize == 16 and FIELDS_DTYPE.itemsize == 256
+    assert REC8_DTYPE.itemsize == 8 and abi.GENEVE_FIELDS_DTYPE.itemsize == 384
 
 
 def test_string_tables(lib):
@@ -103,6 +98,7 @@ def test_argument_validation_without_gpu(lib):
     assert lib.ingot_gpu_parse(null, None, None, None, 10, 0, None, None) == -1
     assert lib.ingot_gpu_parse_strided(null, None, 64, None, 10, 0, None, None) == -1
     assert lib.ingot_gpu_fields(null, None, None, None, 64, 10, 0, None, None) == -1
+    assert lib.ingot_gpu_geneve_fields(null, None, None, None, 64, 10, None, None) == -1
     assert lib.ingot_gpu_parse_compact(null, None, None, None, 10, 0, None, None) == -1
     assert lib.ingot_gpu_parse_strided_compact(null, None, 64, None, 10, 0, None, None) == -1
     assert lib.ingot_pktgen_fill(0, 1, 0, 1, None, 0, None, None, 0, None) == -1
