@@ -240,6 +240,65 @@ TEST(bench_parse_stack_v4_batch) {
     }
 }
 
+static std::vector<uint8_t> opte_in_pkt() {
+    // ingot-examples/src/tests.rs:192-261 (== ingot-examples/benches/packet.rs:59-128)
+    std::vector<uint8_t> p = {
+        0xA8, 0x40, 0x25, 0x77, 0x77, 0x76, 0xA8, 0x40, 0x25, 0x77, 0x77, 0x77, 0x86, 0xdd,
+        0x60, 0x00, 0x00, 0x00, 0x00, 0x10, 0x11, 0xf0,
+        0xFD, 0x00, 0x00, 0x00, 0x00, 0xF7, 0x01, 0x01, 0, 0, 0, 0, 0, 0, 0, 0x02,
+        0xFD, 0x00, 0x00, 0x00, 0x00, 0xF7, 0x01, 0x01, 0, 0, 0, 0, 0, 0, 0, 0x01,
+        0x1E, 0x61, 0x17, 0xC1, 0x00, 0x14, 0x00, 0x00,
+        0x01, 0x00, 0x65, 0x58, 0x00, 0x04, 0xD2, 0x00,
+        0x01, 0x29, 0x00, 0x00};
+    const auto inner = would_be_valid();
+    p.insert(p.end(), inner.begin(), inner.end());
+    for (uint8_t b = 0; b < 8; ++b) p.push_back(b);
+    return p;
+}
+
+// ingot-examples/src/tests.rs:189-275
+TEST(test_tunnelled_unconditionals) {
+    auto pkt = opte_in_pkt();
+    {
+        auto [opte_in, hint, rest] = GeneveOverV6Tunnel::parse(pkt).unwrap();
+        (void)hint;
+        ASSERT_EQ(opte_in.outer_encap.options_ref().size(), 4u);
+        ASSERT_EQ(opte_in.inner_eth.ethertype(), ethernet::Ethertype::IPV4);
+        ASSERT_TRUE(opte_in.inner_l3.has_value());
+        ASSERT_TRUE(opte_in.inner_ulp.has_value());
+        ASSERT_EQ(opte_in.outer_encap.vni(), 0x0004D2u);
+        ASSERT_EQ(rest.size(), 8u);
+    }
+    // Now, try out pretending we're ARP and early exiting.
+    put16(pkt, 74 + 12, ethernet::Ethertype::ARP);
+    auto [opte_in, hint, rest] = GeneveOverV6Tunnel::parse(pkt).unwrap();
+    (void)hint;
+    (void)rest;
+    ASSERT_TRUE(!opte_in.inner_l3.has_value());
+    ASSERT_TRUE(!opte_in.inner_ulp.has_value());
+}
+
+// ingot/src/tests.rs:384-419 (to_owned of g_opt, here the tunnel's outer_encap)
+TEST(geneve_to_owned_in_tunnel) {
+    auto [t, hint, rest] = GeneveOverV6Tunnel::parse(opte_in_pkt()).unwrap();
+    (void)hint;
+    (void)rest;
+    const auto& g = t.outer_encap;
+    ASSERT_EQ(g.version(), 0);
+    ASSERT_EQ(g.opt_len(), 1);
+    ASSERT_EQ(g.flags(), 0);
+    ASSERT_EQ(g.protocol_type(), 0x6558);
+    ASSERT_EQ(g.vni(), 0x0004d2u);
+    ASSERT_EQ(g.reserved(), 0);
+    ASSERT_EQ(g.packet_length(), 12u);
+    auto opts = g.options();
+    ASSERT_EQ(opts.size(), 1u);
+    ASSERT_EQ(opts[0].class_, 0x0129);
+    ASSERT_EQ(opts[0].option_type, 0);
+    ASSERT_EQ(opts[0].length, 0);
+    ASSERT_TRUE(opts[0].data.empty());
+}
+
 int main() {
     for (auto& [name, fn] : registry()) {
         ++g_run;
