@@ -126,13 +126,19 @@ std::array<uint8_t, N> arr(const uint8_t* p) {
 
 class ValidEthernet {
    public:
-    explicit ValidEthernet(const ingot_fields* f) : f_(f) {}
-    MacAddr6 destination() const { return detail::arr<6>(f_->eth_destination); }
-    MacAddr6 source() const { return detail::arr<6>(f_->eth_source); }
-    uint16_t ethertype() const { return f_->eth_ethertype; }
+    explicit ValidEthernet(const ingot_fields* f)
+        : dst_(f->eth_destination), src_(f->eth_source), et_(f->eth_ethertype) {}
+    // GeneveOverV6Tunnel's outer_eth
+    explicit ValidEthernet(const ingot_tunnel_fields* t)
+        : dst_(t->outer_eth_destination), src_(t->outer_eth_source), et_(t->outer_eth_ethertype) {}
+    MacAddr6 destination() const { return detail::arr<6>(dst_); }
+    MacAddr6 source() const { return detail::arr<6>(src_); }
+    uint16_t ethertype() const { return et_; }
 
    private:
-    const ingot_fields* f_;
+    const uint8_t* dst_;
+    const uint8_t* src_;
+    uint16_t et_;
 };
 
 class ValidVlanBody {
@@ -221,14 +227,86 @@ class ValidTcp {
 
 class ValidUdp {
    public:
-    explicit ValidUdp(const ingot_fields* f) : f_(f) {}
-    uint16_t source() const { return f_->l4_source; }
-    uint16_t destination() const { return f_->l4_destination; }
-    uint16_t length() const { return f_->udp_length; }
-    uint16_t checksum() const { return f_->udp_checksum; }
+    explicit ValidUdp(const ingot_fields* f)
+        : src_(f->l4_source), dst_(f->l4_destination), len_(f->udp_length),
+          csum_(f->udp_checksum) {}
+    // GeneveOverV6Tunnel's outer_udp
+    explicit ValidUdp(const ingot_tunnel_fields* t)
+        : src_(t->outer_udp_source), dst_(t->outer_udp_destination), len_(t->outer_udp_length),
+          csum_(t->outer_udp_checksum) {}
+    uint16_t source() const { return src_; }
+    uint16_t destination() const { return dst_; }
+    uint16_t length() const { return len_; }
+    uint16_t checksum() const { return csum_; }
 
    private:
-    const ingot_fields* f_;
+    uint16_t src_, dst_, len_, csum_;
+};
+
+// GeneveOverV6Tunnel's outer_v6 (ingot/src/ip.rs:159-182 getters).
+class ValidOuterIpv6 {
+   public:
+    explicit ValidOuterIpv6(const ingot_tunnel_fields* t) : t_(t) {}
+    uint8_t version() const { return t_->outer_v6_version; }
+    uint8_t dscp() const { return t_->outer_v6_dscp; }
+    ip::Ecn ecn() const { return (ip::Ecn)t_->outer_v6_ecn; }
+    uint32_t flow_label() const { return t_->outer_v6_flow_label; }
+    uint16_t payload_len() const { return t_->outer_v6_payload_len; }
+    uint8_t next_header() const { return t_->outer_v6_next_header; }
+    uint8_t hop_limit() const { return t_->outer_v6_hop_limit; }
+    Ipv6Addr source() const { return detail::arr<16>(t_->outer_v6_source); }
+    Ipv6Addr destination() const { return detail::arr<16>(t_->outer_v6_destination); }
+    uint8_t next_layer() const { return t_->outer_l4_proto; }
+    size_t extension_header_count() const { return t_->outer_v6_n_ext; }
+
+   private:
+    const ingot_tunnel_fields* t_;
+};
+
+// ingot::geneve::GeneveOpt (geneve.rs:80-102) with its data bytes.
+struct GeneveOpt {
+    uint16_t class_;
+    uint8_t option_type;
+    uint8_t reserved;
+    uint8_t length;
+    std::vector<uint8_t> data;
+    bool is_critical() const { return (option_type >> 7) == 1; }
+};
+
+// ingot::geneve::ValidGeneve getters (geneve.rs:16-44).
+class ValidGeneve {
+   public:
+    ValidGeneve(const ingot_tunnel_fields* t, const std::vector<uint8_t>* frame)
+        : t_(t), frame_(frame) {}
+    uint8_t version() const { return t_->geneve_version; }
+    uint8_t opt_len() const { return t_->geneve_opt_len; }
+    uint8_t flags() const { return t_->geneve_flags; }
+    uint16_t protocol_type() const { return t_->geneve_protocol_type; }
+    uint32_t vni() const { return t_->geneve_vni; }
+    uint8_t reserved() const { return t_->geneve_reserved; }
+    size_t packet_length() const { return 8u + 4u * t_->geneve_opt_len; }
+    std::vector<uint8_t> options_ref() const {
+        auto b = frame_->begin() + t_->geneve_off + 8;
+        return std::vector<uint8_t>(b, b + 4 * t_->geneve_opt_len);
+    }
+    size_t option_count() const { return t_->geneve_n_opts; }
+    // the first INGOT_MAX_GENEVE_OPT_FIELDS options
+    std::vector<GeneveOpt> options() const {
+        std::vector<GeneveOpt> out;
+        const size_t n = option_count() < INGOT_MAX_GENEVE_OPT_FIELDS ? option_count()
+                                                                      : INGOT_MAX_GENEVE_OPT_FIELDS;
+        for (size_t i = 0; i < n; ++i) {
+            const ingot_geneve_opt& g = t_->geneve_opt[i];
+            auto b = frame_->begin() + g.data_off;
+            out.push_back(GeneveOpt{g.opt_class, g.option_type, g.reserved, g.length,
+                                    std::vector<uint8_t>(b, b + 4 * g.length)});
+        }
+        return out;
+    }
+
+   private:
+    const ingot_tunnel_fields* t_;
+    const std::vector<uint8_t>* frame_;
 };
 
 // L3 choice (ingot-examples/src/choices.rs:17-21) and L4 / Ulp choices.
@@ -247,6 +325,7 @@ struct L4 {
 struct Packet {
     std::vector<uint8_t> frame;
     ingot_fields fields;
+    ingot_tunnel_fields outer;  // GENEVE_OVER_V6 only (zero otherwise)
 };
 
 namespace gpu {
@@ -291,20 +370,36 @@ inline std::vector<Packet> parse_batch(Context& ctx, const std::vector<std::vect
     uint8_t* d_arena = nullptr;
     uint64_t* d_off = nullptr;
     uint16_t* d_len = nullptr;
-    ingot_fields* d_f = nullptr;
+    const bool tun = chain == INGOT_CHAIN_GENEVE_OVER_V6;
+    const size_t blk = tun ? sizeof(ingot_geneve_fields) : sizeof(ingot_fields);
+    uint8_t* d_f = nullptr;
     hip_check(hipMalloc(&d_arena, arena.size()), "hipMalloc");
     hip_check(hipMalloc(&d_off, n * 8 + 8), "hipMalloc");
     hip_check(hipMalloc(&d_len, n * 2 + 8), "hipMalloc");
-    hip_check(hipMalloc(&d_f, n * sizeof(ingot_fields) + 256), "hipMalloc");
+    hip_check(hipMalloc(&d_f, n * blk + 512), "hipMalloc");
     hip_check(hipMemcpy(d_arena, arena.data(), arena.size(), hipMemcpyHostToDevice), "H2D");
     hip_check(hipMemcpy(d_off, off.data(), n * 8, hipMemcpyHostToDevice), "H2D");
     hip_check(hipMemcpy(d_len, len.data(), n * 2, hipMemcpyHostToDevice), "H2D");
-    check(ingot_gpu_fields(ctx.get(), d_arena, d_off, d_len, 0, n, chain, d_f, nullptr),
-          "ingot_gpu_fields");
+    if (tun)
+        check(ingot_gpu_geneve_fields(ctx.get(), d_arena, d_off, d_len, 0, n,
+                                      reinterpret_cast<ingot_geneve_fields*>(d_f), nullptr),
+              "ingot_gpu_geneve_fields");
+    else
+        check(ingot_gpu_fields(ctx.get(), d_arena, d_off, d_len, 0, n, chain,
+                               reinterpret_cast<ingot_fields*>(d_f), nullptr),
+              "ingot_gpu_fields");
     std::vector<Packet> out(n);
-    std::vector<ingot_fields> f(n);
-    hip_check(hipMemcpy(f.data(), d_f, n * sizeof(ingot_fields), hipMemcpyDeviceToHost), "D2H");
-    for (size_t i = 0; i < n; ++i) out[i] = Packet{frames[i], f[i]};
+    std::vector<uint8_t> f(n * blk);
+    hip_check(hipMemcpy(f.data(), d_f, n * blk, hipMemcpyDeviceToHost), "D2H");
+    for (size_t i = 0; i < n; ++i) {
+        out[i].frame = frames[i];
+        std::memcpy(&out[i].fields, f.data() + i * blk, sizeof(ingot_fields));
+        if (tun)
+            std::memcpy(&out[i].outer, f.data() + i * blk + sizeof(ingot_fields),
+                        sizeof(ingot_tunnel_fields));
+        else
+            std::memset(&out[i].outer, 0, sizeof(ingot_tunnel_fields));
+    }
     (void)hipFree(d_arena);
     (void)hipFree(d_off);
     (void)hipFree(d_len);
@@ -418,6 +513,53 @@ struct GenericUlp {
     }
     static types::ParseResult<Success<GenericUlp>> parse_slice(const std::vector<uint8_t>& frame) {
         return parse(frame);
+    }
+};
+
+// ingot-examples/src/packets.rs:27-40 — outer_eth, outer_v6: from L3 -> Ipv6,
+// outer_udp: from L4 -> Udp, outer_encap: Geneve, then GenericUlp's layers.
+struct GeneveOverV6Tunnel {
+    static constexpr int CHAIN = INGOT_CHAIN_GENEVE_OVER_V6;
+    std::shared_ptr<const Packet> pkt;
+    ValidEthernet outer_eth;
+    ValidOuterIpv6 outer_v6;
+    ValidUdp outer_udp;
+    ValidGeneve outer_encap;
+    ValidEthernet inner_eth;
+    std::optional<L3> inner_l3;
+    std::optional<L4> inner_ulp;
+
+    static std::vector<types::ParseResult<Success<GeneveOverV6Tunnel>>> parse_all(
+        const std::vector<std::vector<uint8_t>>& frames,
+        gpu::Context& ctx = gpu::default_context()) {
+        std::vector<types::ParseResult<Success<GeneveOverV6Tunnel>>> out;
+        for (auto& p : gpu::parse_batch(ctx, frames, CHAIN)) {
+            auto sp = std::make_shared<const Packet>(std::move(p));
+            if (sp->fields.rec.status != INGOT_OK) {
+                out.push_back(types::ParseResult<Success<GeneveOverV6Tunnel>>::err(
+                    detail::error_of(CHAIN, sp->fields.rec)));
+                continue;
+            }
+            GeneveOverV6Tunnel c{sp,
+                                 ValidEthernet(&sp->outer),
+                                 ValidOuterIpv6(&sp->outer),
+                                 ValidUdp(&sp->outer),
+                                 ValidGeneve(&sp->outer, &sp->frame),
+                                 ValidEthernet(&sp->fields),
+                                 std::nullopt,
+                                 std::nullopt};
+            if (!(sp->fields.rec.flags & INGOT_REC_ACCEPTED)) {
+                c.inner_l3 = detail::l3_of(*sp);
+                c.inner_ulp = detail::l4_of(*sp);
+            }
+            out.push_back(types::ParseResult<Success<GeneveOverV6Tunnel>>::ok(
+                Success<GeneveOverV6Tunnel>{c, std::nullopt, detail::remainder(*sp)}));
+        }
+        return out;
+    }
+    static types::ParseResult<Success<GeneveOverV6Tunnel>> parse(
+        const std::vector<uint8_t>& frame) {
+        return std::move(parse_all({frame})[0]);
     }
 };
 
