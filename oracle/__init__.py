@@ -61,6 +61,9 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     lib.oracle_parse_geneve.restype = None
     lib.oracle_geneve_fields_batch.argtypes = [vp, vp, vp, ctypes.c_uint32, ctypes.c_uint64, vp]
     lib.oracle_geneve_fields_batch.restype = ctypes.c_int
+    lib.oracle_parse_read_batch.argtypes = [vp, vp, vp, vp, ctypes.c_uint64, ctypes.c_int, vp,
+                                            vp, vp, vp]
+    lib.oracle_parse_read_batch.restype = ctypes.c_int
     if path is None:
         _lib = lib
     return lib
@@ -126,6 +129,53 @@ def geneve_fields_batch(arena: np.ndarray, off: np.ndarray | None, lens: np.ndar
     if lib.oracle_geneve_fields_batch(_p(arena), _p(off), _p(lens), stride, n, _p(out)) != 0:
         raise ValueError("oracle_geneve_fields_batch: bad arguments")
     return out
+
+
+def segments(packets):
+    """[[chunk bytes, ...], ...] -> (arena, seg_off u64, seg_len u16, pkt_seg u32):
+    every chunk stored separately (16-B aligned, a gap after each)."""
+    seg_off, seg_len, pkt_seg, parts, o = [], [], [0], [], 0
+    for chunks in packets:
+        for c in chunks:
+            seg_off.append(o)
+            seg_len.append(len(c))
+            pad = (len(c) + 15) // 16 * 16 + 16
+            parts.append(bytes(c) + b"\xee" * (pad - len(c)))
+            o += pad
+        pkt_seg.append(len(seg_off))
+    arena = np.frombuffer(b"".join(parts) + bytes(64), dtype=np.uint8).copy()
+    return (arena, np.array(seg_off, dtype=np.uint64), np.array(seg_len, dtype=np.uint16),
+            np.array(pkt_seg, dtype=np.uint32))
+
+
+def parse_read_batch(arena, seg_off, seg_len, pkt_seg, chain: Chain, fields: str | None = None,
+                     lib: ctypes.CDLL | None = None):
+    """parse_read over multi-segment packets -> (records, field blocks or None,
+    chunk index u16[n]).  fields: None, "fields" (ingot_fields) or "geneve"."""
+    lib = lib or load()
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    seg_off = np.ascontiguousarray(seg_off, dtype=np.uint64)
+    seg_len = np.ascontiguousarray(seg_len, dtype=np.uint16)
+    pkt_seg = np.ascontiguousarray(pkt_seg, dtype=np.uint32)
+    n = len(pkt_seg) - 1
+    rec = np.zeros(n, dtype=REC_DTYPE)
+    chunk = np.zeros(n, dtype=np.uint16)
+    fld = gf = None
+    if fields == "fields":
+        fld = np.zeros(n, dtype=FIELDS_DTYPE)
+    elif fields == "geneve":
+        gf = np.zeros(n, dtype=GENEVE_FIELDS_DTYPE)
+    rc = lib.oracle_parse_read_batch(_p(arena), _p(seg_off), _p(seg_len), _p(pkt_seg), n,
+                                     int(chain), _p(rec), _p(fld), _p(gf), _p(chunk))
+    if rc != 0:
+        raise ValueError("oracle_parse_read_batch: bad arguments")
+    return rec, (fld if fld is not None else gf), chunk
+
+
+def parse_read(chunks, chain: Chain, fields: str | None = None):
+    """One packet given as a list of chunks -> (record, fields, chunk index)."""
+    rec, f, ch = parse_read_batch(*segments([chunks]), chain, fields=fields)
+    return rec[0], (None if f is None else f[0]), int(ch[0])
 
 
 def be_bits(hdr: bytes, first_bit: int, n_bits: int) -> int:

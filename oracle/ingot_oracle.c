@@ -24,6 +24,7 @@ enum {
     PE_UNWANTED = INGOT_ERR_UNWANTED,
     PE_NEEDS_HINT = INGOT_ERR_NEEDS_HINT,
     PE_TOO_SMALL = INGOT_ERR_TOO_SMALL,
+    PE_STRADDLED = INGOT_ERR_STRADDLED_HEADER,
     PE_CANNOT_ACCEPT = INGOT_ERR_CANNOT_ACCEPT
 };
 
@@ -330,15 +331,40 @@ static void fields_icmp(ingot_fields* F, const uint8_t* s) {
  * ---------------------------------------------------------------------- */
 typedef struct {
     const uint8_t* f;
-    uint32_t len;
-    uint32_t p; /* bytes consumed */
+    uint32_t len; /* end of the current chunk (the whole frame for parse_slice) */
+    uint32_t p;   /* bytes consumed */
     ingot_rec* r;
     ingot_fields* F;
+    /* parse_read over chunks (parse.rs:511-537): f is the chunks concatenated,
+     * chunk k spans seglen[0..k) .. +seglen[k]; NULL for parse_slice. */
+    const uint16_t* seglen;
+    uint32_t nseg, k;
 } walk_t;
 
+static int more_chunks(const walk_t* w) { return w->seglen && w->k + 1 < w->nseg; }
+
 static void fail(walk_t* w, int layer, int code) {
+    /* parse_read: a header that does not fit its chunk is StraddledHeader when
+     * another chunk exists, else TooSmall (ParseError::convert_read_parse,
+     * error.rs:65-72, applied to every layer's parse error, parse.rs:296-347). */
+    if (code == PE_TOO_SMALL && more_chunks(w)) code = PE_STRADDLED;
     w->r->status = (uint8_t)code;
     w->r->err_layer = (uint8_t)layer;
+}
+
+/* parse_read's step between a layer and the next (parse.rs:205-218): if the
+ * layer left the chunk empty, the next chunk becomes the slice; with none
+ * left that is TooSmall at this layer's label.  No-op for parse_slice and
+ * after the last layer. */
+static int next_slice(walk_t* w, int layer) {
+    if (!w->seglen || w->p != w->len) return PE_OK;
+    if (!more_chunks(w)) {
+        fail(w, layer, PE_TOO_SMALL);
+        return PE_TOO_SMALL;
+    }
+    w->k++;
+    w->len += w->seglen[w->k];
+    return PE_OK;
 }
 
 /* L3 choice (ingot-examples/src/choices.rs:17-21; choice.rs:231-246). */
@@ -500,6 +526,7 @@ static void geneve_chain(walk_t* w, uint32_t et, ingot_fields* inner, ingot_tunn
         memcpy(T->outer_eth_source, f + 6, 6);
         T->outer_eth_ethertype = (uint16_t)et;
     }
+    if (next_slice(w, 0) != PE_OK) return;
     if (layer_l3(w, 1, et, &proto) != PE_OK) return;
     if (r->l3_kind != INGOT_L3_IPV6) {
         fail(w, 1, PE_UNWANTED);
@@ -521,6 +548,7 @@ static void geneve_chain(walk_t* w, uint32_t et, ingot_fields* inner, ingot_tunn
         T->outer_v6_n_ext = r->n_v6ext;
         T->outer_l4_proto = (uint8_t)proto;
     }
+    if (next_slice(w, 1) != PE_OK) return;
     if (layer_l4(w, 2, proto, 0, 1) != PE_OK) return;
     if (T) {
         const uint8_t* s = f + r->l4_off;
@@ -530,6 +558,7 @@ static void geneve_chain(walk_t* w, uint32_t et, ingot_fields* inner, ingot_tunn
         T->outer_udp_length = (uint16_t)be16(s + 4);
         T->outer_udp_checksum = (uint16_t)be16(s + 6);
     }
+    if (next_slice(w, 2) != PE_OK) return;
     e = parse_geneve(f + w->p, w->len - w->p, w->p, &used, T);
     if (e != PE_OK) {
         fail(w, 3, e);
@@ -538,6 +567,7 @@ static void geneve_chain(walk_t* w, uint32_t et, ingot_fields* inner, ingot_tunn
     if (T) T->geneve_off = (uint16_t)w->p;
     w->p += used;
     r->payload_off = (uint16_t)w->p;
+    if (next_slice(w, 3) != PE_OK) return;
 
     e = parse_eth(f + w->p, w->len - w->p, &used, &iet);
     if (e != PE_OK) {
@@ -557,32 +587,34 @@ static void geneve_chain(walk_t* w, uint32_t et, ingot_fields* inner, ingot_tunn
     w->p += used;
     r->payload_off = (uint16_t)w->p;
     if (iet == ET_ARP) {
+        /* accepted: inner_l3 / inner_ulp are None, but parse_read still
+         * steps the slice after each non-final layer */
         r->flags |= INGOT_REC_ACCEPTED;
+        if (next_slice(w, 4) == PE_OK) next_slice(w, 5);
         return;
     }
+    if (next_slice(w, 4) != PE_OK) return;
     if (layer_l3(w, 5, iet, &proto) != PE_OK) return;
+    if (next_slice(w, 5) != PE_OK) return;
     layer_l4(w, 6, proto, 1, 0);
 }
 
-static void parse_one(const uint8_t* frame, uint32_t len, int chain, ingot_rec* rec,
-                      ingot_fields* fields, ingot_tunnel_fields* tunnel) {
-    memset(rec, 0, sizeof *rec);
-    if (fields) memset(fields, 0, sizeof *fields);
-    if (tunnel) memset(tunnel, 0, sizeof *tunnel);
-    const int tun = chain == INGOT_CHAIN_GENEVE_OVER_V6;
-    /* the tunnel's outer layers have no ingot_fields slots */
-    walk_t w = {frame, len, 0, rec, tun ? 0 : fields};
+static void walk_chain(walk_t* w, int chain, ingot_fields* fields, ingot_tunnel_fields* tunnel) {
+    ingot_rec* rec = w->r;
+    const uint8_t* frame = w->f;
     uint32_t et = 0, proto = 0;
     rec->err_layer = 0xff;
 
-    if (layer_eth(&w, &et) != PE_OK) goto out;
+    if (layer_eth(w, &et) != PE_OK) goto out;
 
     switch (chain) {
     case INGOT_CHAIN_UDP_PARSER:
         /* UdpParser { eth, l3: L3, #[ingot(from = "L4<Q>")] l4: UdpPacket }
          * (ingot-examples/src/packets.rs:18-24) */
-        if (layer_l3(&w, 1, et, &proto) != PE_OK) goto out;
-        layer_l4(&w, 2, proto, 0, 1);
+        if (next_slice(w, 0) != PE_OK) goto out;
+        if (layer_l3(w, 1, et, &proto) != PE_OK) goto out;
+        if (next_slice(w, 1) != PE_OK) goto out;
+        layer_l4(w, 2, proto, 0, 1);
         break;
     case INGOT_CHAIN_GENERIC_ULP:
         /* GenericUlp { #[ingot(control = exit_on_arp)] inner_eth,
@@ -592,34 +624,41 @@ static void parse_one(const uint8_t* frame, uint32_t len, int chain, ingot_rec* 
          * layer is allowed and skips both optional layers. */
         if (et == ET_ARP) {
             rec->flags |= INGOT_REC_ACCEPTED;
+            if (next_slice(w, 0) == PE_OK) next_slice(w, 1);
             break;
         }
-        if (layer_l3(&w, 1, et, &proto) != PE_OK) goto out;
-        layer_l4(&w, 2, proto, 1, 0);
+        if (next_slice(w, 0) != PE_OK) goto out;
+        if (layer_l3(w, 1, et, &proto) != PE_OK) goto out;
+        if (next_slice(w, 1) != PE_OK) goto out;
+        layer_l4(w, 2, proto, 1, 0);
         break;
     case INGOT_CHAIN_VLAN_ULP:
-        /* Build-defined chain (no reference chain uses VlanBody). */
+        /* Build-defined chain (no reference chain uses VlanBody); under
+         * parse_read each tag is a header followed by the slice step. */
+        if (next_slice(w, 0) != PE_OK) goto out;
         while ((et == ET_VLAN || et == ET_QINQ) && rec->n_vlan < 2) {
             uint32_t used = 0;
-            const uint8_t* s = frame + w.p;
-            if (parse_vlan(s, len - w.p, &used, &et) != PE_OK) {
-                fail(&w, 1, PE_TOO_SMALL);
+            const uint8_t* s = frame + w->p;
+            if (parse_vlan(s, w->len - w->p, &used, &et) != PE_OK) {
+                fail(w, 1, PE_TOO_SMALL);
                 goto out;
             }
             if (fields) fields_vlan(fields, rec->n_vlan, s);
             rec->n_vlan++;
-            w.p += used;
-            rec->payload_off = (uint16_t)w.p;
+            w->p += used;
+            rec->payload_off = (uint16_t)w->p;
             rec->ethertype = (uint16_t)et;
+            if (next_slice(w, 1) != PE_OK) goto out;
         }
-        if (layer_l3(&w, 2, et, &proto) != PE_OK) goto out;
-        layer_l4(&w, 3, proto, 1, 0);
+        if (layer_l3(w, 2, et, &proto) != PE_OK) goto out;
+        if (next_slice(w, 2) != PE_OK) goto out;
+        layer_l4(w, 3, proto, 1, 0);
         break;
     case INGOT_CHAIN_GENEVE_OVER_V6:
-        geneve_chain(&w, et, fields, tunnel);
+        geneve_chain(w, et, fields, tunnel);
         break;
     default:
-        fail(&w, 0, PE_UNWANTED);
+        fail(w, 0, PE_UNWANTED);
         break;
     }
 out:
@@ -627,9 +666,63 @@ out:
     if (fields) fields->rec = *rec;
 }
 
+static void parse_one(const uint8_t* frame, uint32_t len, int chain, ingot_rec* rec,
+                      ingot_fields* fields, ingot_tunnel_fields* tunnel) {
+    memset(rec, 0, sizeof *rec);
+    if (fields) memset(fields, 0, sizeof *fields);
+    if (tunnel) memset(tunnel, 0, sizeof *tunnel);
+    const int tun = chain == INGOT_CHAIN_GENEVE_OVER_V6;
+    /* the tunnel's outer layers have no ingot_fields slots */
+    walk_t w = {frame, len, 0, rec, tun ? 0 : fields, 0, 0, 0};
+    walk_chain(&w, chain, fields, tunnel);
+}
+
+/* parse_read: the chunks are concatenated (bytes past 65535 are dropped: the
+ * record's offsets are u16) and walked with chunk-end bounds. */
+static void parse_read_one(const uint8_t* arena, const uint64_t* seg_off,
+                           const uint16_t* seg_len, uint32_t nseg, int chain, ingot_rec* rec,
+                           ingot_fields* fields, ingot_tunnel_fields* tunnel, uint16_t* chunk) {
+    uint8_t* buf = (uint8_t*)malloc(65536 + 16);
+    uint16_t* lens = (uint16_t*)malloc(sizeof(uint16_t) * (nseg ? nseg : 1));
+    uint32_t total = 0;
+    for (uint32_t k = 0; k < nseg; ++k) {
+        uint32_t l = seg_len[k];
+        if (total + l > 65535u) l = 65535u - total;
+        memcpy(buf + total, arena + seg_off[k], l);
+        lens[k] = (uint16_t)l;
+        total += l;
+    }
+    memset(rec, 0, sizeof *rec);
+    if (fields) memset(fields, 0, sizeof *fields);
+    if (tunnel) memset(tunnel, 0, sizeof *tunnel);
+    const int tun = chain == INGOT_CHAIN_GENEVE_OVER_V6;
+    /* next_chunk() for the first slice: no chunks -> TooSmall (lib.rs:169-175),
+     * which the eth layer then reports (a zero-length first slice). */
+    walk_t w = {buf, nseg ? lens[0] : 0u, 0, rec, tun ? 0 : fields, lens, nseg, 0};
+    walk_chain(&w, chain, fields, tunnel);
+    if (chunk) *chunk = (uint16_t)w.k;
+    free(lens);
+    free(buf);
+}
 void oracle_parse_one(const uint8_t* frame, uint32_t len, int chain, ingot_rec* rec,
                       ingot_fields* fields) {
     parse_one(frame, len, chain, rec, fields, 0);
+}
+
+int oracle_parse_read_batch(const uint8_t* arena, const uint64_t* seg_off, const uint16_t* seg_len,
+                            const uint32_t* pkt_seg, uint64_t n, int chain, ingot_rec* rec,
+                            ingot_fields* fields, ingot_geneve_fields* gfields, uint16_t* chunk) {
+    if ((!rec && n) || !pkt_seg || chain < 0 || chain >= INGOT_CHAIN_COUNT) return -1;
+    if (fields && gfields) return -1;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t a = pkt_seg[i], b = pkt_seg[i + 1];
+        ingot_rec* r = gfields ? &gfields[i].inner.rec : &rec[i];
+        parse_read_one(arena, seg_off + a, seg_len + a, b - a, chain, r,
+                       gfields ? &gfields[i].inner : fields ? &fields[i] : 0,
+                       gfields ? &gfields[i].outer : 0, chunk ? &chunk[i] : 0);
+        if (gfields) rec[i] = *r;
+    }
+    return 0;
 }
 
 void oracle_parse_geneve(const uint8_t* frame, uint32_t len, ingot_geneve_fields* out) {

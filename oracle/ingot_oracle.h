@@ -35,6 +35,16 @@ int oracle_geneve_fields_batch(const uint8_t* arena, const uint64_t* off,
                                const uint16_t* len, uint32_t stride, uint64_t n,
                                ingot_geneve_fields* out);
 
+/* parse_read (ingot-macros/src/parse.rs:511-537) over multi-segment packets:
+ * packet i is the chunks seg[pkt_seg[i] .. pkt_seg[i+1]) of (seg_off, seg_len)
+ * in `arena`; record offsets are logical (the chunks concatenated).  chunk[i]
+ * (optional) = index of the chunk holding the remainder.  fields (ingot_fields)
+ * or gfields (GENEVE_OVER_V6's ingot_geneve_fields) optional, not both. */
+int oracle_parse_read_batch(const uint8_t* arena, const uint64_t* seg_off,
+                            const uint16_t* seg_len, const uint32_t* pkt_seg, uint64_t n,
+                            int chain, ingot_rec* rec, ingot_fields* fields,
+                            ingot_geneve_fields* gfields, uint16_t* chunk);
+
 /* Batch form.  off == NULL selects the strided layout (frame i at i*stride);
  * len == NULL means every frame is `stride` bytes long.  fields may be NULL.
  * nthreads <= 1 runs on the calling thread; otherwise a static contiguous

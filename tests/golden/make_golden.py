@@ -382,6 +382,69 @@ def geneve_frames():
     return out
 
 
+def read_kats():
+    """parse_read (multi-chunk) vectors: `chunks` instead of `frame`; expect
+    adds `chunk` (index of the chunk holding the remainder), `last_chunk_len`
+    (Parsed::last_chunk length, 0 = None) and `data_left` (chunks after it)."""
+    out = []
+    # ingot-examples/src/tests.rs:120-187 parse_header_chain_multichunk
+    e = eth(BROADCAST, MAC_ABCDEF, 0x86DD)
+    v6 = [0] * 40
+    v6[6] = 17
+    v6[8:24] = [0] * 15 + [1]
+    udp = u16(6082) + u16(6081) + u16(128) + u16(0xFFFF)
+    out.append(dict(
+        name="parse_header_chain_multichunk", source="ingot-examples/src/tests.rs:120-187",
+        chain="UdpParser", chunks=[hexs(e), hexs(v6), hexs(udp), hexs([0xAA] * 128)],
+        expect=dict(ok=True, l3="ipv6", l4="udp", chunk=2, last_chunk_len=0, data_left=1,
+                    l4_proto=17,
+                    fields=dict(eth_source=hexs(MAC_ABCDEF), eth_destination=hexs(BROADCAST),
+                                eth_ethertype=0x86DD, v6_next_header=17,
+                                v6_source=hexs([0] * 15 + [1]), v6_destination=hexs([0] * 16),
+                                l4_source=6082, l4_destination=6081, udp_length=128,
+                                udp_checksum=0xFFFF))))
+    # ingot-examples/src/tests.rs:277-305 chunks_present_on_early_accept
+    out.append(dict(
+        name="chunks_present_on_early_accept", source="ingot-examples/src/tests.rs:277-305",
+        chain="GenericUlp", chunks=[hexs(ARP_PKT[:14]), hexs(ARP_PKT[14:])],
+        expect=dict(ok=True, accepted=True, chunk=1, last_chunk_len=8, data_left=0)))
+    # ingot-examples/src/tests.rs:381-423 straddle_failure
+    out.append(dict(
+        name="straddle_failure", source="ingot-examples/src/tests.rs:381-412",
+        chain="GenericUlp", chunks=[hexs(WOULD_BE_VALID[:16]), hexs(WOULD_BE_VALID[16:])],
+        expect=dict(ok=False, error="StraddledHeader", label="inner_l3")))
+    out.append(dict(
+        name="straddle_failure_last_chunk", source="ingot-examples/src/tests.rs:414-422",
+        chain="GenericUlp", chunks=[hexs(WOULD_BE_VALID[:16])],
+        expect=dict(ok=False, error="TooSmall", label="inner_l3")))
+    # Derived from the generated parse_read (parse.rs:205-218): a layer that
+    # ends its chunk pulls the next one even when the rest is accepted, so an
+    # ARP frame alone in one chunk is TooSmall at inner_eth under parse_read
+    # (Ok under parse_slice).
+    out.append(dict(
+        name="read_accept_needs_next_chunk", source="ingot-macros/src/parse.rs:205-218",
+        chain="GenericUlp", chunks=[hexs(ARP_PKT[:14])], derived="slice step after the control",
+        expect=dict(ok=False, error="TooSmall", label="inner_eth")))
+    # No chunks at all: next_chunk() fails at the first label (parse.rs:520-521).
+    out.append(dict(
+        name="read_no_chunks", source="ingot-macros/src/parse.rs:520-521", chain="UdpParser",
+        chunks=[], derived="empty reader", expect=dict(ok=False, error="TooSmall", label="eth")))
+    # The tunnel frame of ingot-examples/src/tests.rs:189-268, one header per chunk.
+    cuts = [0, 14, 54, 62, 74, 88, 108, 116, len(OPTE_IN)]
+    out.append(dict(
+        name="tunnel_one_header_per_chunk", source="ingot-examples/src/tests.rs:189-268",
+        chain="GeneveOverV6Tunnel", derived="reference frame split at every header boundary",
+        chunks=[hexs(OPTE_IN[a:b]) for a, b in zip(cuts, cuts[1:])],
+        expect=dict(ok=True, l3="ipv4", l4="udp", inner=True, chunk=6, last_chunk_len=0,
+                    data_left=1, outer_fields={"geneve_vni": 0x04D2, "geneve_n_opts": 1})))
+    out.append(dict(
+        name="tunnel_straddled_outer_v6", source="ingot-examples/src/tests.rs:189-268",
+        chain="GeneveOverV6Tunnel", derived="split inside the outer IPv6 header",
+        chunks=[hexs(OPTE_IN[:30]), hexs(OPTE_IN[30:])],
+        expect=dict(ok=False, error="StraddledHeader", label="outer_v6")))
+    return out
+
+
 def header_kats():
     """Header-level vectors: (header kind, bytes, hint) -> (status, used, hint)."""
     zero54 = [0] * 54
@@ -471,11 +534,13 @@ def main() -> None:
         generator="tests/golden/make_golden.py",
         chain_kats=chain_frames() + geneve_frames(),
         header_kats=header_kats(),
+        read_kats=read_kats(),
         bitfield_kats=bitfield_kats(),
         rss_kats=rss_kats(),
     )
     (HERE / "kats.json").write_text(json.dumps(doc, indent=1) + "\n")
-    print(f"wrote {len(doc['chain_kats'])} chain, {len(doc['header_kats'])} header, "
+    print(f"wrote {len(doc['chain_kats'])} chain, {len(doc['read_kats'])} read, "
+          f"{len(doc['header_kats'])} header, "
           f"{len(doc['bitfield_kats'])} bitfield vectors")
 
 

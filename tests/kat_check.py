@@ -29,10 +29,18 @@ def _outer_field(t, name):
     return bytes(v).hex() if getattr(v, "shape", ()) else int(v)
 
 
-def check(kat: dict, rec, fld) -> list[str]:
+def kat_frame(kat: dict) -> bytes:
+    """The frame bytes (parse_read vectors: the chunks concatenated)."""
+    if "chunks" in kat:
+        return b"".join(bytes.fromhex(c) for c in kat["chunks"])
+    return bytes.fromhex(kat["frame"])
+
+
+def check(kat: dict, rec, fld, chunk: int | None = None) -> list[str]:
     """Return a list of mismatches (empty = pass).  For the tunnel chain `fld`
-    may be an ingot_geneve_fields (inner + outer blocks)."""
-    frame = bytes.fromhex(kat["frame"])
+    may be an ingot_geneve_fields (inner + outer blocks); for parse_read
+    vectors `chunk` is the index of the chunk holding the remainder."""
+    frame = kat_frame(kat)
     outer = None
     if fld is not None and fld.dtype.names and "outer" in fld.dtype.names:
         outer, fld = fld["outer"], fld["inner"]
@@ -58,6 +66,16 @@ def check(kat: dict, rec, fld) -> list[str]:
         got = (ParseError(status).name, CHAIN_LABELS[chain][int(rec["err_layer"])])
         if got != (e["error"], e["label"]):
             bad.append(f"expected {e['error']} at {e['label']}, got {got}")
+    if "chunk" in e:
+        lens = [len(bytes.fromhex(c)) for c in kat["chunks"]]
+        if chunk != e["chunk"]:
+            bad.append(f"chunk {chunk} != {e['chunk']}")
+        else:
+            last = sum(lens[:chunk + 1]) - int(rec["payload_off"])
+            if last != e["last_chunk_len"]:
+                bad.append(f"last_chunk_len {last} != {e['last_chunk_len']}")
+            if len(lens) - chunk - 1 != e["data_left"]:
+                bad.append(f"data_left {len(lens) - chunk - 1} != {e['data_left']}")
     if "inner" in e and bool(int(rec["flags"]) & REC_INNER) != e["inner"]:
         bad.append(f"inner flag {int(rec['flags'])} != {e['inner']}")
     if outer is not None:

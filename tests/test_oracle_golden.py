@@ -32,6 +32,43 @@ def test_chain_kat(kats, idx):
     assert not bad, f"{kat['name']} ({kat['source']}): {bad}"
 
 
+def test_read_kats(kats):
+    """parse_read (multi-chunk) vectors: StraddledHeader, chunk stepping."""
+    assert len(kats["read_kats"]) >= 6
+    for kat in kats["read_kats"]:
+        chunks = [bytes.fromhex(c) for c in kat["chunks"]]
+        chain = Chain[kat["chain"]]
+        kind = "geneve" if chain == Chain.GeneveOverV6Tunnel else "fields"
+        rec, fld, ch = oracle.parse_read(chunks, chain, fields=kind)
+        bad = check(kat, rec, fld, chunk=ch)
+        assert not bad, f"{kat['name']} ({kat['source']}): {bad}"
+
+
+def test_read_single_chunk_equals_parse_slice():
+    """One chunk holding the whole frame: parse_read == parse_slice, except
+    that a layer ending exactly at the frame end before the last layer now
+    pulls a (missing) next chunk (parse.rs:205-218)."""
+    from tests.frames import build_frames
+
+    for chain in Chain:
+        for f in build_frames(1500, seed=int(chain) + 3, vlan=True, broken=0.3):
+            r1, _ = oracle.parse_one(f, chain)
+            r2, _, ch = oracle.parse_read([f], chain)
+            assert ch == 0
+            if r1.tobytes() != r2.tobytes():
+                # only when a non-final layer ended the only chunk: the slice
+                # step then fails with TooSmall at that layer
+                assert int(r1["payload_off"]) == len(f) >= 14, (chain, f.hex())
+                assert ParseError(int(r2["status"])) == ParseError.TooSmall, f.hex()
+                assert int(r2["err_layer"]) < ingot_amd_layers(chain) - 1
+
+
+def ingot_amd_layers(chain):
+    from ingot_amd.abi import CHAIN_LABELS
+
+    return len(CHAIN_LABELS[chain])
+
+
 def test_header_kats(kats):
     for kat in kats["header_kats"]:
         st, used, hint = oracle.parse_header(kat["header"], bytes.fromhex(kat["bytes"]))
