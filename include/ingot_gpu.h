@@ -42,9 +42,9 @@ extern "C" {
 
 /* ---------------------------------------------------------------------------
  * Per-packet status: 0 = Ok, else 1 + the ParseError discriminant in the
- * declaration order of ingot-types/src/error.rs:22-44.  On the single-slice
- * chains below only UNWANTED, TOO_SMALL and CANNOT_ACCEPT are reachable
- * (SURVEY §8a A17); the others are listed so the numbering is ingot's.
+ * declaration order of ingot-types/src/error.rs:22-44.  Reachable: UNWANTED
+ * and TOO_SMALL, STRADDLED_HEADER under ingot_gpu_parse_read;
+ * the others are listed so the numbering is ingot's.
  * ------------------------------------------------------------------------- */
 enum ingot_status {
     INGOT_OK = 0,
@@ -414,6 +414,39 @@ int ingot_gpu_geneve_fields(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
                             const uint64_t* d_off, const uint16_t* d_len,
                             uint32_t stride, uint64_t n,
                             ingot_geneve_fields* d_out, void* stream);
+
+/*
+ * Batched `<Chain>::parse_read` (ingot-macros/src/parse.rs:511-537) over
+ * multi-chunk packets (mblk_t-style chains) — the `Read` input of
+ * ingot-types/src/lib.rs:151-166 as a chunk list:
+ *   d_seg_off / d_seg_len  every chunk's device offset into d_arena and length;
+ *   d_pkt_seg              n+1 u32 bounds: packet i is chunks
+ *                          [d_pkt_seg[i], d_pkt_seg[i+1]) in order.
+ * Semantics are parse_read's: a header must lie inside one chunk; a layer
+ * that ends its chunk makes the next chunk the slice (none left: TooSmall at
+ * that layer, even if the rest was accepted); a header cut by its chunk's end
+ * is StraddledHeader when another chunk follows, else TooSmall
+ * (error.rs:65-72); no chunks at all is TooSmall at the first label.
+ * Record offsets are logical (into the chunks concatenated; a packet's
+ * chunks should total <= 65535 B: later bytes are not seen).  d_chunk
+ * (optional, n x u16) = index within the packet of the chunk holding the
+ * remainder: Parsed::last_chunk is that chunk from payload_off (None when
+ * empty), Parsed::data the chunks after it.  No 8-B records or flow mode.
+ */
+int ingot_gpu_parse_read(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
+                         const uint64_t* d_seg_off, const uint16_t* d_seg_len,
+                         const uint32_t* d_pkt_seg, uint64_t n, int chain,
+                         ingot_rec* d_out, uint16_t* d_chunk, void* stream);
+/* Parity mode of the same (GENEVE_OVER_V6: EINVAL, use the geneve form). */
+int ingot_gpu_fields_read(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
+                          const uint64_t* d_seg_off, const uint16_t* d_seg_len,
+                          const uint32_t* d_pkt_seg, uint64_t n, int chain,
+                          ingot_fields* d_out, uint16_t* d_chunk, void* stream);
+int ingot_gpu_geneve_fields_read(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
+                                 const uint64_t* d_seg_off, const uint16_t* d_seg_len,
+                                 const uint32_t* d_pkt_seg, uint64_t n,
+                                 ingot_geneve_fields* d_out, uint16_t* d_chunk,
+                                 void* stream);
 
 /*
  * Flow classification + per-flow histogram (config 5; build-defined, ingot

@@ -206,6 +206,36 @@ class Context:
                    "ingot_gpu_geneve_fields")
         return out
 
+    def parse_read(self, arena, seg_off, seg_len, pkt_seg, chain: Chain, out=None, chunk=None,
+                   fields: Optional[str] = None, stream=None):
+        """Batched `<chain>::parse_read` over multi-chunk packets (packet i =
+        chunks pkt_seg[i]..pkt_seg[i+1] of (seg_off int64, seg_len uint16);
+        pkt_seg int32/uint32 with n+1 entries).  Returns (out, chunk): records
+        (fields=None), ingot_fields blocks (fields="fields") or
+        ingot_geneve_fields blocks (fields="geneve"), and per packet the index
+        of the chunk holding the remainder (uint16 stored in an int16 tensor)."""
+        torch = _torch()
+        n = pkt_seg.numel() - 1
+        width = {None: REC_BYTES, "fields": FIELDS_BYTES,
+                 "geneve": GENEVE_FIELDS_DTYPE.itemsize}[fields]
+        if out is None:
+            out = torch.empty((n, width), dtype=torch.uint8, device=arena.device)
+        if chunk is None:
+            chunk = torch.empty(n, dtype=torch.int16, device=arena.device)
+        self._check_dev(arena, seg_off, seg_len, pkt_seg, out, chunk)
+        args = (self._h, _ptr(arena), _ptr(seg_off), _ptr(seg_len), _ptr(pkt_seg), n)
+        if fields is None:
+            rc = self._lib.ingot_gpu_parse_read(*args, int(chain), _ptr(out), _ptr(chunk),
+                                                _stream(stream))
+        elif fields == "fields":
+            rc = self._lib.ingot_gpu_fields_read(*args, int(chain), _ptr(out), _ptr(chunk),
+                                                 _stream(stream))
+        else:
+            rc = self._lib.ingot_gpu_geneve_fields_read(*args, _ptr(out), _ptr(chunk),
+                                                        _stream(stream))
+        _lib.check(rc, "ingot_gpu_parse_read")
+        return out, chunk
+
     def flow_hist(self, arena, off, lens, chain: Chain, hist=None, bins: Optional[int] = None,
                   stride: int = 0, n: Optional[int] = None, key: Optional[bytes] = None,
                   flow=None, hashes=None, stream=None):

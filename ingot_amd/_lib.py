@@ -50,6 +50,20 @@ SIGNATURES = {
         ctypes.c_int,
         [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, ctypes.c_uint32, c_u64, c_u8p, ctypes.c_void_p],
     ),
+    "ingot_gpu_parse_read": (
+        ctypes.c_int,
+        [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, c_u8p, c_u64, ctypes.c_int, c_u8p, c_u8p,
+         ctypes.c_void_p],
+    ),
+    "ingot_gpu_fields_read": (
+        ctypes.c_int,
+        [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, c_u8p, c_u64, ctypes.c_int, c_u8p, c_u8p,
+         ctypes.c_void_p],
+    ),
+    "ingot_gpu_geneve_fields_read": (
+        ctypes.c_int,
+        [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, c_u8p, c_u64, c_u8p, c_u8p, ctypes.c_void_p],
+    ),
     "ingot_gpu_flow_hist": (
         ctypes.c_int,
         [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, ctypes.c_uint32, c_u64, ctypes.c_int, c_u8p,

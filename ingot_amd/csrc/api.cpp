@@ -77,6 +77,18 @@ int parse_strided(ingot_gpu_ctx* ctx, const uint8_t* d_arena, uint32_t stride,
                                             ctx->tuning, (hipStream_t)stream));
 }
 
+int parse_segmented(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_seg_off,
+                    const uint16_t* d_seg_len, const uint32_t* d_pkt_seg, uint64_t n, int chain,
+                    void* d_out, uint16_t* d_chunk, int mode, void* stream) {
+    if (!ctx || !chain_ok(chain)) return INGOT_GPU_EINVAL;
+    if (n == 0) return INGOT_GPU_SUCCESS;
+    if (!d_arena || !d_seg_off || !d_seg_len || !d_pkt_seg || !d_out) return INGOT_GPU_EINVAL;
+    if (int e = enter(ctx)) return e;
+    ingot_gpu::ParseArgs a{d_arena, d_seg_off, d_seg_len, 0, n, d_out, d_pkt_seg, d_chunk};
+    return from_hip(ingot_gpu::launch_parse(a, ingot_gpu::LAYOUT_SEGMENTED, chain, mode,
+                                            ctx->tuning, (hipStream_t)stream));
+}
+
 }  // namespace
 
 extern "C" {
@@ -178,6 +190,30 @@ int ingot_gpu_geneve_fields(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const ui
                              stream);
     return parse_strided(ctx, d_arena, stride, d_len, n, chain, d_out, ingot_gpu::OUT_FIELDS,
                          stream);
+}
+
+int ingot_gpu_parse_read(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_seg_off,
+                         const uint16_t* d_seg_len, const uint32_t* d_pkt_seg, uint64_t n,
+                         int chain, ingot_rec* d_out, uint16_t* d_chunk, void* stream) {
+    return parse_segmented(ctx, d_arena, d_seg_off, d_seg_len, d_pkt_seg, n, chain, d_out,
+                           d_chunk, ingot_gpu::OUT_REC16, stream);
+}
+
+int ingot_gpu_fields_read(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_seg_off,
+                          const uint16_t* d_seg_len, const uint32_t* d_pkt_seg, uint64_t n,
+                          int chain, ingot_fields* d_out, uint16_t* d_chunk, void* stream) {
+    if (chain == INGOT_CHAIN_GENEVE_OVER_V6) return INGOT_GPU_EINVAL;  // 384-B blocks
+    return parse_segmented(ctx, d_arena, d_seg_off, d_seg_len, d_pkt_seg, n, chain, d_out,
+                           d_chunk, ingot_gpu::OUT_FIELDS, stream);
+}
+
+int ingot_gpu_geneve_fields_read(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
+                                 const uint64_t* d_seg_off, const uint16_t* d_seg_len,
+                                 const uint32_t* d_pkt_seg, uint64_t n,
+                                 ingot_geneve_fields* d_out, uint16_t* d_chunk, void* stream) {
+    return parse_segmented(ctx, d_arena, d_seg_off, d_seg_len, d_pkt_seg, n,
+                           INGOT_CHAIN_GENEVE_OVER_V6, d_out, d_chunk, ingot_gpu::OUT_FIELDS,
+                           stream);
 }
 
 int ingot_gpu_flow_hist(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,

@@ -9,7 +9,10 @@
 
 namespace ingot_gpu {
 
-enum LayoutKind { LAYOUT_STRIDED = 0, LAYOUT_INDEXED = 1 };
+// STRIDED: frame i at i*stride; INDEXED: (off[i], len[i]); SEGMENTED: packet i
+// is the chunks pkt_seg[i] .. pkt_seg[i+1] of (off, len) = (seg_off, seg_len),
+// walked with parse_read's chunk semantics.
+enum LayoutKind { LAYOUT_STRIDED = 0, LAYOUT_INDEXED = 1, LAYOUT_SEGMENTED = 2 };
 
 // Output mode: 16-B ingot_rec, 8-B ingot_rec8, 256-B ingot_fields, or the
 // flow hash + histogram.
@@ -21,11 +24,13 @@ constexpr uint32_t FLOW_INPUT_BITS = 36 * 8;
 
 struct ParseArgs {
     const uint8_t* arena;
-    const uint64_t* off;   // LAYOUT_INDEXED
-    const uint16_t* len;   // optional for LAYOUT_STRIDED
+    const uint64_t* off;   // LAYOUT_INDEXED (LAYOUT_SEGMENTED: per chunk)
+    const uint16_t* len;   // optional for LAYOUT_STRIDED (LAYOUT_SEGMENTED: per chunk)
     uint32_t stride;       // LAYOUT_STRIDED
     uint64_t n;
     void* out;             // n records of the OutMode's type
+    const uint32_t* pkt_seg = nullptr;  // LAYOUT_SEGMENTED: n+1 chunk-index bounds
+    uint16_t* chunk = nullptr;          // LAYOUT_SEGMENTED, optional: remainder's chunk
 };
 
 struct FlowArgs {

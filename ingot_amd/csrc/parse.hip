@@ -65,6 +65,7 @@ __device__ __forceinline__ uint32_t slot_of(uint32_t p, uint32_t c) {
 // One lane's view of its frame: LDS window for the first bytes, HBM beyond.
 template <uint32_t NCH>
 struct Frame {
+    static constexpr bool kRead = false;
     const lds_u32* win;  // this wave's LDS image
     uint32_t p;          // packet index within the wave (== lane)
     uint32_t sh;         // frame start inside its first staged chunk (0..15)
@@ -107,6 +108,32 @@ struct Frame {
     // Getter of a layout field of the header starting at `hdr`.
     __device__ __forceinline__ uint32_t get(uint32_t hdr, Field f) const {
         return (be(hdr + f.byte0(), f.nbytes()) >> f.rshift()) & f.mask();
+    }
+};
+
+// parse_read's view of a multi-chunk packet (parse.rs:511-537): offsets are
+// logical (the chunks concatenated); `len` is the end of the current chunk, so
+// every bounds check in the walk is a chunk bound.  Chunk 0 is staged in LDS
+// like a single frame; later chunks are read from L2/HBM.
+template <uint32_t NCH>
+struct SegFrame : Frame<NCH> {
+    static constexpr bool kRead = true;
+    const uint8_t* arena;
+    const uint64_t* seg_off;
+    const uint16_t* seg_len;
+    uint32_t s0, k, nseg;  // first chunk's index, current chunk, chunk count
+
+    // Frame::be serves reads: bytes below `avail` (chunk 0's window) from LDS,
+    // the rest through g, which advance() rebases so that g[i] is logical
+    // byte i of the current chunk.
+    __device__ __forceinline__ bool more() const { return k + 1 < nseg; }
+    // next_chunk(): the next chunk starts at logical offset `len`.
+    __device__ __forceinline__ void advance() {
+        ++k;
+        const uint32_t l = seg_len[s0 + k];
+        this->g = arena + seg_off[s0 + k] - this->len;
+        const uint32_t e = this->len + l;
+        this->len = e > 65535u ? 65535u : e;  // record offsets are u16
     }
 };
 
@@ -214,22 +241,47 @@ __device__ __forceinline__ bool v6_ext_chain(const FR& f, uint32_t len, uint32_t
 // Layer indices are the chain's PacketParseError labels (parse.rs:36-50).
 // F: the (inner) frame's getters; T: the tunnel's outer getters (FIELDS only).
 // ---------------------------------------------------------------------------
+// parse_read: a layer's TooSmall is StraddledHeader when another chunk exists
+// (ParseError::convert_read_parse, error.rs:65-72).
+template <class FR>
+__device__ __forceinline__ uint32_t read_error(const FR& f, uint32_t code) {
+    if constexpr (FR::kRead) {
+        if (code == INGOT_ERR_TOO_SMALL && f.more()) return INGOT_ERR_STRADDLED_HEADER;
+    }
+    return code;
+}
+
 template <int CHAIN, bool FIELDS, class FR>
-__device__ __forceinline__ void walk(const FR& f, Rec& r, ingot_fields* F,
-                                     ingot_tunnel_fields* T) {
+__device__ __forceinline__ void walk(FR& f, Rec& r, ingot_fields* F, ingot_tunnel_fields* T) {
     constexpr bool TUN = CHAIN == INGOT_CHAIN_GENEVE_OVER_V6;
     constexpr uint32_t L_L3 = CHAIN == INGOT_CHAIN_VLAN_ULP ? 2u : TUN ? 5u : 1u;
     constexpr uint32_t L_L4 = L_L3 + 1u;
     constexpr bool ULP = CHAIN != INGOT_CHAIN_UDP_PARSER;  // Ulp vs L4 choice
-    const uint32_t len = f.len;
+    uint32_t len = f.len;  // end of the current chunk (parse_read) / of the frame
 
     r = Rec{};
     r.err_layer = 0xffu;
-#define FAIL(layer, code)          \
-    do {                           \
-        r.status = (code);         \
-        r.err_layer = (layer);     \
-        return;                    \
+#define FAIL(layer, code)                  \
+    do {                                   \
+        r.status = read_error(f, (code));  \
+        r.err_layer = (layer);             \
+        return;                            \
+    } while (0)
+    // parse_read's slice step after a non-final layer (parse.rs:205-218): an
+    // exhausted chunk is replaced by the next; none left is TooSmall here.
+#define NEXT_SLICE(layer)                              \
+    do {                                               \
+        if constexpr (FR::kRead) {                     \
+            if (p == len) {                            \
+                if (!f.more()) {                       \
+                    r.status = INGOT_ERR_TOO_SMALL;    \
+                    r.err_layer = (layer);             \
+                    return;                            \
+                }                                      \
+                f.advance();                           \
+                len = f.len;                           \
+            }                                          \
+        }                                              \
     } while (0)
 
     // -- layer 0: Ethernet (ethernet.rs:46-55); Accessor 14 B else TooSmall.
@@ -247,6 +299,7 @@ __device__ __forceinline__ void walk(const FR& f, Rec& r, ingot_fields* F,
         copy_bytes(f, 6, F->eth_source, 6);
         F->eth_ethertype = (uint16_t)et;
     }
+    if constexpr (CHAIN != INGOT_CHAIN_GENERIC_ULP) NEXT_SLICE(0u);
 
     // GeneveOverV6Tunnel's outer layers (ingot-examples/src/packets.rs:27-40).
     if constexpr (TUN) {
@@ -291,6 +344,7 @@ __device__ __forceinline__ void walk(const FR& f, Rec& r, ingot_fields* F,
         p = q;
         r.payload_off = p;
         r.l4_proto = h;
+        NEXT_SLICE(1u);
 
         // -- layer 2 outer_udp: #[ingot(from = "L4<Q>")] Udp (TCP parses, then
         // is Unwanted; anything else is Unwanted at the choice).
@@ -317,6 +371,7 @@ __device__ __forceinline__ void walk(const FR& f, Rec& r, ingot_fields* F,
         }
         p += udp::LEN;
         r.payload_off = p;
+        NEXT_SLICE(2u);
 
         // -- layer 3 outer_encap: Geneve (geneve.rs:16-44): 8 B, then options
         // split_at(opt_len*4) subparsed as Repeated<GeneveOpt>
@@ -369,6 +424,7 @@ __device__ __forceinline__ void walk(const FR& f, Rec& r, ingot_fields* F,
         }
         p += geneve::LEN + span;
         r.payload_off = p;
+        NEXT_SLICE(3u);
 
         // -- layer 4 inner_eth; from here the record describes the inner frame.
         if (len - p < eth::LEN) FAIL(4u, INGOT_ERR_TOO_SMALL);
@@ -390,8 +446,11 @@ __device__ __forceinline__ void walk(const FR& f, Rec& r, ingot_fields* F,
         // control = exit_on_arp; the Option<> sled allows Accept here.
         if (et == ET_ARP) {
             r.flags |= INGOT_REC_ACCEPTED;
+            NEXT_SLICE(4u);  // parse_read still steps past skipped layers
+            NEXT_SLICE(5u);
             return;
         }
+        NEXT_SLICE(4u);
     }
 
     // GenericUlp: control = exit_on_arp on inner_eth (packets.rs:45-51); the
@@ -399,8 +458,11 @@ __device__ __forceinline__ void walk(const FR& f, Rec& r, ingot_fields* F,
     if constexpr (CHAIN == INGOT_CHAIN_GENERIC_ULP) {
         if (et == ET_ARP) {
             r.flags = INGOT_REC_ACCEPTED;
+            NEXT_SLICE(0u);  // parse_read still steps past skipped layers
+            NEXT_SLICE(1u);
             return;
         }
+        NEXT_SLICE(0u);
     }
 
     // -- build-defined VLAN layer: up to two VlanBody tags (ethernet.rs:57-65).
@@ -418,6 +480,7 @@ __device__ __forceinline__ void walk(const FR& f, Rec& r, ingot_fields* F,
             r.n_vlan = v + 1u;
             r.payload_off = p;
             r.ethertype = et;
+            NEXT_SLICE(1u);
         }
     }
 
@@ -486,6 +549,7 @@ __device__ __forceinline__ void walk(const FR& f, Rec& r, ingot_fields* F,
     }
     r.payload_off = p;
     r.l4_proto = proto;
+    NEXT_SLICE(L_L3);
 
     // -- L4 choice (choices.rs:25-29) / Ulp choice (choices.rs:32-38).
     uint32_t kind;
@@ -542,6 +606,7 @@ __device__ __forceinline__ void walk(const FR& f, Rec& r, ingot_fields* F,
         if (kind != INGOT_L4_UDP) FAIL(L_L4, INGOT_ERR_UNWANTED);
     }
 #undef FAIL
+#undef NEXT_SLICE
 }
 
 // ---------------------------------------------------------------------------
@@ -627,7 +692,14 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
         const bool valid = i < a.n;
         uint64_t off;
         uint32_t len;
-        if constexpr (LAYOUT == LAYOUT_STRIDED) {
+        uint32_t s0 = 0, nseg = 0;
+        if constexpr (LAYOUT == LAYOUT_SEGMENTED) {
+            // chunk 0 is staged like a frame; the rest is read on demand
+            s0 = valid ? a.pkt_seg[i] : 0u;
+            nseg = valid ? a.pkt_seg[i + 1] - s0 : 0u;
+            off = nseg ? a.off[s0] : 0u;
+            len = nseg ? (uint32_t)a.len[s0] : 0u;
+        } else if constexpr (LAYOUT == LAYOUT_STRIDED) {
             off = i * a.stride;
             len = valid ? (a.len ? (uint32_t)a.len[i] : a.stride) : 0u;
             if (len > a.stride) len = a.stride;  // a slot holds at most one frame
@@ -662,7 +734,23 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-        Frame<NCH> fr{(const lds_u32*)wimg, lane, sh, take, len, a.arena + off};
+        using FR = typename std::conditional<LAYOUT == LAYOUT_SEGMENTED, SegFrame<NCH>,
+                                             Frame<NCH>>::type;
+        FR fr;
+        fr.win = (const lds_u32*)wimg;
+        fr.p = lane;
+        fr.sh = sh;
+        fr.avail = take;
+        fr.len = len;
+        fr.g = a.arena + off;
+        if constexpr (LAYOUT == LAYOUT_SEGMENTED) {
+            fr.arena = a.arena;
+            fr.seg_off = a.off;
+            fr.seg_len = a.len;
+            fr.s0 = s0;
+            fr.k = 0;
+            fr.nseg = nseg;
+        }
         Rec r;
         if constexpr (MODE == OUT_FIELDS) {
             // ingot_fields, or ingot_geneve_fields (inner + outer) for the tunnel.
@@ -697,6 +785,9 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
         } else {
             walk<CHAIN, false>(fr, r, nullptr, nullptr);
             if (valid) static_cast<uint4*>(a.out)[i] = pack(r);
+        }
+        if constexpr (LAYOUT == LAYOUT_SEGMENTED) {
+            if (valid && a.chunk) a.chunk[i] = (uint16_t)fr.k;
         }
         // The next tile's LDS-DMA overwrites this image: every lane's reads
         // above have returned (their values were consumed by the store).
@@ -756,6 +847,13 @@ hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, int mode
                         const Tuning& t, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
     const uint32_t g = grid_for(a.n, t.max_blocks);
+    // parse_read over chunk lists: chunk 0 staged in a 4-chunk (64-B) window
+    // (first mblk-style chunks are short header blocks), the rest from L2/HBM.
+    if (layout_kind == LAYOUT_SEGMENTED) {
+        if (mode == OUT_FIELDS) return launch_chain<4, LAYOUT_SEGMENTED, OUT_FIELDS>(a, chain, g, s);
+        if (mode == OUT_REC16) return launch_chain<4, LAYOUT_SEGMENTED, OUT_REC16>(a, chain, g, s);
+        return hipErrorInvalidValue;
+    }
     // Staged window (16-B chunks per frame); defaults measured on MI355X with
     // interleaved A/B in one process (tools/abtune.py):
     //  * packed frames: 3 chunks (C3 595-598 us/step at 2-3 chunks, 614 at 4,
