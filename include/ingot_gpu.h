@@ -448,6 +448,68 @@ int ingot_gpu_geneve_fields_read(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
                                  ingot_geneve_fields* d_out, uint16_t* d_chunk,
                                  void* stream);
 
+/* ---------------------------------------------------------------------------
+ * In-place header rewrite: ingot's generated setters (packet/mod.rs:2097-2255;
+ * BE bitfield set paths, bitfield.rs:188-315) after the parse, e.g. the
+ * reference's `parse-and-decr-v4` bench (ingot-examples/benches/packet.rs:
+ * 139-145: l4.set_destination(l4.destination() - 1)).
+ *
+ * Every packet is parsed as `chain`; for packets that parse Ok the edits are
+ * applied in order, each to the header at chain layer `layer` (the label
+ * index: UdpParser 0 eth, 1 l3, 2 l4; GenericUlp 0-2; VlanUlp 0 eth, 1 vlan
+ * (tag `index`), 2 l3, 3 l4; GeneveOverV6Tunnel 0-6) when that layer holds
+ * the header kind the field belongs to (an IPv4 field on an IPv6 layer, or
+ * on a layer skipped by an accepting control, is not applied).  Values are
+ * the raw wire bits (NetworkRepr::to_network already applied, e.g. Ecn
+ * Capable1 = 2); ADD/SUB wrap modulo 2^width; the neighbouring bits of a
+ * bitfield are preserved.  Offsets come from the one parse: an edit never
+ * re-parses (as in ingot, setting ihl does not move the L4 view).
+ * ------------------------------------------------------------------------- */
+enum ingot_field {
+    INGOT_F_ETH_ETHERTYPE = 0,
+    INGOT_F_VLAN_PRIORITY, INGOT_F_VLAN_DEI, INGOT_F_VLAN_VID, INGOT_F_VLAN_ETHERTYPE,
+    INGOT_F_V4_VERSION, INGOT_F_V4_IHL, INGOT_F_V4_DSCP, INGOT_F_V4_ECN, INGOT_F_V4_TOTAL_LEN,
+    INGOT_F_V4_IDENTIFICATION, INGOT_F_V4_FLAGS, INGOT_F_V4_FRAGMENT_OFFSET,
+    INGOT_F_V4_HOP_LIMIT, INGOT_F_V4_PROTOCOL, INGOT_F_V4_CHECKSUM, INGOT_F_V4_SOURCE,
+    INGOT_F_V4_DESTINATION,
+    INGOT_F_V6_VERSION, INGOT_F_V6_DSCP, INGOT_F_V6_ECN, INGOT_F_V6_FLOW_LABEL,
+    INGOT_F_V6_PAYLOAD_LEN, INGOT_F_V6_NEXT_HEADER, INGOT_F_V6_HOP_LIMIT,
+    INGOT_F_TCP_SOURCE, INGOT_F_TCP_DESTINATION, INGOT_F_TCP_SEQUENCE,
+    INGOT_F_TCP_ACKNOWLEDGEMENT, INGOT_F_TCP_DATA_OFFSET, INGOT_F_TCP_RESERVED,
+    INGOT_F_TCP_FLAGS, INGOT_F_TCP_WINDOW_SIZE, INGOT_F_TCP_CHECKSUM, INGOT_F_TCP_URGENT_PTR,
+    INGOT_F_UDP_SOURCE, INGOT_F_UDP_DESTINATION, INGOT_F_UDP_LENGTH, INGOT_F_UDP_CHECKSUM,
+    INGOT_F_ICMP_TY, INGOT_F_ICMP_CODE, INGOT_F_ICMP_CHECKSUM,
+    INGOT_F_GENEVE_VERSION, INGOT_F_GENEVE_OPT_LEN, INGOT_F_GENEVE_FLAGS,
+    INGOT_F_GENEVE_PROTOCOL_TYPE, INGOT_F_GENEVE_VNI, INGOT_F_GENEVE_RESERVED,
+    INGOT_F_COUNT
+};
+enum ingot_edit_op {
+    INGOT_OP_SET = 0, INGOT_OP_ADD = 1, INGOT_OP_SUB = 2, INGOT_OP_AND = 3, INGOT_OP_OR = 4,
+    INGOT_OP_XOR = 5
+};
+#define INGOT_MAX_EDITS 16
+
+typedef struct ingot_edit {
+    uint8_t layer;   /* chain layer index (label) */
+    uint8_t field;   /* enum ingot_field */
+    uint8_t op;      /* enum ingot_edit_op */
+    uint8_t index;   /* VLAN tag (VLAN_ULP's vlan layer), else 0 */
+    uint32_t value;  /* raw wire bits */
+} ingot_edit;
+
+#ifdef __cplusplus
+static_assert(sizeof(ingot_edit) == 8, "ingot_edit is 8 bytes");
+#endif
+
+/* Parse + rewrite in place.  `edits` is host memory (<= INGOT_MAX_EDITS);
+ * d_out (optional) receives the parse records.  d_off == NULL selects the
+ * strided layout (as ingot_gpu_fields). */
+int ingot_gpu_parse_modify(ingot_gpu_ctx* ctx, uint8_t* d_arena,
+                           const uint64_t* d_off, const uint16_t* d_len,
+                           uint32_t stride, uint64_t n, int chain,
+                           const ingot_edit* edits, uint32_t n_edits,
+                           ingot_rec* d_out, void* stream);
+
 /*
  * Flow classification + per-flow histogram (config 5; build-defined, ingot
  * has no flow hash).  For every packet that parses Ok as `chain` with an

@@ -42,7 +42,10 @@ from .abi import (  # noqa: F401  (re-exports)
     IngotRec8,
     L3Kind,
     L4Kind,
+    EditOp,
+    Field,
     ParseError,
+    edits_array,
     rec16_to_rec8,
 )
 
@@ -235,6 +238,22 @@ class Context:
                                                         _stream(stream))
         _lib.check(rc, "ingot_gpu_parse_read")
         return out, chunk
+
+    def parse_modify(self, arena, off, lens, chain: Chain, edits, stride: int = 0,
+                     n: Optional[int] = None, out=None, stream=None):
+        """Parse, then rewrite header fields in place (ingot's setters):
+        edits = [(layer, Field, EditOp, value[, vlan index]), ...] applied in
+        order to packets that parse Ok.  Returns the parse records if `out`
+        (an (n, 16) uint8 tensor) is given, else None."""
+        if n is None:
+            n = off.numel()
+        self._check_dev(arena, off, lens, out)
+        e = edits_array(edits)
+        _lib.check(self._lib.ingot_gpu_parse_modify(
+            self._h, _ptr(arena), _ptr(off), _ptr(lens), int(stride), n, int(chain),
+            e.ctypes.data_as(ctypes.c_void_p), len(e), _ptr(out), _stream(stream)),
+            "ingot_gpu_parse_modify")
+        return out
 
     def flow_hist(self, arena, off, lens, chain: Chain, hist=None, bins: Optional[int] = None,
                   stride: int = 0, n: Optional[int] = None, key: Optional[bytes] = None,

@@ -268,6 +268,48 @@ def rec16_to_rec8(rec: np.ndarray) -> np.ndarray:
 FIELDS_BYTES = FIELDS_DTYPE.itemsize
 
 
+_FIELD_NAMES = """ETH_ETHERTYPE VLAN_PRIORITY VLAN_DEI VLAN_VID VLAN_ETHERTYPE
+V4_VERSION V4_IHL V4_DSCP V4_ECN V4_TOTAL_LEN V4_IDENTIFICATION V4_FLAGS V4_FRAGMENT_OFFSET
+V4_HOP_LIMIT V4_PROTOCOL V4_CHECKSUM V4_SOURCE V4_DESTINATION
+V6_VERSION V6_DSCP V6_ECN V6_FLOW_LABEL V6_PAYLOAD_LEN V6_NEXT_HEADER V6_HOP_LIMIT
+TCP_SOURCE TCP_DESTINATION TCP_SEQUENCE TCP_ACKNOWLEDGEMENT TCP_DATA_OFFSET TCP_RESERVED
+TCP_FLAGS TCP_WINDOW_SIZE TCP_CHECKSUM TCP_URGENT_PTR
+UDP_SOURCE UDP_DESTINATION UDP_LENGTH UDP_CHECKSUM ICMP_TY ICMP_CODE ICMP_CHECKSUM
+GENEVE_VERSION GENEVE_OPT_LEN GENEVE_FLAGS GENEVE_PROTOCOL_TYPE GENEVE_VNI
+GENEVE_RESERVED""".split()
+# enum ingot_field (include/ingot_gpu.h): setter targets of ingot_gpu_parse_modify
+Field = enum.IntEnum("Field", [(n, i) for i, n in enumerate(_FIELD_NAMES)])
+
+
+class EditOp(enum.IntEnum):
+    SET = 0
+    ADD = 1
+    SUB = 2
+    AND = 3
+    OR = 4
+    XOR = 5
+
+
+MAX_EDITS = 16
+
+
+class IngotEdit(ctypes.Structure):
+    _fields_ = [("layer", U8), ("field", U8), ("op", U8), ("index", U8), ("value", U32)]
+
+
+assert ctypes.sizeof(IngotEdit) == 8
+EDIT_DTYPE = np.dtype(IngotEdit)
+
+
+def edits_array(edits) -> np.ndarray:
+    """[(layer, Field, EditOp, value[, index]), ...] -> ingot_edit array."""
+    a = np.zeros(len(edits), dtype=EDIT_DTYPE)
+    for k, e in enumerate(edits):
+        a[k]["layer"], a[k]["field"], a[k]["op"], a[k]["value"] = e[0], int(e[1]), int(e[2]), e[3]
+        a[k]["index"] = e[4] if len(e) > 4 else 0
+    return a
+
+
 class GenProfile(enum.IntEnum):
     """Synthetic traffic profiles (include/ingot_pktgen.h)."""
 

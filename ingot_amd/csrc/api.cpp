@@ -77,6 +77,38 @@ int parse_strided(ingot_gpu_ctx* ctx, const uint8_t* d_arena, uint32_t stride,
                                             ctx->tuning, (hipStream_t)stream));
 }
 
+// ingot_field -> (header kind, first bit, width): the setters' BE geometry
+// (ethernet.rs:46-65, ip.rs:63-93 / 159-182, tcp.rs:9-30, udp.rs:8-15,
+// icmp.rs:42-50, geneve.rs:16-44; layout rules packet/mod.rs:547-821).
+struct FieldGeo {
+    uint8_t kind;
+    uint16_t bit;
+    uint8_t bits;
+};
+constexpr FieldGeo kFieldGeo[INGOT_F_COUNT] = {
+    {ingot_gpu::HK_ETH, 96, 16},
+    {ingot_gpu::HK_VLAN, 0, 3},    {ingot_gpu::HK_VLAN, 3, 1},
+    {ingot_gpu::HK_VLAN, 4, 12},   {ingot_gpu::HK_VLAN, 16, 16},
+    {ingot_gpu::HK_V4, 0, 4},      {ingot_gpu::HK_V4, 4, 4},     {ingot_gpu::HK_V4, 8, 6},
+    {ingot_gpu::HK_V4, 14, 2},     {ingot_gpu::HK_V4, 16, 16},   {ingot_gpu::HK_V4, 32, 16},
+    {ingot_gpu::HK_V4, 48, 3},     {ingot_gpu::HK_V4, 51, 13},   {ingot_gpu::HK_V4, 64, 8},
+    {ingot_gpu::HK_V4, 72, 8},     {ingot_gpu::HK_V4, 80, 16},   {ingot_gpu::HK_V4, 96, 32},
+    {ingot_gpu::HK_V4, 128, 32},
+    {ingot_gpu::HK_V6, 0, 4},      {ingot_gpu::HK_V6, 4, 6},     {ingot_gpu::HK_V6, 10, 2},
+    {ingot_gpu::HK_V6, 12, 20},    {ingot_gpu::HK_V6, 32, 16},   {ingot_gpu::HK_V6, 48, 8},
+    {ingot_gpu::HK_V6, 56, 8},
+    {ingot_gpu::HK_TCP, 0, 16},    {ingot_gpu::HK_TCP, 16, 16},  {ingot_gpu::HK_TCP, 32, 32},
+    {ingot_gpu::HK_TCP, 64, 32},   {ingot_gpu::HK_TCP, 96, 4},   {ingot_gpu::HK_TCP, 100, 4},
+    {ingot_gpu::HK_TCP, 104, 8},   {ingot_gpu::HK_TCP, 112, 16}, {ingot_gpu::HK_TCP, 128, 16},
+    {ingot_gpu::HK_TCP, 144, 16},
+    {ingot_gpu::HK_UDP, 0, 16},    {ingot_gpu::HK_UDP, 16, 16},  {ingot_gpu::HK_UDP, 32, 16},
+    {ingot_gpu::HK_UDP, 48, 16},
+    {ingot_gpu::HK_ICMP, 0, 8},    {ingot_gpu::HK_ICMP, 8, 8},   {ingot_gpu::HK_ICMP, 16, 16},
+    {ingot_gpu::HK_GENEVE, 0, 2},  {ingot_gpu::HK_GENEVE, 2, 6}, {ingot_gpu::HK_GENEVE, 8, 8},
+    {ingot_gpu::HK_GENEVE, 16, 16}, {ingot_gpu::HK_GENEVE, 32, 24},
+    {ingot_gpu::HK_GENEVE, 56, 8},
+};
+
 int parse_segmented(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_seg_off,
                     const uint16_t* d_seg_len, const uint32_t* d_pkt_seg, uint64_t n, int chain,
                     void* d_out, uint16_t* d_chunk, int mode, void* stream) {
@@ -214,6 +246,45 @@ int ingot_gpu_geneve_fields_read(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
     return parse_segmented(ctx, d_arena, d_seg_off, d_seg_len, d_pkt_seg, n,
                            INGOT_CHAIN_GENEVE_OVER_V6, d_out, d_chunk, ingot_gpu::OUT_FIELDS,
                            stream);
+}
+
+int ingot_gpu_parse_modify(ingot_gpu_ctx* ctx, uint8_t* d_arena, const uint64_t* d_off,
+                           const uint16_t* d_len, uint32_t stride, uint64_t n, int chain,
+                           const ingot_edit* edits, uint32_t n_edits, ingot_rec* d_out,
+                           void* stream) {
+    if (!ctx || !chain_ok(chain) || n_edits > INGOT_MAX_EDITS || (n_edits && !edits))
+        return INGOT_GPU_EINVAL;
+    ingot_gpu::ModifyArgs a{};
+    for (uint32_t k = 0; k < n_edits; ++k) {
+        const ingot_edit& e = edits[k];
+        if (e.field >= INGOT_F_COUNT || e.op > INGOT_OP_XOR ||
+            (int)e.layer >= ingot_chain_layer_count(chain))
+            return INGOT_GPU_EINVAL;
+        const FieldGeo g = kFieldGeo[e.field];
+        ingot_gpu::Edit& d = a.e[k];
+        d.layer = e.layer;
+        d.kind = g.kind;
+        d.op = e.op;
+        d.index = e.index;
+        d.byte0 = (uint8_t)(g.bit / 8u);
+        d.nbytes = (uint8_t)((g.bit % 8u + g.bits + 7u) / 8u);
+        d.rshift = (uint8_t)((8u - ((g.bit + g.bits) % 8u)) % 8u);
+        d.bits = g.bits;
+        d.value = e.value;
+    }
+    a.n_edits = n_edits;
+    if (n == 0) return INGOT_GPU_SUCCESS;
+    if (!d_arena) return INGOT_GPU_EINVAL;
+    int layout = ingot_gpu::LAYOUT_INDEXED;
+    if (!d_off) {
+        if (int e = stride_ok(d_arena, stride)) return e;
+        layout = ingot_gpu::LAYOUT_STRIDED;
+    } else if (!d_len) {
+        return INGOT_GPU_EINVAL;
+    }
+    if (int e = enter(ctx)) return e;
+    a.p = ingot_gpu::ParseArgs{d_arena, d_off, d_len, stride, n, d_out};
+    return from_hip(ingot_gpu::launch_modify(a, layout, chain, ctx->tuning, (hipStream_t)stream));
 }
 
 int ingot_gpu_flow_hist(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,

@@ -16,7 +16,7 @@ enum LayoutKind { LAYOUT_STRIDED = 0, LAYOUT_INDEXED = 1, LAYOUT_SEGMENTED = 2 }
 
 // Output mode: 16-B ingot_rec, 8-B ingot_rec8, 256-B ingot_fields, or the
 // flow hash + histogram.
-enum OutMode { OUT_REC16 = 0, OUT_REC8 = 1, OUT_FIELDS = 2, OUT_FLOWS = 3 };
+enum OutMode { OUT_REC16 = 0, OUT_REC8 = 1, OUT_FIELDS = 2, OUT_FLOWS = 3, OUT_MODIFY = 4 };
 
 // Toeplitz key windows: w[b] = the 32 key bits starting at input bit b, for
 // every bit of the longest input (IPv6 src|dst|ports = 36 bytes).
@@ -41,6 +41,19 @@ struct FlowArgs {
     uint32_t w[FLOW_INPUT_BITS];
 };
 
+// In-place rewrite (ingot_gpu_parse_modify): api.cpp resolves each ingot_edit's
+// field to its header kind and BE bit geometry, so the kernel needs no tables.
+enum HdrKind : uint8_t { HK_ETH, HK_VLAN, HK_V4, HK_V6, HK_TCP, HK_UDP, HK_ICMP, HK_GENEVE };
+struct Edit {
+    uint8_t layer, kind, op, index;
+    uint8_t byte0, nbytes, rshift, bits;  // field bytes [byte0, byte0+nbytes) of the header
+    uint32_t value;
+};
+struct ModifyArgs {
+    ParseArgs p;
+    uint32_t n_edits;
+    Edit e[INGOT_MAX_EDITS];
+};
 // Histogram pass over flow bins (flow.hip).
 hipError_t launch_flow_hist(const uint32_t* flow, uint64_t n, uint32_t* hist, uint32_t bins,
                             hipStream_t s);
@@ -56,6 +69,8 @@ hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, int mode
                         const Tuning& t, hipStream_t s);
 hipError_t launch_flows(const FlowArgs& a, int layout_kind, int chain, const Tuning& t,
                         hipStream_t s);
+hipError_t launch_modify(const ModifyArgs& a, int layout_kind, int chain, const Tuning& t,
+                         hipStream_t s);
 bool tuning_valid(int key, int value);
 
 }  // namespace ingot_gpu

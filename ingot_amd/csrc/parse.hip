@@ -140,6 +140,7 @@ struct SegFrame : Frame<NCH> {
 struct Rec {
     uint32_t status, err_layer, l3_kind, l4_kind, n_vlan, n_v6ext, l4_proto, flags;
     uint32_t l3_off, l4_off, payload_off, ethertype;
+    uint32_t o_udp, o_gen, i_eth;  // tunnel: outer_udp / outer_encap / inner_eth offsets
 };
 
 __device__ __forceinline__ uint2 pack8(const Rec& r) {
@@ -361,6 +362,7 @@ __device__ __forceinline__ void walk(FR& f, Rec& r, ingot_fields* F, ingot_tunne
         if (h != IPP_UDP) FAIL(2u, INGOT_ERR_UNWANTED);
         r.l4_kind = INGOT_L4_UDP;
         r.l4_off = p;
+        r.o_udp = p;
         if (len - p < udp::LEN) FAIL(2u, INGOT_ERR_TOO_SMALL);
         if constexpr (FIELDS) {
             T->outer_udp_off = (uint16_t)p;
@@ -377,6 +379,7 @@ __device__ __forceinline__ void walk(FR& f, Rec& r, ingot_fields* F, ingot_tunne
         // split_at(opt_len*4) subparsed as Repeated<GeneveOpt>
         // (mod.rs:1940-1957, util.rs:199-216); an option overrunning the span
         // is TooSmall (GeneveOpt never returns Unwanted).
+        r.o_gen = p;
         if (len - p < geneve::LEN) FAIL(3u, INGOT_ERR_TOO_SMALL);
         const uint32_t g0 = f.be(p, 4);  // version | opt_len | flags | protocol_type
         const uint32_t span = ((g0 >> 24) & 0x3fu) * 4u;
@@ -427,6 +430,7 @@ __device__ __forceinline__ void walk(FR& f, Rec& r, ingot_fields* F, ingot_tunne
         NEXT_SLICE(3u);
 
         // -- layer 4 inner_eth; from here the record describes the inner frame.
+        r.i_eth = p;
         if (len - p < eth::LEN) FAIL(4u, INGOT_ERR_TOO_SMALL);
         et = f.get(p, eth::ethertype);
         if constexpr (FIELDS) {
@@ -614,6 +618,70 @@ __device__ __forceinline__ void walk(FR& f, Rec& r, ingot_fields* F, ingot_tunne
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ const ParseArgs& base_args(const ParseArgs& a) { return a; }
 __device__ __forceinline__ const ParseArgs& base_args(const FlowArgs& a) { return a.p; }
+__device__ __forceinline__ const ParseArgs& base_args(const ModifyArgs& a) { return a.p; }
+
+// The header at chain layer `layer` of a parsed-Ok record, if it is of `kind`.
+template <int CHAIN>
+__device__ __forceinline__ bool header_at(const Rec& r, uint32_t layer, uint32_t kind,
+                                          uint32_t index, uint32_t& h) {
+    const uint32_t k3 = r.l3_kind == INGOT_L3_IPV4 ? HK_V4 : r.l3_kind == INGOT_L3_IPV6 ? HK_V6
+                                                                                      : 0xffu;
+    const uint32_t k4 = r.l4_kind == INGOT_L4_TCP   ? HK_TCP
+                        : r.l4_kind == INGOT_L4_UDP ? HK_UDP
+                        : r.l4_kind != INGOT_L4_NONE ? HK_ICMP
+                                                     : 0xffu;
+    uint32_t have = 0xffu;
+    h = 0;
+    if constexpr (CHAIN == INGOT_CHAIN_GENEVE_OVER_V6) {
+        switch (layer) {
+        case 0: have = HK_ETH; break;
+        case 1: have = HK_V6; h = eth::LEN; break;
+        case 2: have = HK_UDP; h = r.o_udp; break;
+        case 3: have = HK_GENEVE; h = r.o_gen; break;
+        case 4: have = HK_ETH; h = r.i_eth; break;
+        case 5: have = k3; h = r.l3_off; break;
+        case 6: have = k4; h = r.l4_off; break;
+        }
+    } else if constexpr (CHAIN == INGOT_CHAIN_VLAN_ULP) {
+        switch (layer) {
+        case 0: have = HK_ETH; break;
+        case 1:
+            if (index < r.n_vlan) have = HK_VLAN;
+            h = eth::LEN + vlan::LEN * index;
+            break;
+        case 2: have = k3; h = r.l3_off; break;
+        case 3: have = k4; h = r.l4_off; break;
+        }
+    } else {
+        switch (layer) {
+        case 0: have = HK_ETH; break;
+        case 1: have = k3; h = r.l3_off; break;
+        case 2: have = k4; h = r.l4_off; break;
+        }
+    }
+    return have == kind;
+}
+
+// One generated setter: read-modify-write of the field's covering bytes,
+// neighbouring bits preserved (bitfield.rs:188-315), big-endian.
+__device__ __forceinline__ void apply_edit(uint8_t* hdr, const Edit& e) {
+    uint64_t w = 0;
+    for (uint32_t k = 0; k < e.nbytes; ++k) w = (w << 8) | hdr[e.byte0 + k];
+    const uint32_t fm = e.bits >= 32 ? 0xffffffffu : ((1u << e.bits) - 1u);
+    const uint32_t cur = (uint32_t)(w >> e.rshift) & fm;
+    uint32_t v;
+    switch (e.op) {
+    case INGOT_OP_ADD: v = cur + e.value; break;
+    case INGOT_OP_SUB: v = cur - e.value; break;
+    case INGOT_OP_AND: v = cur & e.value; break;
+    case INGOT_OP_OR: v = cur | e.value; break;
+    case INGOT_OP_XOR: v = cur ^ e.value; break;
+    default: v = e.value; break;
+    }
+    w = (w & ~((uint64_t)fm << e.rshift)) | ((uint64_t)(v & fm) << e.rshift);
+    for (uint32_t k = 0; k < e.nbytes; ++k)
+        hdr[e.byte0 + k] = (uint8_t)(w >> (8u * (e.nbytes - 1u - k)));
+}
 
 // RSS Toeplitz over one 32-bit input word (MSB first) whose first bit is
 // input bit B: XOR in the key window W[B + k] for every set bit k.  W is
@@ -774,6 +842,19 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
         } else if constexpr (MODE == OUT_REC8) {
             walk<CHAIN, false>(fr, r, nullptr, nullptr);
             if (valid) static_cast<uint2*>(a.out)[i] = pack8(r);
+        } else if constexpr (MODE == OUT_MODIFY) {
+            // parse, then the setters in order on the frame in HBM (bytes are
+            // re-read there, so an edit sees the previous edits' results)
+            walk<CHAIN, false>(fr, r, nullptr, nullptr);
+            if (valid && r.status == INGOT_OK) {
+                uint8_t* frame = const_cast<uint8_t*>(a.arena) + off;
+                for (uint32_t k = 0; k < args.n_edits; ++k) {
+                    const Edit e = args.e[k];
+                    uint32_t h;
+                    if (header_at<CHAIN>(r, e.layer, e.kind, e.index, h)) apply_edit(frame + h, e);
+                }
+            }
+            if (valid && a.out) static_cast<uint4*>(a.out)[i] = pack(r);
         } else if constexpr (MODE == OUT_FLOWS) {
             walk<CHAIN, false>(fr, r, nullptr, nullptr);
             uint32_t h;
@@ -884,6 +965,21 @@ hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, int mode
     case 9: return launch_mode<9, LAYOUT_INDEXED>(a, chain, mode, g, s);
     default: return launch_mode<5, LAYOUT_INDEXED>(a, chain, mode, g, s);
     }
+}
+
+// Parse + rewrite: the default windows of the record path.
+hipError_t launch_modify(const ModifyArgs& a, int layout_kind, int chain, const Tuning& t,
+                         hipStream_t s) {
+    if (a.p.n == 0) return hipSuccess;
+    const uint32_t g = grid_for(a.p.n, t.max_blocks);
+    const bool tun = chain == INGOT_CHAIN_GENEVE_OVER_V6;
+    if (layout_kind == LAYOUT_STRIDED) {
+        if (tun) return launch_chain<8, LAYOUT_STRIDED, OUT_MODIFY>(a, chain, g, s);
+        return a.p.stride <= 64u ? launch_chain<4, LAYOUT_STRIDED, OUT_MODIFY>(a, chain, g, s)
+                                 : launch_chain<3, LAYOUT_STRIDED, OUT_MODIFY>(a, chain, g, s);
+    }
+    return tun ? launch_chain<8, LAYOUT_INDEXED, OUT_MODIFY>(a, chain, g, s)
+               : launch_chain<3, LAYOUT_INDEXED, OUT_MODIFY>(a, chain, g, s);
 }
 
 // Flow mode needs the addresses (IPv6: 32 bytes past byte 22) and ports, so

@@ -14,7 +14,8 @@ from pathlib import Path
 
 import numpy as np
 
-from ingot_amd.abi import FIELDS_DTYPE, GENEVE_FIELDS_DTYPE, REC_DTYPE, Chain  # ABI layouts only
+from ingot_amd.abi import (FIELDS_DTYPE, GENEVE_FIELDS_DTYPE, REC_DTYPE, Chain,  # ABI layouts only
+                           edits_array)
 
 HERE = Path(__file__).resolve().parent
 LIB_PATH = HERE / "build" / "libingot_oracle.so"
@@ -176,6 +177,43 @@ def parse_read(chunks, chain: Chain, fields: str | None = None):
     """One packet given as a list of chunks -> (record, fields, chunk index)."""
     rec, f, ch = parse_read_batch(*segments([chunks]), chain, fields=fields)
     return rec[0], (None if f is None else f[0]), int(ch[0])
+
+
+def be_set_bits(hdr: bytes, first_bit: int, n_bits: int, value: int) -> bytes:
+    lib = load()
+    lib.oracle_be_set_bits.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                       ctypes.c_uint64]
+    buf = np.frombuffer(bytes(hdr), dtype=np.uint8).copy()
+    lib.oracle_be_set_bits(_p(buf), first_bit, n_bits, value)
+    return buf.tobytes()
+
+
+def parse_modify_batch(arena: np.ndarray, off, lens, chain: Chain, edits, stride: int = 0,
+                       n: int | None = None):
+    """In place on `arena` (numpy u8); returns the parse records."""
+    lib = load()
+    lib.oracle_parse_modify_batch.argtypes = [ctypes.c_void_p] * 3 + [
+        ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32,
+        ctypes.c_void_p]
+    if off is not None:
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        n = len(off) if n is None else n
+    if lens is not None:
+        lens = np.ascontiguousarray(lens, dtype=np.uint16)
+    e = edits_array(edits)
+    rec = np.zeros(n, dtype=REC_DTYPE)
+    if lib.oracle_parse_modify_batch(_p(arena), _p(off), _p(lens), stride, n, int(chain), _p(e),
+                                     len(e), _p(rec)) != 0:
+        raise ValueError("oracle_parse_modify_batch: bad arguments")
+    return rec
+
+
+def parse_modify(frame: bytes, chain: Chain, edits):
+    """-> (rewritten frame bytes, record)."""
+    buf = np.frombuffer(bytes(frame) + bytes(8), dtype=np.uint8).copy()
+    rec = parse_modify_batch(buf, np.array([0], dtype=np.uint64),
+                             np.array([len(frame)], dtype=np.uint16), chain, edits)
+    return buf[:len(frame)].tobytes(), rec[0]
 
 
 def be_bits(hdr: bytes, first_bit: int, n_bits: int) -> int:

@@ -743,6 +743,132 @@ int oracle_geneve_fields_batch(const uint8_t* arena, const uint64_t* off, const 
 }
 
 /* ------------------------------------------------------------------------
+ * Setters (packet/mod.rs:2097-2255; BE bitfield set paths bitfield.rs:188-315):
+ * write n_bits at first_bit, MSB first, leaving every other bit of the
+ * covering bytes unchanged.
+ * ---------------------------------------------------------------------- */
+void oracle_be_set_bits(uint8_t* hdr, uint32_t first_bit, uint32_t n_bits, uint64_t value) {
+    for (uint32_t k = 0; k < n_bits; ++k) {
+        const uint32_t bit = first_bit + k;                   /* MSB-first position */
+        const uint64_t v = (value >> (n_bits - 1u - k)) & 1u;  /* k-th bit from the top */
+        const uint8_t m = (uint8_t)(0x80u >> (bit % 8u));
+        hdr[bit / 8u] = (uint8_t)(v ? (hdr[bit / 8u] | m) : (hdr[bit / 8u] & ~m));
+    }
+}
+
+/* ingot_field -> (header kind, first bit, width), restated from the header
+ * declarations (ethernet.rs:46-65, ip.rs:63-93, 159-182, tcp.rs:9-30,
+ * udp.rs:8-15, icmp.rs:42-50, geneve.rs:16-44). */
+enum { HK_ETH, HK_VLAN, HK_V4, HK_V6, HK_TCP, HK_UDP, HK_ICMP, HK_GENEVE };
+static const struct { uint8_t kind; uint16_t bit; uint8_t bits; } FIELD_GEO[INGOT_F_COUNT] = {
+    [INGOT_F_ETH_ETHERTYPE] = {HK_ETH, 96, 16},
+    [INGOT_F_VLAN_PRIORITY] = {HK_VLAN, VLAN_PRIORITY}, [INGOT_F_VLAN_DEI] = {HK_VLAN, VLAN_DEI},
+    [INGOT_F_VLAN_VID] = {HK_VLAN, VLAN_VID}, [INGOT_F_VLAN_ETHERTYPE] = {HK_VLAN, VLAN_ETHERTYPE},
+    [INGOT_F_V4_VERSION] = {HK_V4, V4_VERSION}, [INGOT_F_V4_IHL] = {HK_V4, V4_IHL},
+    [INGOT_F_V4_DSCP] = {HK_V4, V4_DSCP}, [INGOT_F_V4_ECN] = {HK_V4, V4_ECN},
+    [INGOT_F_V4_TOTAL_LEN] = {HK_V4, V4_TOTAL_LEN}, [INGOT_F_V4_IDENTIFICATION] = {HK_V4, V4_IDENT},
+    [INGOT_F_V4_FLAGS] = {HK_V4, V4_FLAGS}, [INGOT_F_V4_FRAGMENT_OFFSET] = {HK_V4, V4_FRAG_OFF},
+    [INGOT_F_V4_HOP_LIMIT] = {HK_V4, V4_HOP_LIMIT}, [INGOT_F_V4_PROTOCOL] = {HK_V4, V4_PROTOCOL},
+    [INGOT_F_V4_CHECKSUM] = {HK_V4, V4_CHECKSUM}, [INGOT_F_V4_SOURCE] = {HK_V4, 96, 32},
+    [INGOT_F_V4_DESTINATION] = {HK_V4, 128, 32},
+    [INGOT_F_V6_VERSION] = {HK_V6, V6_VERSION}, [INGOT_F_V6_DSCP] = {HK_V6, V6_DSCP},
+    [INGOT_F_V6_ECN] = {HK_V6, V6_ECN}, [INGOT_F_V6_FLOW_LABEL] = {HK_V6, V6_FLOW},
+    [INGOT_F_V6_PAYLOAD_LEN] = {HK_V6, V6_PAYLOAD_LEN},
+    [INGOT_F_V6_NEXT_HEADER] = {HK_V6, V6_NEXT_HEADER}, [INGOT_F_V6_HOP_LIMIT] = {HK_V6, V6_HOP_LIMIT},
+    [INGOT_F_TCP_SOURCE] = {HK_TCP, 0, 16}, [INGOT_F_TCP_DESTINATION] = {HK_TCP, 16, 16},
+    [INGOT_F_TCP_SEQUENCE] = {HK_TCP, 32, 32}, [INGOT_F_TCP_ACKNOWLEDGEMENT] = {HK_TCP, 64, 32},
+    [INGOT_F_TCP_DATA_OFFSET] = {HK_TCP, TCP_DATA_OFFSET}, [INGOT_F_TCP_RESERVED] = {HK_TCP, TCP_RESERVED},
+    [INGOT_F_TCP_FLAGS] = {HK_TCP, 104, 8}, [INGOT_F_TCP_WINDOW_SIZE] = {HK_TCP, 112, 16},
+    [INGOT_F_TCP_CHECKSUM] = {HK_TCP, 128, 16}, [INGOT_F_TCP_URGENT_PTR] = {HK_TCP, 144, 16},
+    [INGOT_F_UDP_SOURCE] = {HK_UDP, 0, 16}, [INGOT_F_UDP_DESTINATION] = {HK_UDP, 16, 16},
+    [INGOT_F_UDP_LENGTH] = {HK_UDP, 32, 16}, [INGOT_F_UDP_CHECKSUM] = {HK_UDP, 48, 16},
+    [INGOT_F_ICMP_TY] = {HK_ICMP, 0, 8}, [INGOT_F_ICMP_CODE] = {HK_ICMP, 8, 8},
+    [INGOT_F_ICMP_CHECKSUM] = {HK_ICMP, 16, 16},
+    [INGOT_F_GENEVE_VERSION] = {HK_GENEVE, GENEVE_VERSION},
+    [INGOT_F_GENEVE_OPT_LEN] = {HK_GENEVE, GENEVE_OPT_LEN_F},
+    [INGOT_F_GENEVE_FLAGS] = {HK_GENEVE, 8, 8}, [INGOT_F_GENEVE_PROTOCOL_TYPE] = {HK_GENEVE, 16, 16},
+    [INGOT_F_GENEVE_VNI] = {HK_GENEVE, 32, 24}, [INGOT_F_GENEVE_RESERVED] = {HK_GENEVE, 56, 8},
+};
+
+static int l3_hk(const ingot_rec* r) {
+    return r->l3_kind == INGOT_L3_IPV4 ? HK_V4 : r->l3_kind == INGOT_L3_IPV6 ? HK_V6 : -1;
+}
+static int l4_hk(const ingot_rec* r) {
+    switch (r->l4_kind) {
+    case INGOT_L4_TCP: return HK_TCP;
+    case INGOT_L4_UDP: return HK_UDP;
+    case INGOT_L4_ICMPV4: case INGOT_L4_ICMPV6: return HK_ICMP;
+    default: return -1;
+    }
+}
+
+int oracle_parse_modify(uint8_t* frame, uint32_t len, int chain, const ingot_edit* edits,
+                        uint32_t n_edits, ingot_rec* rec) {
+    ingot_geneve_fields g;
+    ingot_rec* r = &g.inner.rec;
+    if (chain == INGOT_CHAIN_GENEVE_OVER_V6) oracle_parse_geneve(frame, len, &g);
+    else parse_one(frame, len, chain, r, 0, 0);
+    if (rec) *rec = *r;
+    if (r->status != PE_OK) return 0;
+    for (uint32_t k = 0; k < n_edits; ++k) {
+        const ingot_edit* e = &edits[k];
+        if (e->field >= INGOT_F_COUNT) return -1;
+        int have = -1;
+        uint32_t h = 0;
+        const int L = e->layer;
+        if (chain == INGOT_CHAIN_GENEVE_OVER_V6) {
+            const ingot_tunnel_fields* t = &g.outer;
+            if (L == 0) have = HK_ETH;
+            else if (L == 1) { have = HK_V6; h = ETH_LEN; }
+            else if (L == 2) { have = HK_UDP; h = t->outer_udp_off; }
+            else if (L == 3) { have = HK_GENEVE; h = t->geneve_off; }
+            else if (L == 4) { have = HK_ETH; h = t->inner_eth_off; }
+            else if (L == 5) { have = l3_hk(r); h = r->l3_off; }
+            else if (L == 6) { have = l4_hk(r); h = r->l4_off; }
+        } else if (chain == INGOT_CHAIN_VLAN_ULP) {
+            if (L == 0) have = HK_ETH;
+            else if (L == 1) { if (e->index < r->n_vlan) have = HK_VLAN; h = ETH_LEN + VLAN_LEN * e->index; }
+            else if (L == 2) { have = l3_hk(r); h = r->l3_off; }
+            else if (L == 3) { have = l4_hk(r); h = r->l4_off; }
+        } else {
+            if (L == 0) have = HK_ETH;
+            else if (L == 1) { have = l3_hk(r); h = r->l3_off; }
+            else if (L == 2) { have = l4_hk(r); h = r->l4_off; }
+        }
+        if (have != FIELD_GEO[e->field].kind) continue;
+        const uint32_t bit = FIELD_GEO[e->field].bit, bits = FIELD_GEO[e->field].bits;
+        const uint64_t m = (bits >= 64) ? ~0ull : ((1ull << bits) - 1u);
+        const uint64_t cur = oracle_be_bits(frame + h, bit, bits);
+        uint64_t v;
+        switch (e->op) {
+        case INGOT_OP_SET: v = e->value; break;
+        case INGOT_OP_ADD: v = cur + e->value; break;  /* wrapping (release-mode Rust) */
+        case INGOT_OP_SUB: v = cur - e->value; break;
+        case INGOT_OP_AND: v = cur & e->value; break;
+        case INGOT_OP_OR: v = cur | e->value; break;
+        case INGOT_OP_XOR: v = cur ^ e->value; break;
+        default: return -1;
+        }
+        oracle_be_set_bits(frame + h, bit, bits, v & m);
+    }
+    return 0;
+}
+
+int oracle_parse_modify_batch(uint8_t* arena, const uint64_t* off, const uint16_t* len,
+                              uint32_t stride, uint64_t n, int chain, const ingot_edit* edits,
+                              uint32_t n_edits, ingot_rec* rec) {
+    if ((!off && stride == 0 && n) || chain < 0 || chain >= INGOT_CHAIN_COUNT) return -1;
+    for (uint64_t i = 0; i < n; ++i) {
+        uint64_t o = off ? off[i] : i * (uint64_t)stride;
+        uint32_t l = len ? len[i] : stride;
+        if (!off && l > stride) l = stride;
+        if (oracle_parse_modify(arena + o, l, chain, edits, n_edits, rec ? &rec[i] : 0) != 0)
+            return -1;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------
  * Batch driver (pthreads, static contiguous partition).
  * ---------------------------------------------------------------------- */
 typedef struct {

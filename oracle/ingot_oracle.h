@@ -58,6 +58,17 @@ int oracle_parse_batch(const uint8_t* arena, const uint64_t* off,
  * BE get paths): the n_bits (<= 64) starting at bit first_bit, MSB first. */
 uint64_t oracle_be_bits(const uint8_t* hdr, uint32_t first_bit, uint32_t n_bits);
 
+/* BE setter (bitfield.rs set paths): n_bits of value at first_bit, other bits
+ * of the covering bytes unchanged. */
+void oracle_be_set_bits(uint8_t* hdr, uint32_t first_bit, uint32_t n_bits, uint64_t value);
+
+/* ingot_gpu_parse_modify semantics on one frame / a batch (in place). */
+int oracle_parse_modify(uint8_t* frame, uint32_t len, int chain, const ingot_edit* edits,
+                        uint32_t n_edits, ingot_rec* rec);
+int oracle_parse_modify_batch(uint8_t* arena, const uint64_t* off, const uint16_t* len,
+                              uint32_t stride, uint64_t n, int chain, const ingot_edit* edits,
+                              uint32_t n_edits, ingot_rec* rec);
+
 /* IpProtocol::class (ingot/src/ip.rs:40-54): 0 = None, 1 = FragmentHeader,
  * 2 = Rfc6564. */
 int oracle_v6eh_class(uint8_t proto);

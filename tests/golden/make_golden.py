@@ -445,6 +445,91 @@ def read_kats():
     return out
 
 
+def modify_kats():
+    """In-place rewrite vectors (ingot_gpu_parse_modify): frame, chain, edits
+    [layer, field, op, value(, index)] -> the frame bytes after, written out
+    byte by byte here (not computed by the oracle)."""
+    out = []
+    # ingot-examples/benches/packet.rs:139-145 parse-and-decr-v4:
+    # l4.set_destination(l4.destination() - 1): 0x17C1 -> 0x17C0.
+    after = list(PKT_BODY_V4)
+    after[36:38] = [0x17, 0xC0]
+    out.append(dict(
+        name="parse_and_decr_v4", source="ingot-examples/benches/packet.rs:139-145",
+        chain="UdpParser", frame=hexs(PKT_BODY_V4), edits=[[2, "UDP_DESTINATION", "SUB", 1]],
+        after=hexs(after)))
+    # ingot/src/tests.rs:223-294 bitset_fields_do_not_disturb_neighbours: the
+    # four setters write the values already there; the bytes must not change.
+    f = eth(BROADCAST, MAC_ABCDEF, 0x86DD) + V6_BITSET + u16(7) + u16(9) + u16(8) + u16(0)
+    out.append(dict(
+        name="bitset_fields_do_not_disturb_neighbours_set",
+        source="ingot/src/tests.rs:223-294", chain="UdpParser", frame=hexs(f),
+        edits=[[1, "V6_VERSION", "SET", 6], [1, "V6_DSCP", "SET", 41],
+               [1, "V6_ECN", "SET", 2], [1, "V6_FLOW_LABEL", "SET", 123456]],
+        after=hexs(f), note="Ecn::Capable1.to_network() == 2 (ip.rs:120-134)"))
+    # The same header, new values: version 4 / dscp 0x3F / ecn 1 / flow 0xABCDE.
+    after = list(f)
+    after[14:18] = [0x4F, 0xDA, 0xBC, 0xDE]  # 0100 111111 01 1010 1011 1100 1101 1110
+    out.append(dict(
+        name="v6_bitfield_setters", source="ingot/src/ip.rs:159-170", chain="UdpParser",
+        frame=hexs(f), derived="bitfield layout version u4 | dscp u6 | ecn u2 | flow_label u20be",
+        edits=[[1, "V6_VERSION", "SET", 4], [1, "V6_DSCP", "SET", 0x3F],
+               [1, "V6_ECN", "SET", 1], [1, "V6_FLOW_LABEL", "SET", 0xABCDE]],
+        after=hexs(after)))
+    # OPTE-style rewrite of the tunnel frame (ingot-examples/src/tests.rs:189-268):
+    # new VNI, inner TTL - 1, inner UDP destination.
+    after = list(OPTE_IN)
+    after[66:69] = [0x12, 0x34, 0x56]
+    after[88 + 8] = 0xF0 - 1
+    after[108 + 2:108 + 4] = u16(54)
+    out.append(dict(
+        name="tunnel_rewrite", source="ingot-examples/src/tests.rs:189-268", chain="GeneveOverV6Tunnel",
+        frame=hexs(OPTE_IN), derived="setters on outer_encap / inner_l3 / inner_ulp",
+        edits=[[3, "GENEVE_VNI", "SET", 0x123456], [5, "V4_HOP_LIMIT", "SUB", 1],
+               [6, "UDP_DESTINATION", "SET", 54]],
+        after=hexs(after)))
+    # Edits whose layer does not hold the field's header, or on a packet that
+    # did not parse, change nothing.
+    out.append(dict(
+        name="rewrite_kind_mismatch", source="include/ingot_gpu.h (parse_modify)",
+        chain="UdpParser", frame=hexs(PKT_BODY_V4), derived="IPv6 / TCP fields on IPv4 / UDP layers",
+        edits=[[1, "V6_HOP_LIMIT", "SET", 1], [2, "TCP_FLAGS", "SET", 0xFF]],
+        after=hexs(PKT_BODY_V4)))
+    out.append(dict(
+        name="rewrite_on_error_is_noop", source="include/ingot_gpu.h (parse_modify)",
+        chain="UdpParser", frame=hexs(PKT_BODY_V4[:40]), derived="truncated UDP header",
+        edits=[[0, "ETH_ETHERTYPE", "SET", 0x86DD]], after=hexs(PKT_BODY_V4[:40])))
+    # Wrapping arithmetic (release-mode Rust): 0 - 1 = 0xFFFF.
+    f = list(PKT_BODY_V4)
+    f[34:36] = [0, 0]
+    after = list(f)
+    after[34:36] = [0xFF, 0xFF]
+    out.append(dict(
+        name="rewrite_wraps", source="ingot-examples/benches/packet.rs:139-145", chain="UdpParser",
+        frame=hexs(f), derived="u16 source 0 - 1", edits=[[2, "UDP_SOURCE", "SUB", 1]],
+        after=hexs(after)))
+    return out
+
+
+def setter_kats():
+    """ingot/src/tests.rs:118-164 (unaligned_bitfield_read_write, setters; BE
+    members of TestFunFields, :27-55): the set sequence, then every getter."""
+    return [dict(
+        name="unaligned_bitfield_setters", source="ingot/src/tests.rs:118-164",
+        bytes=hexs(FUN_FIELDS),
+        sets=[dict(name="fine", bit=0, bits=8, value=0xFF),
+              dict(name="memcpy_be", bit=8, bits=24, value=0x22_2324),
+              dict(name="still_fine", bit=56, bits=8, value=0x0F),
+              dict(name="tricky_be0", bit=64, bits=9, value=300),
+              dict(name="tricky_be1", bit=73, bits=9, value=301),
+              dict(name="tricky_be2", bit=82, bits=14, value=13_011),
+              dict(name="trickier_be0", bit=96, bits=1, value=0),
+              dict(name="trickier_be1", bit=97, bits=30, value=0x1BBB_BBBB),
+              dict(name="trickier_be2", bit=127, bits=1, value=1)],
+        untouched_bytes=[[4, 7], [16, 28], [28, 32]],
+        note="LE members (memcpy_le, tricky_le*) are out of scope (README.md:23)")]
+
+
 def header_kats():
     """Header-level vectors: (header kind, bytes, hint) -> (status, used, hint)."""
     zero54 = [0] * 54
@@ -535,6 +620,8 @@ def main() -> None:
         chain_kats=chain_frames() + geneve_frames(),
         header_kats=header_kats(),
         read_kats=read_kats(),
+        modify_kats=modify_kats(),
+        setter_kats=setter_kats(),
         bitfield_kats=bitfield_kats(),
         rss_kats=rss_kats(),
     )

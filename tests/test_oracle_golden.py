@@ -82,6 +82,29 @@ def test_header_kats(kats):
             assert ParseError(st).name == e["error"], kat["name"]
 
 
+def test_setter_kats(kats):
+    """BE setters leave neighbouring bits alone (ingot/src/tests.rs:118-164)."""
+    for kat in kats["setter_kats"]:
+        orig = bytes.fromhex(kat["bytes"])
+        b = orig
+        for st in kat["sets"]:
+            b = oracle.be_set_bits(b, st["bit"], st["bits"], st["value"])
+        for st in kat["sets"]:
+            assert oracle.be_bits(b, st["bit"], st["bits"]) == st["value"], st["name"]
+        for lo, hi in kat["untouched_bytes"]:
+            assert b[lo:hi] == orig[lo:hi], (lo, hi)
+
+
+def test_modify_kats(kats):
+    from ingot_amd.abi import EditOp, Field
+
+    assert len(kats["modify_kats"]) >= 6
+    for kat in kats["modify_kats"]:
+        edits = [(e[0], Field[e[1]], EditOp[e[2]], e[3], *e[4:]) for e in kat["edits"]]
+        out, rec = oracle.parse_modify(bytes.fromhex(kat["frame"]), Chain[kat["chain"]], edits)
+        assert out.hex() == kat["after"], kat["name"]
+
+
 def test_bitfield_kats(kats):
     for kat in kats["bitfield_kats"]:
         data = bytes.fromhex(kat["bytes"])
