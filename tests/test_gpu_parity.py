@@ -290,6 +290,8 @@ def test_window_boundary_and_long_chains(ctx, torch):
         recs, flds = ingot_amd.parse_frames(frames, chain)
         for i, f in enumerate(frames):
             orec, ofld = oracle.parse_one(f, chain)
+            if chain == TUN:
+                ofld = oracle.parse_geneve(f)
             assert recs[i].tobytes() == orec.tobytes(), (i, recs[i], orec)
             assert flds[i].tobytes() == ofld.tobytes(), i
 

@@ -76,8 +76,8 @@ def test_read_kats_on_device(ctx, torch, kats):
         chunks = [bytes.fromhex(c) for c in kat["chunks"]]
         out, recs, chunk, _ = run_device(ctx, torch, [chunks], chain, kind)
         dt = ingot_amd.GENEVE_FIELDS_DTYPE if chain == TUN else ingot_amd.FIELDS_DTYPE
-        fld = out.view(dt)[0]
-        rec = recs.view(ingot_amd.REC_DTYPE)[0]
+        fld = out.reshape(-1).view(dt)[0]
+        rec = recs.reshape(-1).view(ingot_amd.REC_DTYPE)[0]
         bad = check(kat, rec, fld, chunk=int(chunk[0]))
         assert not bad, f"{kat['name']}: {bad}"
         orec, ofld, och = oracle.parse_read(chunks, chain, fields=kind)
@@ -97,7 +97,7 @@ def test_read_fuzz_bit_exact(ctx, torch, chain):
     w_rec, w_fld, w_chunk = oracle.parse_read_batch(*segs, chain, fields=kind)
     n = len(packets)
     bad = np.nonzero((recs.reshape(n, 16) != w_rec.view(np.uint8).reshape(n, 16)).any(1))[0]
-    assert bad.size == 0, (bad[:5], recs[bad[0]].view(ingot_amd.REC_DTYPE), w_rec[bad[0]],
+    assert bad.size == 0, (bad[:5], recs[bad[0]].view(ingot_amd.REC_DTYPE)[0], w_rec[bad[0]],
                            [len(c) for c in packets[bad[0]]])
     width = w_fld.dtype.itemsize
     fb = np.nonzero((out.reshape(n, width) != w_fld.view(np.uint8).reshape(n, width)).any(1))[0]
