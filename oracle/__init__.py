@@ -144,6 +144,10 @@ def segments(packets):
             parts.append(bytes(c) + b"\xee" * (pad - len(c)))
             o += pad
         pkt_seg.append(len(seg_off))
+    # one unreferenced trailing entry keeps the tables non-empty (device
+    # pointers must be non-NULL even when no packet has chunks)
+    seg_off.append(o)
+    seg_len.append(0)
     arena = np.frombuffer(b"".join(parts) + bytes(64), dtype=np.uint8).copy()
     return (arena, np.array(seg_off, dtype=np.uint64), np.array(seg_len, dtype=np.uint16),
             np.array(pkt_seg, dtype=np.uint32))

@@ -89,15 +89,16 @@ def test_modify_strided_decr(ctx, torch):
     """The C2 batch as parse-and-decr-v4: every UDP destination - 1."""
     n = 1 << 20
     arena, _, _ = ingot_amd.gen_frames(GenProfile.V4UDP64, n, stride=64)
-    before = arena.view(n, 64)[:, 36:38].cpu().numpy().copy()
+    before = arena[:n * 64].view(n, 64)[:, 36:38].cpu().numpy().copy()
     ctx.parse_modify(arena, None, None, Chain.UdpParser,
                      [(2, Field.UDP_DESTINATION, EditOp.SUB, 1)], stride=64, n=n)
     torch.cuda.synchronize()
-    after = arena.view(n, 64).cpu().numpy()
+    after = arena[:n * 64].view(n, 64).cpu().numpy()
     b = before[:, 0].astype(np.int32) << 8 | before[:, 1]
     a = after[:, 36].astype(np.int32) << 8 | after[:, 37]
     assert ((b - 1) & 0xFFFF == a).all()
     rest = np.delete(after, [36, 37], axis=1)
     assert rest.tobytes() == np.delete(
-        ingot_amd.gen_frames(GenProfile.V4UDP64, n, stride=64)[0].view(n, 64).cpu().numpy(),
+        ingot_amd.gen_frames(GenProfile.V4UDP64, n, stride=64)[0][:n * 64].view(n, 64).cpu()
+        .numpy(),
         [36, 37], axis=1).tobytes()
