@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py — device-resident L2/L3/L4 parse throughput on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c3s|c4|c5|c6]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2m|c3|c3r|c3s|c4|c5|c6]
                     [--streams S] [--record 16|8]
 
 A *step* is one launch of the parse path over one batch of synthetic frames
@@ -63,7 +63,15 @@ CONFIGS = {
            "C6 (SURVEY 8f-1): 8,388,608 Geneve-over-IPv6 tunnel frames per GPU (OPTE inbound: "
            "outer Eth/IPv6/UDP/Geneve+options, inner 64-1500 B Eth/v4|v6/TCP|UDP|ICMP, 2% ARP), "
            "packed, GeneveOverV6Tunnel"),
+    "c2m": ("V4UDP64", 1 << 20, 64, "UdpParser",
+            "C2 as the reference's parse-and-decr-v4 (ingot-examples/benches/packet.rs:139-145):"
+            " 1,048,576 x 64 B, parse UdpParser + l4.destination -= 1 in place (SURVEY 8f-4)"),
+    "c3r": ("MIXED", 1 << 24, None, "GenericUlp",
+            "C3 frames as 2-chunk packets (header chunk + payload chunk, mblk-style), "
+            "parse_read over chunk lists (SURVEY 8f-3), 16,777,216 per GPU, GenericUlp"),
 }
+# configs that time something other than the batched parse_slice records
+MODES = {"c5": "flows", "c2m": "modify", "c3r": "read"}
 FLOW_BINS = 1 << 16
 
 
@@ -155,6 +163,50 @@ class Runner:
 
     def run(self, steps):
         """Time `steps` launches: fork all streams from streams[0], join back."""
+        return _timed(self.torch, self.streams, self.launch, steps)
+
+
+class ModifyRunner:
+    """parse-and-decr: parse + `l4.set_destination(l4.destination() - 1)` in
+    place on arena k % R, no records (the reference bench keeps none)."""
+
+    def __init__(self, torch, lib, ctx, chain, n, stride, arenas, off, lens, streams):
+        import ingot_amd
+
+        self.torch, self.streams = torch, streams
+        reps, h, c = len(arenas), ctx._h, int(chain)
+        self._edits = ingot_amd.edits_array([(2, ingot_amd.Field.UDP_DESTINATION,
+                                              ingot_amd.EditOp.SUB, 1)])
+        eptr = self._edits.ctypes.data
+        aptrs = [a.data_ptr() for a in arenas]
+        optr = off.data_ptr() if off is not None else None
+        lptr = lens.data_ptr() if lens is not None else None
+        sps = [s.cuda_stream for s in streams]
+        ns = len(sps)
+        self.launch = lambda k: lib.ingot_gpu_parse_modify(h, aptrs[k % reps], optr, lptr,
+                                                           stride or 0, n, c, eptr, 1, None,
+                                                           sps[k % ns])
+
+    def run(self, steps):
+        return _timed(self.torch, self.streams, self.launch, steps)
+
+
+class ReadRunner:
+    """parse_read over chunk lists: arena k % R with the shared segment tables."""
+
+    def __init__(self, torch, lib, ctx, chain, n, arenas, seg_off, seg_len, pkt_seg, outs,
+                 streams):
+        self.torch, self.streams = torch, streams
+        reps, h, c = len(arenas), ctx._h, int(chain)
+        aptrs = [a.data_ptr() for a in arenas]
+        outptrs = [o.data_ptr() for o in outs]
+        so, sl, ps = seg_off.data_ptr(), seg_len.data_ptr(), pkt_seg.data_ptr()
+        sps = [s.cuda_stream for s in streams]
+        ns = len(sps)
+        self.launch = lambda k: lib.ingot_gpu_parse_read(h, aptrs[k % reps], so, sl, ps, n, c,
+                                                         outptrs[k % reps], None, sps[k % ns])
+
+    def run(self, steps):
         return _timed(self.torch, self.streams, self.launch, steps)
 
 
@@ -265,20 +317,40 @@ def main():
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
                                                   for _ in range(max(3, args.streams - 1))]
 
-    flows = args.config == "c5"
+    mode = MODES.get(args.config, "parse")
+    flows = mode == "flows"
     if flows:
         hists = [torch.zeros(FLOW_BINS, dtype=torch.int32, device=dev) for _ in range(reps)]
         flow_ids = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(reps)]
+    if mode == "read":
+        # mblk-style packets: chunk 0 = the header span (payload_off of a
+        # parse_slice pass), chunk 1 = the payload; both in the same arena
+        poff = ingot_amd.records_to_numpy(ctx.parse(arena, off, lens, chain))["payload_off"]
+        poff = torch.from_numpy(poff.astype(np.int64)).to(dev)
+        len64 = lens.to(torch.int64)
+        seg_off = torch.stack([off, off + poff], 1).reshape(-1).contiguous()
+        seg_len = torch.stack([poff, len64 - poff], 1).reshape(-1).to(torch.int32) \
+            .to(torch.uint16).contiguous()
+        pkt_seg = torch.arange(0, 2 * n + 1, 2, dtype=torch.int32, device=dev)
+        del poff, len64
 
     def runner(nstreams, record):
         if flows:
             return FlowRunner(torch, lib, ctx, chain, n, arenas, off, lens, hists, flow_ids,
                               streams[0], idist.reduce_histogram)
+        if mode == "modify":
+            return ModifyRunner(torch, lib, ctx, chain, n, stride, arenas, off, lens,
+                                streams[:nstreams])
+        if mode == "read":
+            return ReadRunner(torch, lib, ctx, chain, n, arenas, seg_off, seg_len, pkt_seg,
+                              outs, streams[:nstreams])
         return Runner(torch, lib, ctx, chain, n, stride, arenas, off, lens, outs,
                       streams[:nstreams], record)
 
     if flows:
         args.streams, args.no_variants = 1, True
+    if mode in ("modify", "read") and args.record == 8:
+        ap.error("8-B records are not offered for this config")
     if chain == Chain.GeneveOverV6Tunnel and args.record == 8:
         ap.error("8-B records are not offered for the tunnel chain (include/ingot_gpu.h)")
     main_run = runner(args.streams, args.record)
@@ -301,10 +373,18 @@ def main():
     torch.cuda.synchronize(dev)
     recs_np = ingot_amd.records_to_numpy(recs)
     lens_np = lens.cpu().numpy() if lens is not None else None
-    rd, wr = algorithmic_bytes(recs_np, lens_np, stride or 0, 0 if stride else 10, args.record)
+    if mode == "read":
+        # chunk 0 read like a frame of the header span's length; descriptors:
+        # pkt_seg (4 B) + chunk 0's (u64 off, u16 len) = 14 B
+        rd, wr = algorithmic_bytes(recs_np, recs_np["payload_off"], 0, 14, 16)
+    else:
+        rd, wr = algorithmic_bytes(recs_np, lens_np, stride or 0, 0 if stride else 10,
+                                   args.record)
     if flows:  # per-packet flow id (4 B) + the flow-id re-read of the histogram pass
         wr = 4 * n + FLOW_BINS * 4
         rd += 4 * n * (FLOW_BINS // min(FLOW_BINS, 16384))
+    if mode == "modify":  # no records; the 2 rewritten bytes per packet
+        wr = 2 * n
     bytes_launch = rd + wr
     pipelined_gbs = bytes_launch / (ms_region / args.steps / 1e3) / 1e9
     # Roofline of the kernel itself: a single-stream pass (launches back to
@@ -334,12 +414,12 @@ def main():
         for ns, rb in ((1, 16), (2, 8), (1, 8), (4, 16)):
             if (ns, rb) == (args.streams, args.record):
                 continue
-            if rb == 8 and chain == Chain.GeneveOverV6Tunnel:
+            if rb == 8 and (chain == Chain.GeneveOverV6Tunnel or mode != "parse"):
                 continue
             r = runner(ns, rb)
             r.run(min(args.warmup, 50))
             ms, _ = r.run(vsteps)
-            bpl = rd + rb * n
+            bpl = rd + (rb * n if mode != "modify" else wr)
             variants[f"streams{ns}_rec{rb}"] = {
                 "value": round(n * vsteps / (ms / 1e3) / 1e6, 2),
                 "us_per_step": round(ms * 1e3 / vsteps, 3),
@@ -348,7 +428,7 @@ def main():
 
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and mode in ("parse", "flows"):
             m = min(n, 1 << 20)  # bounded sample: the first 1M frames of the batch
             if off is not None:
                 o_np = off[:m].cpu().numpy()
@@ -392,7 +472,9 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic["bytes_per_launch"] if traffic else None,
                 "traffic_detail": traffic,
-                "kernel": "k_parse (ingot_amd/csrc/parse.hip)",
+                "kernel": "k_parse (ingot_amd/csrc/parse.hip)" + {
+                    "modify": ", OUT_MODIFY", "read": ", LAYOUT_SEGMENTED",
+                    "flows": ", OUT_FLOWS + k_flow_hist"}.get(mode, ""),
                 "launch_mean_us": round(launch_ms * 1e3, 3),
                 "launch_timing": "single-stream pass, HIP events, region/K",
                 "pipelined_GBps": round(pipelined_gbs, 1),
