@@ -109,6 +109,18 @@ struct Frame {
     __device__ __forceinline__ uint32_t get(uint32_t hdr, Field f) const {
         return (be(hdr + f.byte0(), f.nbytes()) >> f.rshift()) & f.mask();
     }
+
+    // Setter support: byte i of the frame is rewritten in HBM; the staged copy
+    // is kept in step so that a later edit reads the new value.
+    __device__ __forceinline__ void put8(uint32_t i, uint8_t v) const {
+        const_cast<uint8_t*>(g)[i] = v;
+        if (i < avail) {
+            const uint32_t b = sh + i;
+            const uint32_t d = slot_of<NCH>(p, b >> 4) * 4u + ((b >> 2) & 3u);
+            typedef __attribute__((address_space(3))) uint8_t lds_u8;
+            const_cast<lds_u8*>(reinterpret_cast<const lds_u8*>(win))[d * 4u + (b & 3u)] = v;
+        }
+    }
 };
 
 // parse_read's view of a multi-chunk packet (parse.rs:511-537): offsets are
@@ -663,10 +675,12 @@ __device__ __forceinline__ bool header_at(const Rec& r, uint32_t layer, uint32_t
 }
 
 // One generated setter: read-modify-write of the field's covering bytes,
-// neighbouring bits preserved (bitfield.rs:188-315), big-endian.
-__device__ __forceinline__ void apply_edit(uint8_t* hdr, const Edit& e) {
-    uint64_t w = 0;
-    for (uint32_t k = 0; k < e.nbytes; ++k) w = (w << 8) | hdr[e.byte0 + k];
+// neighbouring bits preserved (bitfield.rs:188-315), big-endian.  The bytes
+// are read through the frame view (staged window first) and written to HBM
+// and the window.
+template <class FR>
+__device__ __forceinline__ void apply_edit(const FR& f, uint32_t h, const Edit& e) {
+    uint64_t w = f.be(h + e.byte0, e.nbytes);  // fields span <= 4 bytes
     const uint32_t fm = e.bits >= 32 ? 0xffffffffu : ((1u << e.bits) - 1u);
     const uint32_t cur = (uint32_t)(w >> e.rshift) & fm;
     uint32_t v;
@@ -680,7 +694,7 @@ __device__ __forceinline__ void apply_edit(uint8_t* hdr, const Edit& e) {
     }
     w = (w & ~((uint64_t)fm << e.rshift)) | ((uint64_t)(v & fm) << e.rshift);
     for (uint32_t k = 0; k < e.nbytes; ++k)
-        hdr[e.byte0 + k] = (uint8_t)(w >> (8u * (e.nbytes - 1u - k)));
+        f.put8(h + e.byte0 + k, (uint8_t)(w >> (8u * (e.nbytes - 1u - k))));
 }
 
 // RSS Toeplitz over one 32-bit input word (MSB first) whose first bit is
@@ -843,18 +857,19 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
             walk<CHAIN, false>(fr, r, nullptr, nullptr);
             if (valid) static_cast<uint2*>(a.out)[i] = pack8(r);
         } else if constexpr (MODE == OUT_MODIFY) {
-            // parse, then the setters in order on the frame in HBM (bytes are
-            // re-read there, so an edit sees the previous edits' results)
+            // parse, then the setters in order (each sees the previous
+            // edits' bytes: put8 updates HBM and the staged window)
             walk<CHAIN, false>(fr, r, nullptr, nullptr);
             if (valid && r.status == INGOT_OK) {
-                uint8_t* frame = const_cast<uint8_t*>(a.arena) + off;
                 for (uint32_t k = 0; k < args.n_edits; ++k) {
                     const Edit e = args.e[k];
                     uint32_t h;
-                    if (header_at<CHAIN>(r, e.layer, e.kind, e.index, h)) apply_edit(frame + h, e);
+                    if (header_at<CHAIN>(r, e.layer, e.kind, e.index, h)) apply_edit(fr, h, e);
                 }
             }
             if (valid && a.out) static_cast<uint4*>(a.out)[i] = pack(r);
+            // the window writes must land before the next tile's LDS-DMA
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         } else if constexpr (MODE == OUT_FLOWS) {
             walk<CHAIN, false>(fr, r, nullptr, nullptr);
             uint32_t h;
