@@ -110,16 +110,20 @@ struct Frame {
         return (be(hdr + f.byte0(), f.nbytes()) >> f.rshift()) & f.mask();
     }
 
-    // Setter support: byte i of the frame is rewritten in HBM; the staged copy
-    // is kept in step so that a later edit reads the new value.
-    __device__ __forceinline__ void put8(uint32_t i, uint8_t v) const {
-        const_cast<uint8_t*>(g)[i] = v;
+    // Setter support: byte i of the frame in the staged copy (so a later
+    // edit reads the new value) ...
+    __device__ __forceinline__ void put_staged(uint32_t i, uint8_t v) const {
         if (i < avail) {
             const uint32_t b = sh + i;
             const uint32_t d = slot_of<NCH>(p, b >> 4) * 4u + ((b >> 2) & 3u);
             typedef __attribute__((address_space(3))) uint8_t lds_u8;
             const_cast<lds_u8*>(reinterpret_cast<const lds_u8*>(win))[d * 4u + (b & 3u)] = v;
         }
+    }
+    // ... and staged chunk c (16 B from the 16-B-aligned staging base).
+    __device__ __forceinline__ uint4 chunk(uint32_t c) const {
+        const uint32_t d = slot_of<NCH>(p, c) * 4u;
+        return make_uint4(win[d], win[d + 1], win[d + 2], win[d + 3]);
     }
 };
 
@@ -674,12 +678,42 @@ __device__ __forceinline__ bool header_at(const Rec& r, uint32_t layer, uint32_t
     return have == kind;
 }
 
+// Where a setter's bytes go.  An aligned WB_BYTES block that lies wholly
+// inside the frame and inside the staged chunks is written back whole from the
+// staged copy after all edits (`dirty` marks its first chunk): HBM then sees
+// full blocks instead of byte-masked partial writes.  Other bytes are stored
+// at once.  The staged copy always gets the byte.
+// Measured on C2 parse-and-decr (1 M x 64 B): 32-B sectors 23.1 us/step vs
+// byte stores 25.2 and whole 64-B lines 26.8 (non-temporal stores: no gain).
+constexpr uint32_t WB_BYTES = 32;  // write-back unit (aligned), see below
+
+struct EditSink {
+    uint8_t* frame;     // frame start in HBM
+    uint64_t off;       // frame start, arena offset
+    uint64_t base;      // staging base (off & ~15), arena offset
+    uint32_t len;       // frame length
+    uint32_t staged;    // staged chunks for this frame (0 = none)
+    uint32_t dirty;     // sector first-chunk bits
+};
+
+template <class FR>
+__device__ __forceinline__ void put_byte(const FR& f, EditSink& k, uint32_t i, uint8_t v) {
+    f.put_staged(i, v);
+    const uint64_t a = k.off + i;
+    const uint64_t s = a & ~(uint64_t)(WB_BYTES - 1u);
+    if (s >= k.off && s + WB_BYTES <= k.off + k.len && s + WB_BYTES <= k.base + 16u * k.staged) {
+        k.dirty |= 1u << (uint32_t)((s - k.base) >> 4);
+    } else {
+        k.frame[i] = v;
+    }
+}
+
 // One generated setter: read-modify-write of the field's covering bytes,
 // neighbouring bits preserved (bitfield.rs:188-315), big-endian.  The bytes
-// are read through the frame view (staged window first) and written to HBM
-// and the window.
+// are read through the frame view (staged window first).
 template <class FR>
-__device__ __forceinline__ void apply_edit(const FR& f, uint32_t h, const Edit& e) {
+__device__ __forceinline__ void apply_edit(const FR& f, EditSink& sink, uint32_t h,
+                                           const Edit& e) {
     uint64_t w = f.be(h + e.byte0, e.nbytes);  // fields span <= 4 bytes
     const uint32_t fm = e.bits >= 32 ? 0xffffffffu : ((1u << e.bits) - 1u);
     const uint32_t cur = (uint32_t)(w >> e.rshift) & fm;
@@ -694,7 +728,7 @@ __device__ __forceinline__ void apply_edit(const FR& f, uint32_t h, const Edit& 
     }
     w = (w & ~((uint64_t)fm << e.rshift)) | ((uint64_t)(v & fm) << e.rshift);
     for (uint32_t k = 0; k < e.nbytes; ++k)
-        f.put8(h + e.byte0 + k, (uint8_t)(w >> (8u * (e.nbytes - 1u - k))));
+        put_byte(f, sink, h + e.byte0 + k, (uint8_t)(w >> (8u * (e.nbytes - 1u - k))));
 }
 
 // RSS Toeplitz over one 32-bit input word (MSB first) whose first bit is
@@ -861,10 +895,19 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
             // edits' bytes: put8 updates HBM and the staged window)
             walk<CHAIN, false>(fr, r, nullptr, nullptr);
             if (valid && r.status == INGOT_OK) {
+                EditSink sink{const_cast<uint8_t*>(a.arena) + off, off, base, len, NCH ? nch : 0u, 0u};
                 for (uint32_t k = 0; k < args.n_edits; ++k) {
                     const Edit e = args.e[k];
                     uint32_t h;
-                    if (header_at<CHAIN>(r, e.layer, e.kind, e.index, h)) apply_edit(fr, h, e);
+                    if (header_at<CHAIN>(r, e.layer, e.kind, e.index, h))
+                        apply_edit(fr, sink, h, e);
+                }
+                // whole-sector write-back of the staged copy
+                uint4* dst = reinterpret_cast<uint4*>(const_cast<uint8_t*>(a.arena) + base);
+                for (uint32_t d = sink.dirty; d; d &= d - 1u) {
+                    const uint32_t c = __builtin_ctz(d);
+#pragma unroll
+                    for (uint32_t q = 0; q < WB_BYTES / 16u; ++q) dst[c + q] = fr.chunk(c + q);
                 }
             }
             if (valid && a.out) static_cast<uint4*>(a.out)[i] = pack(r);
