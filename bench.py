@@ -88,9 +88,13 @@ def algorithmic_bytes(recs_np, lens_np, stride, descriptor_bytes, record_bytes):
     return int(r.sum()), record_bytes * len(recs_np)
 
 
-def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5):
-    """Time the oracle on the host cores over the same frames (bounded)."""
+def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode="parse",
+                 segs=None):
+    """Time the oracle on the host cores over the same frames (bounded).
+    mode "read": parse_read over `segs` = (seg_off, seg_len, pkt_seg);
+    "modify": parse + the same setter in place on the sample."""
     import oracle
+    from ingot_amd import EditOp, Field
 
     try:  # -march=native build for this host, into a scratch dir
         d = Path(os.environ.get("TMPDIR", "/tmp")) / f"ingot_oracle_native_{os.getpid()}"
@@ -100,26 +104,37 @@ def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5):
         log(f"[bench] native oracle build failed ({e}); using the prebuilt x86-64-v3 one")
         lib = oracle.load()
         arch = "x86-64-v3"
+
+    def one_pass(t):
+        if mode == "read":
+            oracle.parse_read_batch(arena_np, *segs, chain, lib=lib, nthreads=t)
+        elif mode == "modify":
+            oracle.parse_modify_batch(arena_np, off_np, lens_np, chain,
+                                      [(2, Field.UDP_DESTINATION, EditOp.SUB, 1)], stride=stride,
+                                      n=n, lib=lib, nthreads=t)
+        else:
+            oracle.parse_batch(arena_np, off_np, lens_np, chain, stride=stride, n=n,
+                               nthreads=t, lib=lib)
+
     threads = max(1, min(16, os.cpu_count() or 1))
     res = {}
     for t in sorted({1, threads}):
-        oracle.parse_batch(arena_np, off_np, lens_np, chain, stride=stride, n=n,
-                           nthreads=t, lib=lib)
+        one_pass(t)
         reps, t0 = 0, time.perf_counter()
         while True:
-            oracle.parse_batch(arena_np, off_np, lens_np, chain, stride=stride, n=n,
-                               nthreads=t, lib=lib)
+            one_pass(t)
             reps += 1
             el = time.perf_counter() - t0
             if el > (budget_s if t > 1 else budget_s / 2):
                 break
         res[t] = (reps * n / el / 1e6, reps, el)
     mp, reps, el = res[threads]
+    what = {"parse": "parse_slice", "read": "parse_read", "modify": "parse + set_destination"}
     return {
         "value": round(mp, 3), "unit": "Mpkt/s", "cores": threads, "kind": "port",
         "sample": f"{reps} passes x {n} frames of the benchmark batch (same bytes), "
-                  f"{el:.2f} s wall on {threads} threads; C restatement of ingot parse "
-                  f"(oracle/), -march={arch}",
+                  f"{el:.2f} s wall on {threads} threads; C restatement of ingot "
+                  f"{what.get(mode, mode)} (oracle/), -march={arch}",
         "single_core_value": round(res[1][0], 3),
         "cpu_model": _cpu_model(),
         "host_cpus": os.cpu_count(),
@@ -428,7 +443,7 @@ def main():
 
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu_baseline and mode in ("parse", "flows"):
+        if world == 1 and not args.no_cpu_baseline:
             m = min(n, 1 << 20)  # bounded sample: the first 1M frames of the batch
             if off is not None:
                 o_np = off[:m].cpu().numpy()
@@ -437,7 +452,13 @@ def main():
             else:
                 o_np, a_np = None, arenas[0][:m * stride].cpu().numpy()
             l_np = lens_np[:m] if lens_np is not None else None
-            cpu = cpu_baseline(a_np, o_np, l_np, stride or 0, m, chain, args.cpu_budget)
+            segs = None
+            if mode == "read":
+                segs = (seg_off[:2 * m].cpu().numpy().view(np.uint64),
+                        seg_len[:2 * m].to(torch.int32).cpu().numpy().astype(np.uint16),
+                        pkt_seg[:m + 1].cpu().numpy().view(np.uint32))
+            cpu = cpu_baseline(a_np, o_np, l_np, stride or 0, m, chain, args.cpu_budget,
+                               mode="parse" if flows else mode, segs=segs)
         result = {
             "metric": METRIC,
             "value": round(value, 2),

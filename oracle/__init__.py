@@ -63,7 +63,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     lib.oracle_geneve_fields_batch.argtypes = [vp, vp, vp, ctypes.c_uint32, ctypes.c_uint64, vp]
     lib.oracle_geneve_fields_batch.restype = ctypes.c_int
     lib.oracle_parse_read_batch.argtypes = [vp, vp, vp, vp, ctypes.c_uint64, ctypes.c_int, vp,
-                                            vp, vp, vp]
+                                            vp, vp, vp, ctypes.c_int]
     lib.oracle_parse_read_batch.restype = ctypes.c_int
     if path is None:
         _lib = lib
@@ -154,7 +154,7 @@ def segments(packets):
 
 
 def parse_read_batch(arena, seg_off, seg_len, pkt_seg, chain: Chain, fields: str | None = None,
-                     lib: ctypes.CDLL | None = None):
+                     lib: ctypes.CDLL | None = None, nthreads: int = 1):
     """parse_read over multi-segment packets -> (records, field blocks or None,
     chunk index u16[n]).  fields: None, "fields" (ingot_fields) or "geneve"."""
     lib = lib or load()
@@ -171,7 +171,7 @@ def parse_read_batch(arena, seg_off, seg_len, pkt_seg, chain: Chain, fields: str
     elif fields == "geneve":
         gf = np.zeros(n, dtype=GENEVE_FIELDS_DTYPE)
     rc = lib.oracle_parse_read_batch(_p(arena), _p(seg_off), _p(seg_len), _p(pkt_seg), n,
-                                     int(chain), _p(rec), _p(fld), _p(gf), _p(chunk))
+                                     int(chain), _p(rec), _p(fld), _p(gf), _p(chunk), nthreads)
     if rc != 0:
         raise ValueError("oracle_parse_read_batch: bad arguments")
     return rec, (fld if fld is not None else gf), chunk
@@ -193,12 +193,12 @@ def be_set_bits(hdr: bytes, first_bit: int, n_bits: int, value: int) -> bytes:
 
 
 def parse_modify_batch(arena: np.ndarray, off, lens, chain: Chain, edits, stride: int = 0,
-                       n: int | None = None):
+                       n: int | None = None, lib: ctypes.CDLL | None = None, nthreads: int = 1):
     """In place on `arena` (numpy u8); returns the parse records."""
-    lib = load()
+    lib = lib or load()
     lib.oracle_parse_modify_batch.argtypes = [ctypes.c_void_p] * 3 + [
         ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32,
-        ctypes.c_void_p]
+        ctypes.c_void_p, ctypes.c_int]
     if off is not None:
         off = np.ascontiguousarray(off, dtype=np.uint64)
         n = len(off) if n is None else n
@@ -207,7 +207,7 @@ def parse_modify_batch(arena: np.ndarray, off, lens, chain: Chain, edits, stride
     e = edits_array(edits)
     rec = np.zeros(n, dtype=REC_DTYPE)
     if lib.oracle_parse_modify_batch(_p(arena), _p(off), _p(lens), stride, n, int(chain), _p(e),
-                                     len(e), _p(rec)) != 0:
+                                     len(e), _p(rec), nthreads) != 0:
         raise ValueError("oracle_parse_modify_batch: bad arguments")
     return rec
 

@@ -18,6 +18,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* Static contiguous partition of [0, n) over nthreads pthreads (the calling
+ * thread takes the first range); defined with the batch driver below. */
+typedef void (*range_fn)(void* ctx, uint64_t lo, uint64_t hi);
+static int parallel_ranges(uint64_t n, int nthreads, range_fn fn, void* ctx);
+
 /* ParseError discriminants + 1 (ingot-types/src/error.rs:22-44). */
 enum {
     PE_OK = INGOT_OK,
@@ -335,11 +340,24 @@ typedef struct {
     uint32_t p;   /* bytes consumed */
     ingot_rec* r;
     ingot_fields* F;
-    /* parse_read over chunks (parse.rs:511-537): f is the chunks concatenated,
-     * chunk k spans seglen[0..k) .. +seglen[k]; NULL for parse_slice. */
+    /* parse_read over chunks (parse.rs:511-537): f is the chunks
+     * concatenated (copied in as the walk reaches them), chunk k spans
+     * sum(seglen[0..k)) .. + seglen[k]; seglen NULL for parse_slice. */
     const uint16_t* seglen;
     uint32_t nseg, k;
+    const uint8_t* arena;
+    const uint64_t* seg_off;
+    uint8_t* buf;
 } walk_t;
+
+/* Append chunk k of a parse_read packet to the concatenation (bytes past
+ * 65535 are dropped: record offsets are u16). */
+static void pull_chunk(walk_t* w) {
+    uint32_t l = w->seglen[w->k];
+    if (w->len + l > 65535u) l = 65535u - w->len;
+    memcpy(w->buf + w->len, w->arena + w->seg_off[w->k], l);
+    w->len += l;
+}
 
 static int more_chunks(const walk_t* w) { return w->seglen && w->k + 1 < w->nseg; }
 
@@ -363,7 +381,7 @@ static int next_slice(walk_t* w, int layer) {
         return PE_TOO_SMALL;
     }
     w->k++;
-    w->len += w->seglen[w->k];
+    pull_chunk(w);
     return PE_OK;
 }
 
@@ -673,56 +691,65 @@ static void parse_one(const uint8_t* frame, uint32_t len, int chain, ingot_rec* 
     if (tunnel) memset(tunnel, 0, sizeof *tunnel);
     const int tun = chain == INGOT_CHAIN_GENEVE_OVER_V6;
     /* the tunnel's outer layers have no ingot_fields slots */
-    walk_t w = {frame, len, 0, rec, tun ? 0 : fields, 0, 0, 0};
+    walk_t w = {frame, len, 0, rec, tun ? 0 : fields, 0, 0, 0, 0, 0, 0};
     walk_chain(&w, chain, fields, tunnel);
 }
 
-/* parse_read: the chunks are concatenated (bytes past 65535 are dropped: the
- * record's offsets are u16) and walked with chunk-end bounds. */
+/* parse_read: the chunks are concatenated as the walk steps into them and
+ * walked with chunk-end bounds. */
 static void parse_read_one(const uint8_t* arena, const uint64_t* seg_off,
                            const uint16_t* seg_len, uint32_t nseg, int chain, ingot_rec* rec,
                            ingot_fields* fields, ingot_tunnel_fields* tunnel, uint16_t* chunk) {
-    uint8_t* buf = (uint8_t*)malloc(65536 + 16);
-    uint16_t* lens = (uint16_t*)malloc(sizeof(uint16_t) * (nseg ? nseg : 1));
-    uint32_t total = 0;
-    for (uint32_t k = 0; k < nseg; ++k) {
-        uint32_t l = seg_len[k];
-        if (total + l > 65535u) l = 65535u - total;
-        memcpy(buf + total, arena + seg_off[k], l);
-        lens[k] = (uint16_t)l;
-        total += l;
-    }
+    static __thread uint8_t buf[65536 + 16];
     memset(rec, 0, sizeof *rec);
     if (fields) memset(fields, 0, sizeof *fields);
     if (tunnel) memset(tunnel, 0, sizeof *tunnel);
     const int tun = chain == INGOT_CHAIN_GENEVE_OVER_V6;
     /* next_chunk() for the first slice: no chunks -> TooSmall (lib.rs:169-175),
      * which the eth layer then reports (a zero-length first slice). */
-    walk_t w = {buf, nseg ? lens[0] : 0u, 0, rec, tun ? 0 : fields, lens, nseg, 0};
+    walk_t w = {buf, 0, 0, rec, tun ? 0 : fields, seg_len, nseg, 0, arena, seg_off, buf};
+    if (nseg) pull_chunk(&w);
     walk_chain(&w, chain, fields, tunnel);
     if (chunk) *chunk = (uint16_t)w.k;
-    free(lens);
-    free(buf);
 }
+
 void oracle_parse_one(const uint8_t* frame, uint32_t len, int chain, ingot_rec* rec,
                       ingot_fields* fields) {
     parse_one(frame, len, chain, rec, fields, 0);
 }
 
+typedef struct {
+    const uint8_t* arena;
+    const uint64_t* seg_off;
+    const uint16_t* seg_len;
+    const uint32_t* pkt_seg;
+    int chain;
+    ingot_rec* rec;
+    ingot_fields* fields;
+    ingot_geneve_fields* gfields;
+    uint16_t* chunk;
+} read_job_t;
+
+static void read_range(void* ctx, uint64_t lo, uint64_t hi) {
+    const read_job_t* j = (const read_job_t*)ctx;
+    for (uint64_t i = lo; i < hi; ++i) {
+        const uint32_t a = j->pkt_seg[i], b = j->pkt_seg[i + 1];
+        ingot_rec* r = j->gfields ? &j->gfields[i].inner.rec : &j->rec[i];
+        parse_read_one(j->arena, j->seg_off + a, j->seg_len + a, b - a, j->chain, r,
+                       j->gfields ? &j->gfields[i].inner : j->fields ? &j->fields[i] : 0,
+                       j->gfields ? &j->gfields[i].outer : 0, j->chunk ? &j->chunk[i] : 0);
+        if (j->gfields) j->rec[i] = *r;
+    }
+}
+
 int oracle_parse_read_batch(const uint8_t* arena, const uint64_t* seg_off, const uint16_t* seg_len,
                             const uint32_t* pkt_seg, uint64_t n, int chain, ingot_rec* rec,
-                            ingot_fields* fields, ingot_geneve_fields* gfields, uint16_t* chunk) {
+                            ingot_fields* fields, ingot_geneve_fields* gfields, uint16_t* chunk,
+                            int nthreads) {
     if ((!rec && n) || !pkt_seg || chain < 0 || chain >= INGOT_CHAIN_COUNT) return -1;
     if (fields && gfields) return -1;
-    for (uint64_t i = 0; i < n; ++i) {
-        const uint32_t a = pkt_seg[i], b = pkt_seg[i + 1];
-        ingot_rec* r = gfields ? &gfields[i].inner.rec : &rec[i];
-        parse_read_one(arena, seg_off + a, seg_len + a, b - a, chain, r,
-                       gfields ? &gfields[i].inner : fields ? &fields[i] : 0,
-                       gfields ? &gfields[i].outer : 0, chunk ? &chunk[i] : 0);
-        if (gfields) rec[i] = *r;
-    }
-    return 0;
+    read_job_t j = {arena, seg_off, seg_len, pkt_seg, chain, rec, fields, gfields, chunk};
+    return parallel_ranges(n, nthreads, read_range, &j);
 }
 
 void oracle_parse_geneve(const uint8_t* frame, uint32_t len, ingot_geneve_fields* out) {
@@ -854,53 +881,58 @@ int oracle_parse_modify(uint8_t* frame, uint32_t len, int chain, const ingot_edi
     return 0;
 }
 
+typedef struct {
+    uint8_t* arena;
+    const uint64_t* off;
+    const uint16_t* len;
+    uint32_t stride;
+    int chain;
+    const ingot_edit* edits;
+    uint32_t n_edits;
+    ingot_rec* rec;
+    int bad;
+} modify_job_t;
+
+static void modify_range(void* ctx, uint64_t lo, uint64_t hi) {
+    modify_job_t* j = (modify_job_t*)ctx;
+    for (uint64_t i = lo; i < hi; ++i) {
+        uint64_t o = j->off ? j->off[i] : i * (uint64_t)j->stride;
+        uint32_t l = j->len ? j->len[i] : j->stride;
+        if (!j->off && l > j->stride) l = j->stride;
+        if (oracle_parse_modify(j->arena + o, l, j->chain, j->edits, j->n_edits,
+                                j->rec ? &j->rec[i] : 0) != 0)
+            j->bad = 1;
+    }
+}
+
 int oracle_parse_modify_batch(uint8_t* arena, const uint64_t* off, const uint16_t* len,
                               uint32_t stride, uint64_t n, int chain, const ingot_edit* edits,
-                              uint32_t n_edits, ingot_rec* rec) {
+                              uint32_t n_edits, ingot_rec* rec, int nthreads) {
     if ((!off && stride == 0 && n) || chain < 0 || chain >= INGOT_CHAIN_COUNT) return -1;
-    for (uint64_t i = 0; i < n; ++i) {
-        uint64_t o = off ? off[i] : i * (uint64_t)stride;
-        uint32_t l = len ? len[i] : stride;
-        if (!off && l > stride) l = stride;
-        if (oracle_parse_modify(arena + o, l, chain, edits, n_edits, rec ? &rec[i] : 0) != 0)
-            return -1;
-    }
-    return 0;
+    modify_job_t j = {arena, off, len, stride, chain, edits, n_edits, rec, 0};
+    if (parallel_ranges(n, nthreads, modify_range, &j) != 0) return -1;
+    return j.bad ? -1 : 0;
 }
 
 /* ------------------------------------------------------------------------
  * Batch driver (pthreads, static contiguous partition).
  * ---------------------------------------------------------------------- */
 typedef struct {
-    const uint8_t* arena;
-    const uint64_t* off;
-    const uint16_t* len;
-    uint32_t stride;
+    range_fn fn;
+    void* ctx;
     uint64_t lo, hi;
-    int chain;
-    ingot_rec* rec;
-    ingot_fields* fields;
-} job_t;
+} range_job_t;
 
-static void* run_job(void* arg) {
-    job_t* j = (job_t*)arg;
-    for (uint64_t i = j->lo; i < j->hi; ++i) {
-        uint64_t o = j->off ? j->off[i] : i * (uint64_t)j->stride;
-        uint32_t l = j->len ? j->len[i] : j->stride;
-        if (!j->off && l > j->stride) l = j->stride; /* a slot holds one frame */
-        oracle_parse_one(j->arena + o, l, j->chain, &j->rec[i], j->fields ? &j->fields[i] : 0);
-    }
+static void* run_range(void* arg) {
+    range_job_t* j = (range_job_t*)arg;
+    j->fn(j->ctx, j->lo, j->hi);
     return 0;
 }
 
-int oracle_parse_batch(const uint8_t* arena, const uint64_t* off, const uint16_t* len,
-                       uint32_t stride, uint64_t n, int chain, ingot_rec* rec,
-                       ingot_fields* fields, int nthreads) {
-    if ((!arena && n) || (!rec && n) || chain < 0 || chain >= INGOT_CHAIN_COUNT) return -1;
-    if (!off && stride == 0 && n) return -1;
+static int parallel_ranges(uint64_t n, int nthreads, range_fn fn, void* ctx) {
     if (nthreads < 1) nthreads = 1;
     if ((uint64_t)nthreads > n) nthreads = n ? (int)n : 1;
-    job_t* jobs = (job_t*)calloc((size_t)nthreads, sizeof(job_t));
+    range_job_t* jobs = (range_job_t*)calloc((size_t)nthreads, sizeof(range_job_t));
     pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
     if (!jobs || !th) {
         free(jobs);
@@ -912,21 +944,50 @@ int oracle_parse_batch(const uint8_t* arena, const uint64_t* off, const uint16_t
         uint64_t lo = per * (uint64_t)t, hi = lo + per;
         if (lo > n) lo = n;
         if (hi > n) hi = n;
-        job_t j = {arena, off, len, stride, lo, hi, chain, rec, fields};
+        range_job_t j = {fn, ctx, lo, hi};
         jobs[t] = j;
     }
     int started = 0;
     for (int t = 1; t < nthreads; ++t) {
-        if (pthread_create(&th[t], 0, run_job, &jobs[t]) != 0) break;
+        if (pthread_create(&th[t], 0, run_range, &jobs[t]) != 0) break;
         started = t;
     }
-    run_job(&jobs[0]);
+    run_range(&jobs[0]);
     for (int t = 1; t <= started; ++t) pthread_join(th[t], 0);
-    /* any job whose thread failed to start runs here */
-    for (int t = started + 1; t < nthreads; ++t) run_job(&jobs[t]);
+    /* any range whose thread failed to start runs here */
+    for (int t = started + 1; t < nthreads; ++t) run_range(&jobs[t]);
     free(jobs);
     free(th);
     return 0;
+}
+
+typedef struct {
+    const uint8_t* arena;
+    const uint64_t* off;
+    const uint16_t* len;
+    uint32_t stride;
+    int chain;
+    ingot_rec* rec;
+    ingot_fields* fields;
+} slice_job_t;
+
+static void slice_range(void* ctx, uint64_t lo, uint64_t hi) {
+    const slice_job_t* j = (const slice_job_t*)ctx;
+    for (uint64_t i = lo; i < hi; ++i) {
+        uint64_t o = j->off ? j->off[i] : i * (uint64_t)j->stride;
+        uint32_t l = j->len ? j->len[i] : j->stride;
+        if (!j->off && l > j->stride) l = j->stride; /* a slot holds one frame */
+        oracle_parse_one(j->arena + o, l, j->chain, &j->rec[i], j->fields ? &j->fields[i] : 0);
+    }
+}
+
+int oracle_parse_batch(const uint8_t* arena, const uint64_t* off, const uint16_t* len,
+                       uint32_t stride, uint64_t n, int chain, ingot_rec* rec,
+                       ingot_fields* fields, int nthreads) {
+    if ((!arena && n) || (!rec && n) || chain < 0 || chain >= INGOT_CHAIN_COUNT) return -1;
+    if (!off && stride == 0 && n) return -1;
+    slice_job_t j = {arena, off, len, stride, chain, rec, fields};
+    return parallel_ranges(n, nthreads, slice_range, &j);
 }
 
 /* ------------------------------------------------------------------------

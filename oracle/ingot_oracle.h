@@ -43,7 +43,7 @@ int oracle_geneve_fields_batch(const uint8_t* arena, const uint64_t* off,
 int oracle_parse_read_batch(const uint8_t* arena, const uint64_t* seg_off,
                             const uint16_t* seg_len, const uint32_t* pkt_seg, uint64_t n,
                             int chain, ingot_rec* rec, ingot_fields* fields,
-                            ingot_geneve_fields* gfields, uint16_t* chunk);
+                            ingot_geneve_fields* gfields, uint16_t* chunk, int nthreads);
 
 /* Batch form.  off == NULL selects the strided layout (frame i at i*stride);
  * len == NULL means every frame is `stride` bytes long.  fields may be NULL.
@@ -67,7 +67,7 @@ int oracle_parse_modify(uint8_t* frame, uint32_t len, int chain, const ingot_edi
                         uint32_t n_edits, ingot_rec* rec);
 int oracle_parse_modify_batch(uint8_t* arena, const uint64_t* off, const uint16_t* len,
                               uint32_t stride, uint64_t n, int chain, const ingot_edit* edits,
-                              uint32_t n_edits, ingot_rec* rec);
+                              uint32_t n_edits, ingot_rec* rec, int nthreads);
 
 /* IpProtocol::class (ingot/src/ip.rs:40-54): 0 = None, 1 = FragmentHeader,
  * 2 = Rfc6564. */
