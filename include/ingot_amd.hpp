@@ -17,6 +17,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <array>
 #include <cstdint>
 #include <cstring>
@@ -407,6 +408,87 @@ inline std::vector<Packet> parse_batch(Context& ctx, const std::vector<std::vect
     return out;
 }
 
+// parse_read over chunk lists: packet i = chunks[i] (a `Read` of byte chunks,
+// ingot-types/src/lib.rs:151-166).  The Packet's frame is the chunks
+// concatenated (record offsets are logical); `chunk` = the chunk holding the
+// remainder; `ends` = each chunk's logical end.
+using Chunks = std::vector<std::vector<uint8_t>>;
+struct ReadResult {
+    Packet pkt;
+    uint16_t chunk;
+    std::vector<size_t> ends;
+};
+
+inline std::vector<ReadResult> parse_read_batch(Context& ctx, const std::vector<Chunks>& packets,
+                                                int chain) {
+    const size_t n = packets.size();
+    std::vector<uint64_t> seg_off;
+    std::vector<uint16_t> seg_len;
+    std::vector<uint32_t> pkt_seg{0};
+    std::vector<uint8_t> arena;
+    for (const auto& chunks : packets) {
+        for (const auto& c : chunks) {
+            if (c.size() > 65535) throw std::length_error("chunk longer than 65535 bytes");
+            seg_off.push_back(arena.size());
+            seg_len.push_back((uint16_t)c.size());
+            arena.insert(arena.end(), c.begin(), c.end());
+            arena.resize((arena.size() + 15) / 16 * 16 + 16, 0);  // chunks apart in memory
+        }
+        pkt_seg.push_back((uint32_t)seg_off.size());
+    }
+    seg_off.push_back(arena.size());  // keeps the tables non-empty
+    seg_len.push_back(0);
+    arena.resize(arena.size() + 64, 0);
+    const bool tun = chain == INGOT_CHAIN_GENEVE_OVER_V6;
+    const size_t blk = tun ? sizeof(ingot_geneve_fields) : sizeof(ingot_fields);
+    uint8_t *d_arena = nullptr, *d_f = nullptr;
+    uint64_t* d_off = nullptr;
+    uint16_t *d_len = nullptr, *d_chunk = nullptr;
+    uint32_t* d_ps = nullptr;
+    hip_check(hipMalloc(&d_arena, arena.size()), "hipMalloc");
+    hip_check(hipMalloc(&d_off, seg_off.size() * 8), "hipMalloc");
+    hip_check(hipMalloc(&d_len, seg_len.size() * 2), "hipMalloc");
+    hip_check(hipMalloc(&d_ps, pkt_seg.size() * 4), "hipMalloc");
+    hip_check(hipMalloc(&d_f, n * blk + 512), "hipMalloc");
+    hip_check(hipMalloc(&d_chunk, n * 2 + 8), "hipMalloc");
+    hip_check(hipMemcpy(d_arena, arena.data(), arena.size(), hipMemcpyHostToDevice), "H2D");
+    hip_check(hipMemcpy(d_off, seg_off.data(), seg_off.size() * 8, hipMemcpyHostToDevice), "H2D");
+    hip_check(hipMemcpy(d_len, seg_len.data(), seg_len.size() * 2, hipMemcpyHostToDevice), "H2D");
+    hip_check(hipMemcpy(d_ps, pkt_seg.data(), pkt_seg.size() * 4, hipMemcpyHostToDevice), "H2D");
+    if (tun)
+        check(ingot_gpu_geneve_fields_read(ctx.get(), d_arena, d_off, d_len, d_ps, n,
+                                           reinterpret_cast<ingot_geneve_fields*>(d_f), d_chunk,
+                                           nullptr),
+              "ingot_gpu_geneve_fields_read");
+    else
+        check(ingot_gpu_fields_read(ctx.get(), d_arena, d_off, d_len, d_ps, n, chain,
+                                    reinterpret_cast<ingot_fields*>(d_f), d_chunk, nullptr),
+              "ingot_gpu_fields_read");
+    std::vector<uint8_t> f(n * blk);
+    std::vector<uint16_t> chunk(n);
+    hip_check(hipMemcpy(f.data(), d_f, n * blk, hipMemcpyDeviceToHost), "D2H");
+    hip_check(hipMemcpy(chunk.data(), d_chunk, n * 2, hipMemcpyDeviceToHost), "D2H");
+    std::vector<ReadResult> out(n);
+    for (size_t i = 0; i < n; ++i) {
+        ReadResult& r = out[i];
+        for (const auto& c : packets[i]) {
+            r.pkt.frame.insert(r.pkt.frame.end(), c.begin(), c.end());
+            r.ends.push_back(r.pkt.frame.size());
+        }
+        std::memcpy(&r.pkt.fields, f.data() + i * blk, sizeof(ingot_fields));
+        if (tun)
+            std::memcpy(&r.pkt.outer, f.data() + i * blk + sizeof(ingot_fields),
+                        sizeof(ingot_tunnel_fields));
+        else
+            std::memset(&r.pkt.outer, 0, sizeof(ingot_tunnel_fields));
+        r.chunk = chunk[i];
+    }
+    for (void* p : {(void*)d_arena, (void*)d_off, (void*)d_len, (void*)d_ps, (void*)d_f,
+                    (void*)d_chunk})
+        (void)hipFree(p);
+    return out;
+}
+
 inline Context& default_context() {
     static Context ctx(0);
     return ctx;
@@ -418,6 +500,46 @@ namespace examples {
 
 template <class Chain>
 using Success = std::tuple<Chain, std::optional<uint8_t>, std::vector<uint8_t>>;
+
+// ingot_types::Parsed (parse_read's result, parse.rs:525-535): the headers,
+// the chunks not yet read, and the rest of the chunk holding the remainder
+// (None when that chunk was consumed exactly).
+template <class Chain>
+struct Parsed {
+    Chain headers;
+    gpu::Chunks data;
+    std::optional<std::vector<uint8_t>> last_chunk;
+};
+
+// Shared by every chain's parse_read: run the batch, build each Ok packet's
+// headers with Chain::build, attach Parsed's chunk bookkeeping.
+template <class Chain>
+std::vector<types::ParseResult<Parsed<Chain>>> parse_read_all(const std::vector<gpu::Chunks>& pk,
+                                                              gpu::Context& ctx) {
+    std::vector<types::ParseResult<Parsed<Chain>>> out;
+    auto res = gpu::parse_read_batch(ctx, pk, Chain::CHAIN);
+    for (size_t i = 0; i < res.size(); ++i) {
+        auto& r = res[i];
+        const ingot_rec rec = r.pkt.fields.rec;
+        if (rec.status != INGOT_OK) {
+            out.push_back(types::ParseResult<Parsed<Chain>>::err(types::PacketParseError(
+                ingot_chain_layer_label(Chain::CHAIN, rec.err_layer),
+                (types::ParseError)rec.status)));
+            continue;
+        }
+        const size_t end = r.ends.empty() ? 0 : r.ends[r.chunk];
+        std::optional<std::vector<uint8_t>> last;
+        if (end > rec.payload_off)
+            last = std::vector<uint8_t>(r.pkt.frame.begin() + rec.payload_off,
+                                        r.pkt.frame.begin() + end);
+        gpu::Chunks data(pk[i].begin() + std::min(pk[i].size(), (size_t)r.chunk + 1),
+                         pk[i].end());
+        auto sp = std::make_shared<const Packet>(std::move(r.pkt));
+        out.push_back(types::ParseResult<Parsed<Chain>>::ok(
+            Parsed<Chain>{Chain::build(sp), std::move(data), std::move(last)}));
+    }
+    return out;
+}
 
 namespace detail {
 inline types::PacketParseError error_of(int chain, const ingot_rec& r) {
@@ -466,15 +588,22 @@ struct UdpParser {
                     detail::error_of(CHAIN, sp->fields.rec)));
                 continue;
             }
-            UdpParser c{sp, ValidEthernet(&sp->fields), detail::l3_of(*sp),
-                        ValidUdp(&sp->fields)};
             out.push_back(types::ParseResult<Success<UdpParser>>::ok(
-                Success<UdpParser>{c, std::nullopt, detail::remainder(*sp)}));
+                Success<UdpParser>{build(sp), std::nullopt, detail::remainder(*sp)}));
         }
         return out;
     }
     static types::ParseResult<Success<UdpParser>> parse(const std::vector<uint8_t>& frame) {
         return std::move(parse_all({frame})[0]);
+    }
+    // parse.rs:511-537 over a chunk list
+    static types::ParseResult<Parsed<UdpParser>> parse_read(
+        const gpu::Chunks& chunks, gpu::Context& ctx = gpu::default_context()) {
+        return std::move(parse_read_all<UdpParser>({chunks}, ctx)[0]);
+    }
+    static UdpParser build(const std::shared_ptr<const Packet>& sp) {
+        return UdpParser{sp, ValidEthernet(&sp->fields), detail::l3_of(*sp),
+                         ValidUdp(&sp->fields)};
     }
 };
 
@@ -498,15 +627,22 @@ struct GenericUlp {
                     detail::error_of(CHAIN, sp->fields.rec)));
                 continue;
             }
-            GenericUlp c{sp, ValidEthernet(&sp->fields), std::nullopt, std::nullopt};
-            if (!(sp->fields.rec.flags & INGOT_REC_ACCEPTED)) {
-                c.inner_l3 = detail::l3_of(*sp);
-                c.inner_ulp = detail::l4_of(*sp);
-            }
             out.push_back(types::ParseResult<Success<GenericUlp>>::ok(
-                Success<GenericUlp>{c, std::nullopt, detail::remainder(*sp)}));
+                Success<GenericUlp>{build(sp), std::nullopt, detail::remainder(*sp)}));
         }
         return out;
+    }
+    static GenericUlp build(const std::shared_ptr<const Packet>& sp) {
+        GenericUlp c{sp, ValidEthernet(&sp->fields), std::nullopt, std::nullopt};
+        if (!(sp->fields.rec.flags & INGOT_REC_ACCEPTED)) {
+            c.inner_l3 = detail::l3_of(*sp);
+            c.inner_ulp = detail::l4_of(*sp);
+        }
+        return c;
+    }
+    static types::ParseResult<Parsed<GenericUlp>> parse_read(
+        const gpu::Chunks& chunks, gpu::Context& ctx = gpu::default_context()) {
+        return std::move(parse_read_all<GenericUlp>({chunks}, ctx)[0]);
     }
     static types::ParseResult<Success<GenericUlp>> parse(const std::vector<uint8_t>& frame) {
         return std::move(parse_all({frame})[0]);
@@ -540,22 +676,29 @@ struct GeneveOverV6Tunnel {
                     detail::error_of(CHAIN, sp->fields.rec)));
                 continue;
             }
-            GeneveOverV6Tunnel c{sp,
-                                 ValidEthernet(&sp->outer),
-                                 ValidOuterIpv6(&sp->outer),
-                                 ValidUdp(&sp->outer),
-                                 ValidGeneve(&sp->outer, &sp->frame),
-                                 ValidEthernet(&sp->fields),
-                                 std::nullopt,
-                                 std::nullopt};
-            if (!(sp->fields.rec.flags & INGOT_REC_ACCEPTED)) {
-                c.inner_l3 = detail::l3_of(*sp);
-                c.inner_ulp = detail::l4_of(*sp);
-            }
             out.push_back(types::ParseResult<Success<GeneveOverV6Tunnel>>::ok(
-                Success<GeneveOverV6Tunnel>{c, std::nullopt, detail::remainder(*sp)}));
+                Success<GeneveOverV6Tunnel>{build(sp), std::nullopt, detail::remainder(*sp)}));
         }
         return out;
+    }
+    static GeneveOverV6Tunnel build(const std::shared_ptr<const Packet>& sp) {
+        GeneveOverV6Tunnel c{sp,
+                             ValidEthernet(&sp->outer),
+                             ValidOuterIpv6(&sp->outer),
+                             ValidUdp(&sp->outer),
+                             ValidGeneve(&sp->outer, &sp->frame),
+                             ValidEthernet(&sp->fields),
+                             std::nullopt,
+                             std::nullopt};
+        if (!(sp->fields.rec.flags & INGOT_REC_ACCEPTED)) {
+            c.inner_l3 = detail::l3_of(*sp);
+            c.inner_ulp = detail::l4_of(*sp);
+        }
+        return c;
+    }
+    static types::ParseResult<Parsed<GeneveOverV6Tunnel>> parse_read(
+        const gpu::Chunks& chunks, gpu::Context& ctx = gpu::default_context()) {
+        return std::move(parse_read_all<GeneveOverV6Tunnel>({chunks}, ctx)[0]);
     }
     static types::ParseResult<Success<GeneveOverV6Tunnel>> parse(
         const std::vector<uint8_t>& frame) {

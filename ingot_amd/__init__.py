@@ -52,7 +52,7 @@ from .abi import (  # noqa: F401  (re-exports)
 __all__ = [
     "Chain", "Context", "GenProfile", "PacketParseError", "ParseError", "UdpParser",
     "GenericUlp", "VlanUlp", "GeneveOverV6Tunnel", "gen_frames", "gen_lengths", "records_to_numpy",
-    "fields_to_numpy", "load_library",
+    "fields_to_numpy", "load_library", "Parsed", "chunk_tables",
 ]
 
 
@@ -651,9 +651,65 @@ def parse_frames(frames: list, chain: Chain, device: int = 0):
     return records_to_numpy(recs), flds
 
 
+def chunk_tables(packets):
+    """Host-side chunk tables for Context.parse_read: packets = [[chunk bytes,
+    ...], ...] -> (arena u8, seg_off u64, seg_len u16, pkt_seg u32) numpy
+    arrays, each chunk stored apart (16-B aligned, a gap after it)."""
+    import numpy as np
+
+    seg_off, seg_len, pkt_seg, parts, o = [], [], [0], [], 0
+    for chunks in packets:
+        for c in chunks:
+            pad = (len(c) + 15) // 16 * 16 + 16
+            seg_off.append(o)
+            seg_len.append(len(c))
+            parts.append(bytes(c) + bytes(pad - len(c)))
+            o += pad
+        pkt_seg.append(len(seg_off))
+    seg_off.append(o)  # one unreferenced entry keeps the tables non-empty
+    seg_len.append(0)
+    arena = np.frombuffer(b"".join(parts) + bytes(64), dtype=np.uint8).copy()
+    return (arena, np.array(seg_off, dtype=np.uint64), np.array(seg_len, dtype=np.uint16),
+            np.array(pkt_seg, dtype=np.uint32))
+
+
+@dataclass
+class Parsed:
+    """ingot_types::Parsed (parse_read's Ok value, ingot-macros/src/parse.rs:
+    525-535): the headers, the chunks not yet read, and the rest of the chunk
+    holding the remainder (None when that chunk was consumed exactly)."""
+
+    headers: object
+    data: list
+    last_chunk: Optional[bytes]
+
+
 class _ChainParser:
     chain: Chain
     names: tuple
+
+    @classmethod
+    def parse_read(cls, chunks, device: int = 0) -> Parsed:
+        """`<Chain>::parse_read(chunks)` on the device, or raises
+        PacketParseError (StraddledHeader when a header crosses a chunk end
+        and more chunks follow)."""
+        torch = _torch()
+        chunks = [bytes(c) for c in chunks]
+        arena, so, sl, ps = chunk_tables([chunks])
+        dev = f"cuda:{device}"
+        d = (torch.from_numpy(arena).to(dev), torch.from_numpy(so.view("int64")).to(dev),
+             torch.from_numpy(sl.view("int16")).to(dev), torch.from_numpy(ps.view("int32")).to(dev))
+        tun = cls.chain == Chain.GeneveOverV6Tunnel
+        out, ch = _ctx_for(device).parse_read(*d, cls.chain, fields="geneve" if tun else "fields")
+        torch.cuda.synchronize(device)
+        f = (geneve_fields_to_numpy if tun else fields_to_numpy)(out)[0]
+        k = int(ch.cpu().numpy().view("uint16")[0])
+        frame = b"".join(chunks)
+        r = f["inner"]["rec"] if tun else f["rec"]
+        hdrs, _, _ = cls._assemble(frame, r, f)
+        end = sum(len(c) for c in chunks[:k + 1])
+        po = int(r["payload_off"])
+        return Parsed(hdrs, chunks[k + 1:], frame[po:end] if end > po else None)
 
     @classmethod
     def parse(cls, frame: bytes, device: int = 0):

@@ -299,6 +299,64 @@ TEST(geneve_to_owned_in_tunnel) {
     ASSERT_TRUE(opts[0].data.empty());
 }
 
+// ingot-examples/src/tests.rs:120-187 (the parse_read half)
+TEST(parse_header_chain_multichunk) {
+    std::vector<uint8_t> eth(14, 0), v6(40, 0), udp(8, 0), body(128, 0xaa);
+    for (int i = 0; i < 6; ++i) eth[i] = 0xff;
+    const uint8_t src[] = {0xa, 0xb, 0xc, 0xd, 0xe, 0xf};
+    std::memcpy(&eth[6], src, 6);
+    put16(eth, 12, ethernet::Ethertype::IPV6);
+    v6[6] = ip::IpProtocol::UDP;
+    v6[8 + 15] = 1;  // source = ::1
+    put16(udp, 0, 6082);
+    put16(udp, 2, 6081);
+    put16(udp, 4, 128);
+    put16(udp, 6, 0xffff);
+    auto res = UdpParser::parse_read({eth, v6, udp, body});
+    auto& mystack = res.unwrap();
+    const auto& hdr = mystack.headers;
+    ASSERT_EQ(hdr.eth.source(), (MacAddr6{0xa, 0xb, 0xc, 0xd, 0xe, 0xf}));
+    ASSERT_EQ(hdr.eth.destination(), (MacAddr6{0xff, 0xff, 0xff, 0xff, 0xff, 0xff}));
+    ASSERT_EQ(hdr.eth.ethertype(), ethernet::Ethertype::IPV6);
+    ASSERT_TRUE(hdr.l3.ipv6.has_value());
+    ASSERT_EQ(hdr.l3.ipv6->next_header(), ip::IpProtocol::UDP);
+    ASSERT_EQ(hdr.l3.ipv6->next_layer(), ip::IpProtocol::UDP);
+    ASSERT_EQ(hdr.l3.ipv6->source()[15], 1);
+    ASSERT_EQ(hdr.l4.source(), 6082);
+    ASSERT_EQ(hdr.l4.destination(), 6081);
+    ASSERT_EQ(hdr.l4.length(), 128);
+    ASSERT_EQ(hdr.l4.checksum(), 0xffff);
+    ASSERT_TRUE(!mystack.last_chunk.has_value());
+    ASSERT_EQ(mystack.data.size(), 1u);
+    ASSERT_EQ(mystack.data[0].size(), 128u);
+    ASSERT_TRUE(std::all_of(mystack.data[0].begin(), mystack.data[0].end(),
+                            [](uint8_t v) { return v == 0xaa; }));
+}
+
+// ingot-examples/src/tests.rs:277-305 (the parse_read half)
+TEST(chunks_present_on_early_accept_read) {
+    std::vector<uint8_t> eth = {0xA8, 0x40, 0x25, 0x77, 0x77, 0x76, 0xA8,
+                                0x40, 0x25, 0x77, 0x77, 0x77, 0x08, 0x06};
+    std::vector<uint8_t> rest = {0, 1, 2, 3, 4, 5, 6, 7};
+    auto res = GenericUlp::parse_read({eth, rest});
+    auto& parsed = res.unwrap();
+    ASSERT_TRUE(parsed.last_chunk.has_value());
+    ASSERT_EQ(parsed.last_chunk->size(), 8u);
+    ASSERT_EQ(parsed.data.size(), 0u);
+}
+
+// ingot-examples/src/tests.rs:381-423
+TEST(straddle_failure) {
+    const auto v = would_be_valid();
+    const std::vector<uint8_t> a(v.begin(), v.begin() + 16), b(v.begin() + 16, v.end());
+    auto e = GenericUlp::parse_read({a, b}).unwrap_err();
+    ASSERT_EQ(e.error(), ParseError::StraddledHeader);
+    ASSERT_EQ(std::string(e.header()), "inner_l3");
+    e = GenericUlp::parse_read({a}).unwrap_err();
+    ASSERT_EQ(e.error(), ParseError::TooSmall);
+    ASSERT_EQ(std::string(e.header()), "inner_l3");
+}
+
 int main() {
     for (auto& [name, fn] : registry()) {
         ++g_run;

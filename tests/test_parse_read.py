@@ -107,6 +107,36 @@ def test_read_fuzz_bit_exact(ctx, torch, chain):
     assert (st == 0).any() and (st == ingot_amd.ParseError.StraddledHeader).any()
 
 
+def test_reference_read_tests_read_alike(torch):
+    """ingot-examples/src/tests.rs:120-187, 277-305, 381-423 via the mirror."""
+    eth = bytes([0xFF] * 6 + [0xA, 0xB, 0xC, 0xD, 0xE, 0xF]) + b"\x86\xdd"
+    v6 = bytearray(40)
+    v6[6] = 17
+    v6[23] = 1
+    udp = bytes([0x17, 0xC2, 0x17, 0xC1, 0, 128, 0xFF, 0xFF])
+    mystack = ingot_amd.UdpParser.parse_read([eth, bytes(v6), udp, b"\xaa" * 128])
+    hdr = mystack.headers
+    assert hdr.eth.source() == bytes([0xA, 0xB, 0xC, 0xD, 0xE, 0xF])
+    assert hdr.l3.next_header() == 17 and hdr.l3.next_layer() == 17
+    assert (hdr.l4.source(), hdr.l4.destination(), hdr.l4.length()) == (6082, 6081, 128)
+    assert mystack.last_chunk is None
+    assert mystack.data == [b"\xaa" * 128]
+
+    arp = bytes([0xA8, 0x40, 0x25, 0x77, 0x77, 0x76, 0xA8, 0x40, 0x25, 0x77, 0x77, 0x77, 8, 6])
+    parsed = ingot_amd.GenericUlp.parse_read([arp, bytes(range(8))])
+    assert len(parsed.last_chunk) == 8 and parsed.data == []
+
+    pkt = bytes.fromhex("aa000400ff10aa000400ff010800" "45000024000000" "00f0110000080808"
+                        "08c0a80005" "00800035" "00080000")
+    with pytest.raises(ingot_amd.PacketParseError) as e:
+        ingot_amd.GenericUlp.parse_read([pkt[:16], pkt[16:]])
+    assert (e.value.error(), e.value.header()) == (ingot_amd.ParseError.StraddledHeader,
+                                                   "inner_l3")
+    with pytest.raises(ingot_amd.PacketParseError) as e:
+        ingot_amd.GenericUlp.parse_read([pkt[:16]])
+    assert (e.value.error(), e.value.header()) == (ingot_amd.ParseError.TooSmall, "inner_l3")
+
+
 def test_read_single_chunk_matches_parse(ctx, torch):
     """Whole frames as single chunks, C3-style traffic: every record equals
     parse_slice's except where a non-final layer ends the frame."""
