@@ -19,7 +19,8 @@ hiding the ~1.5 us dependent-launch boundary.  Every step is still exactly
 one launch over one 1M-frame batch; `variants` reports S=1 and 8-B records.
 
 To measure HBM and not the 256 MiB Infinity Cache, step k reads arena copy
-k % R and writes record buffer k % R (R copies >= 512 MiB in total).
+k % R and writes record buffer k % R (R copies >= 512 MiB in total, R >= 4
+so concurrent launches on up to 4 streams never share data).
 
 `roofline.achieved` = algorithmic bytes per launch (R_i =
 min(len,128) + max(0, H_i-128) + D, W_i = record bytes) / (timed region / K),
@@ -325,7 +326,10 @@ def main():
     first, n = idist.shard(rank, world, n)
     arena, off, lens = ingot_amd.gen_frames(profile, n, first=first, stride=stride,
                                             device=local)
-    reps = max(1, -(-(args.rotate_mib << 20) // arena.numel()))
+    # >= 512 MiB of distinct arenas (the 256 MiB MALL cannot serve a step from
+    # the previous one), and >= 4 copies so that launches in flight on up to 4
+    # streams never read the same bytes (no cross-step cache sharing)
+    reps = max(4, -(-(args.rotate_mib << 20) // arena.numel()))
     arenas = [arena] + [arena.clone() for _ in range(reps - 1)]
     outs = [torch.empty((n, 16), dtype=torch.uint8, device=dev) for _ in range(reps)]
     torch.cuda.synchronize(dev)

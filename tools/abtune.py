@@ -39,7 +39,7 @@ def main():
     prof, n, stride, chain_name, _ = bench.CONFIGS[args.config]
     chain = Chain[chain_name]
     arena, off, lens = ingot_amd.gen_frames(GenProfile[prof], n, stride=stride)
-    reps = max(1, -(-(512 << 20) // arena.numel()))
+    reps = max(4, -(-(512 << 20) // arena.numel()))
     arenas = [arena] + [arena.clone() for _ in range(reps - 1)]
     outs = [torch.empty((n, 16), dtype=torch.uint8, device="cuda") for _ in range(reps)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(3)]
