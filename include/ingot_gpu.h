@@ -349,10 +349,16 @@ int ingot_gpu_ctx_device(const ingot_gpu_ctx* ctx);
  *                              (default 4 for slots <= 64 B, else 3)
  *   INGOT_TUNE_MAX_BLOCKS      grid cap in 256-thread blocks (0 = one
  *                              64-packet tile per wave)
+ *   INGOT_TUNE_PIPELINE        strided rings (slots >= 64 B) without a length
+ *                              array, 16- or 8-B records: the multi-tile kernel
+ *                              that stages the next tile while parsing one
+ *                              (double-buffered LDS).  0 = on, 2 blocks per CU
+ *                              (default); 1 = off; k >= 2 = k tiles per wave
  */
 #define INGOT_TUNE_WINDOW_INDEXED 1
 #define INGOT_TUNE_WINDOW_STRIDED 2
 #define INGOT_TUNE_MAX_BLOCKS 3
+#define INGOT_TUNE_PIPELINE 4
 int ingot_gpu_ctx_set_tuning(ingot_gpu_ctx* ctx, int key, int value);
 int ingot_gpu_ctx_get_tuning(const ingot_gpu_ctx* ctx, int key);
 

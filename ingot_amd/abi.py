@@ -73,6 +73,7 @@ MAX_GENEVE_OPT_FIELDS = 4
 TUNE_WINDOW_INDEXED = 1
 TUNE_WINDOW_STRIDED = 2
 TUNE_MAX_BLOCKS = 3
+TUNE_PIPELINE = 4
 
 
 class IngotRec(ctypes.Structure):

@@ -144,6 +144,7 @@ int ingot_gpu_ctx_create(int device, ingot_gpu_ctx** out) {
         return INGOT_GPU_ENODEV;
     ingot_gpu_ctx* c = new (std::nothrow) ingot_gpu_ctx{device, {}};
     if (!c) return INGOT_GPU_ENOMEM;
+    if (prop.multiProcessorCount > 0) c->tuning.cus = (uint32_t)prop.multiProcessorCount;
     *out = c;
     return INGOT_GPU_SUCCESS;
 }
@@ -157,6 +158,7 @@ int ingot_gpu_ctx_set_tuning(ingot_gpu_ctx* ctx, int key, int value) {
     switch (key) {
     case INGOT_TUNE_WINDOW_INDEXED: ctx->tuning.window_indexed = value; break;
     case INGOT_TUNE_WINDOW_STRIDED: ctx->tuning.window_strided = value; break;
+    case INGOT_TUNE_PIPELINE: ctx->tuning.pipeline = value; break;
     default: ctx->tuning.max_blocks = (uint32_t)value; break;
     }
     return INGOT_GPU_SUCCESS;
@@ -168,6 +170,7 @@ int ingot_gpu_ctx_get_tuning(const ingot_gpu_ctx* ctx, int key) {
     case INGOT_TUNE_WINDOW_INDEXED: return ctx->tuning.window_indexed;
     case INGOT_TUNE_WINDOW_STRIDED: return ctx->tuning.window_strided;
     case INGOT_TUNE_MAX_BLOCKS: return (int)ctx->tuning.max_blocks;
+    case INGOT_TUNE_PIPELINE: return ctx->tuning.pipeline;
     default: return INGOT_GPU_EINVAL;
     }
 }

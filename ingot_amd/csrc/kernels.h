@@ -63,6 +63,8 @@ struct Tuning {
     int window_indexed = 0;
     int window_strided = 0;
     uint32_t max_blocks = 0;
+    int pipeline = 0;  // ring kernel: 0 = auto (2 blocks per CU), 1 = off, k = k tiles per wave
+    uint32_t cus = 256;  // compute units of the context's device (grid shaping)
 };
 
 hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, int mode,
