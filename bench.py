@@ -417,6 +417,10 @@ def main():
     launch_ms = ms_iso / iso_steps
     achieved = bytes_launch / (launch_ms / 1e3) / 1e9
     ok_frac = float((recs_np["status"] == 0).mean())
+    # the multi-tile ring kernel serves slot rings without a length array
+    # (launch_parse in parse.hip); everything else is the one-tile k_parse
+    ring = (mode == "parse" and stride is not None and stride >= 64 and lens is None
+            and chain != Chain.GeneveOverV6Tunnel)
     traffic = None
     pmc = sorted(ROOT.glob(f"profiles/*_pmc_{args.config}.json"))
     if pmc and args.record == 16:
@@ -497,7 +501,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic["bytes_per_launch"] if traffic else None,
                 "traffic_detail": traffic,
-                "kernel": "k_parse (ingot_amd/csrc/parse.hip)" + {
+                "kernel": ("k_parse_pipe" if ring else "k_parse") + " (ingot_amd/csrc/parse.hip)" + {
                     "modify": ", OUT_MODIFY", "read": ", LAYOUT_SEGMENTED",
                     "flows": ", OUT_FLOWS + k_flow_hist"}.get(mode, ""),
                 "launch_mean_us": round(launch_ms * 1e3, 3),

@@ -354,11 +354,20 @@ int ingot_gpu_ctx_device(const ingot_gpu_ctx* ctx);
  *                              that stages the next tile while parsing one
  *                              (double-buffered LDS).  0 = on, 2 blocks per CU
  *                              (default); 1 = off; k >= 2 = k tiles per wave
+ *   INGOT_TUNE_CACHE_POLICY    0 = measured default (non-temporal record
+ *                              stores; non-temporal staging loads in the
+ *                              ring kernel only); else bit 0: stage frame
+ *                              bytes with non-temporal loads, bit 1:
+ *                              non-temporal record stores (4 = neither)
+ *   INGOT_TUNE_PIPE_DEPTH      the multi-tile ring kernel's tiles in flight
+ *                              per wave (LDS images): 2 (default), 3 or 4
  */
 #define INGOT_TUNE_WINDOW_INDEXED 1
 #define INGOT_TUNE_WINDOW_STRIDED 2
 #define INGOT_TUNE_MAX_BLOCKS 3
 #define INGOT_TUNE_PIPELINE 4
+#define INGOT_TUNE_CACHE_POLICY 5
+#define INGOT_TUNE_PIPE_DEPTH 6
 int ingot_gpu_ctx_set_tuning(ingot_gpu_ctx* ctx, int key, int value);
 int ingot_gpu_ctx_get_tuning(const ingot_gpu_ctx* ctx, int key);
 

@@ -74,6 +74,8 @@ TUNE_WINDOW_INDEXED = 1
 TUNE_WINDOW_STRIDED = 2
 TUNE_MAX_BLOCKS = 3
 TUNE_PIPELINE = 4
+TUNE_CACHE_POLICY = 5
+TUNE_PIPE_DEPTH = 6
 
 
 class IngotRec(ctypes.Structure):

@@ -159,6 +159,8 @@ int ingot_gpu_ctx_set_tuning(ingot_gpu_ctx* ctx, int key, int value) {
     case INGOT_TUNE_WINDOW_INDEXED: ctx->tuning.window_indexed = value; break;
     case INGOT_TUNE_WINDOW_STRIDED: ctx->tuning.window_strided = value; break;
     case INGOT_TUNE_PIPELINE: ctx->tuning.pipeline = value; break;
+    case INGOT_TUNE_CACHE_POLICY: ctx->tuning.cache_policy = value; break;
+    case INGOT_TUNE_PIPE_DEPTH: ctx->tuning.pipe_depth = value; break;
     default: ctx->tuning.max_blocks = (uint32_t)value; break;
     }
     return INGOT_GPU_SUCCESS;
@@ -171,6 +173,8 @@ int ingot_gpu_ctx_get_tuning(const ingot_gpu_ctx* ctx, int key) {
     case INGOT_TUNE_WINDOW_STRIDED: return ctx->tuning.window_strided;
     case INGOT_TUNE_MAX_BLOCKS: return (int)ctx->tuning.max_blocks;
     case INGOT_TUNE_PIPELINE: return ctx->tuning.pipeline;
+    case INGOT_TUNE_CACHE_POLICY: return ctx->tuning.cache_policy;
+    case INGOT_TUNE_PIPE_DEPTH: return ctx->tuning.pipe_depth;
     default: return INGOT_GPU_EINVAL;
     }
 }

@@ -31,6 +31,7 @@ struct ParseArgs {
     void* out;             // n records of the OutMode's type
     const uint32_t* pkt_seg = nullptr;  // LAYOUT_SEGMENTED: n+1 chunk-index bounds
     uint16_t* chunk = nullptr;          // LAYOUT_SEGMENTED, optional: remainder's chunk
+    uint32_t policy = 0;                // INGOT_TUNE_CACHE_POLICY bits (launch_parse sets it)
 };
 
 struct FlowArgs {
@@ -64,6 +65,8 @@ struct Tuning {
     int window_strided = 0;
     uint32_t max_blocks = 0;
     int pipeline = 0;  // ring kernel: 0 = auto (2 blocks per CU), 1 = off, k = k tiles per wave
+    int pipe_depth = 0;    // ring kernel: tiles in flight per wave (0 = 2)
+    int cache_policy = 0;  // bit 0: nt staging loads; bit 1: nt record stores
     uint32_t cus = 256;  // compute units of the context's device (grid shaping)
 };
 

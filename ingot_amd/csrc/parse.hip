@@ -47,6 +47,38 @@ constexpr uint32_t BLOCK = WAVE * WAVES;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) void lds_void;
 
+// HBM -> LDS staging of one 16-B chunk per lane (LDS-DMA).  `nt` (uniform,
+// INGOT_TUNE_CACHE_POLICY bit 0) marks the frame bytes non-temporal: they are
+// read once per launch.
+__device__ __forceinline__ void stage16(const uint8_t* src, uint32_t* dst, bool nt) {
+    if (nt) __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)dst, 16, 0, 2);
+    else __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)dst, 16, 0, 0);
+}
+
+// One record per lane; `nt` = INGOT_TUNE_CACHE_POLICY bit 1.  The nt store
+// is written as asm: with a plain-store twin in the other branch the compiler
+// merges the two and drops the nontemporal hint.  (An extra store the waitcnt
+// pass cannot see only makes its vmcnt waits stricter; the s_nop covers the
+// store-data VGPR hazard the hazard recognizer cannot see in asm.)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void store_rec(uint4* dst, const uint4& v, bool nt) {
+    if (nt) {
+        const u32x4 x{v.x, v.y, v.z, v.w};
+        asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(dst), "v"(x) : "memory");
+    } else {
+        *dst = v;
+    }
+}
+__device__ __forceinline__ void store_rec(uint2* dst, const uint2& v, bool nt) {
+    if (nt) {
+        const u32x2 x{v.x, v.y};
+        asm volatile("global_store_dwordx2 %0, %1, off nt\n\ts_nop 1" ::"v"(dst), "v"(x) : "memory");
+    } else {
+        *dst = v;
+    }
+}
+
 // Slot (16-B unit) of chunk c of packet p inside a wave's LDS image.
 // NCH = 4: g(p) = (p>>2)&3; NCH = 8: g(p) = (p>>1)&7 (see header comment);
 // other NCH: linear.
@@ -843,10 +875,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
             } else {
                 bp = (uint64_t)__shfl((long long)base, (int)pp);
             }
-            if (c < np) {
-                __builtin_amdgcn_global_load_lds((const void*)(a.arena + bp + 16u * c),
-                                                 (lds_void*)(wimg + k * WAVE * 4u), 16, 0, 0);
-            }
+            if (c < np) stage16(a.arena + bp + 16u * c, wimg + k * WAVE * 4u, a.policy & 1u);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
@@ -889,7 +918,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
             }
         } else if constexpr (MODE == OUT_REC8) {
             walk<CHAIN, false>(fr, r, nullptr, nullptr);
-            if (valid) static_cast<uint2*>(a.out)[i] = pack8(r);
+            if (valid) store_rec(static_cast<uint2*>(a.out) + i, pack8(r), a.policy & 2u);
         } else if constexpr (MODE == OUT_MODIFY) {
             // parse, then the setters in order (each sees the previous
             // edits' bytes: put8 updates HBM and the staged window)
@@ -923,7 +952,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
             }
         } else {
             walk<CHAIN, false>(fr, r, nullptr, nullptr);
-            if (valid) static_cast<uint4*>(a.out)[i] = pack(r);
+            if (valid) store_rec(static_cast<uint4*>(a.out) + i, pack(r), a.policy & 2u);
         }
         if constexpr (LAYOUT == LAYOUT_SEGMENTED) {
             if (valid && a.chunk) a.chunk[i] = (uint16_t)fr.k;
@@ -934,23 +963,22 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
 }
 
 // Pipelined variant for fixed slots with no length array (C2-style rings):
-// each wave walks several tiles and issues the next tile's LDS-DMA into the
-// other buffer before parsing the current one, so its loads stay in flight
-// while it parses.  Two distinct LDS arrays keep the buffers' roles static
-// (the loop is unrolled by two).  Requires stride >= 16*NCH.
-template <uint32_t NCH, int CHAIN, int MODE>
+// each wave walks several tiles and keeps the next DEPTH-1 tiles' LDS-DMA in
+// flight while it parses the current one (DEPTH LDS images per wave, used
+// round robin).  Requires stride >= 16*NCH.
+template <uint32_t NCH, uint32_t DEPTH, int CHAIN, int MODE>
 __global__ __launch_bounds__(BLOCK) void k_parse_pipe(ParseArgs a) {
     constexpr uint32_t WIN = NCH * 16u;
     constexpr uint32_t WAVE_DW = WAVE * NCH * 4u;
-    __shared__ __attribute__((aligned(16))) uint32_t s_a[WAVES * WAVE_DW + 16];
-    __shared__ __attribute__((aligned(16))) uint32_t s_b[WAVES * WAVE_DW + 16];
+    constexpr uint32_t IMG_DW = WAVES * WAVE_DW + 16u;
+    __shared__ __attribute__((aligned(16))) uint32_t s_img[DEPTH * IMG_DW];
     const uint32_t lane = threadIdx.x & (WAVE - 1u);
     const uint32_t wave = threadIdx.x / WAVE;
-    uint32_t* img_a = s_a + wave * WAVE_DW;
-    uint32_t* img_b = s_b + wave * WAVE_DW;
+    uint32_t* img0 = s_img + wave * WAVE_DW;
     const uint64_t ntiles = (a.n + WAVE - 1u) / WAVE;
     const uint64_t step = (uint64_t)gridDim.x * WAVES;
     const uint32_t take = a.stride < WIN ? a.stride : WIN;
+    const bool nt_ld = a.policy & 1u, nt_st = a.policy & 2u;
 
     auto stage = [&](uint64_t tt, uint32_t* img) {
 #pragma unroll
@@ -960,8 +988,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse_pipe(ParseArgs a) {
             const uint32_t c = (q - pp * NCH) ^ swz<NCH>(pp);
             uint64_t slot = tt * WAVE + pp;
             if (slot >= a.n) slot = a.n - 1u;  // a valid address for the tail tile
-            __builtin_amdgcn_global_load_lds((const void*)(a.arena + slot * a.stride + 16u * c),
-                                             (lds_void*)(img + k * WAVE * 4u), 16, 0, 0);
+            stage16(a.arena + slot * a.stride + 16u * c, img + k * WAVE * 4u, nt_ld);
         }
     };
     auto parse = [&](uint64_t tt, const uint32_t* img) {
@@ -970,51 +997,46 @@ __global__ __launch_bounds__(BLOCK) void k_parse_pipe(ParseArgs a) {
         Rec r;
         walk<CHAIN, false>(fr, r, nullptr, nullptr);
         if (i < a.n) {
-            if constexpr (MODE == OUT_REC8) static_cast<uint2*>(a.out)[i] = pack8(r);
-            else static_cast<uint4*>(a.out)[i] = pack(r);
+            if constexpr (MODE == OUT_REC8) store_rec(static_cast<uint2*>(a.out) + i, pack8(r), nt_st);
+            else store_rec(static_cast<uint4*>(a.out) + i, pack(r), nt_st);
         }
     };
 
     uint64_t t = (uint64_t)blockIdx.x * WAVES + wave;
     if (t >= ntiles) return;
-    stage(t, img_a);
-    for (;;) {
-        uint64_t tn = t + step;
+    // prologue: the first DEPTH-1 tiles
+#pragma unroll
+    for (uint32_t d = 0; d + 1u < DEPTH; ++d)
+        if (t + d * step < ntiles) stage(t + d * step, img0 + d * IMG_DW);
+    for (uint32_t j = 0;; ++j) {
+        const uint64_t tn = t + (DEPTH - 1u) * step;
         if (tn < ntiles) {
-            stage(tn, img_b);
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NCH) : "memory");
+            stage(tn, img0 + ((j + DEPTH - 1u) % DEPTH) * IMG_DW);
+            // everything but the youngest DEPTH-1 tiles' loads has landed
+            // (record stores count too, so this is conservative)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DEPTH - 1u) * NCH) : "memory");
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        parse(t, img_a);
-        if (tn >= ntiles) break;
-        t = tn;
-        tn = t + step;
-        if (tn < ntiles) {
-            stage(tn, img_a);
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NCH) : "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        parse(t, img_b);
-        if (tn >= ntiles) break;
-        t = tn;
+        parse(t, img0 + (j % DEPTH) * IMG_DW);
+        t += step;
+        if (t >= ntiles) break;
     }
 }
 
-template <uint32_t NCH, int MODE>
+template <uint32_t NCH, uint32_t DEPTH, int MODE>
 hipError_t launch_pipe(const ParseArgs& a, int chain, uint32_t grid, hipStream_t s) {
     switch (chain) {
     case INGOT_CHAIN_UDP_PARSER:
-        hipLaunchKernelGGL((k_parse_pipe<NCH, INGOT_CHAIN_UDP_PARSER, MODE>), dim3(grid),
+        hipLaunchKernelGGL((k_parse_pipe<NCH, DEPTH, INGOT_CHAIN_UDP_PARSER, MODE>), dim3(grid),
                            dim3(BLOCK), 0, s, a);
         break;
     case INGOT_CHAIN_GENERIC_ULP:
-        hipLaunchKernelGGL((k_parse_pipe<NCH, INGOT_CHAIN_GENERIC_ULP, MODE>), dim3(grid),
+        hipLaunchKernelGGL((k_parse_pipe<NCH, DEPTH, INGOT_CHAIN_GENERIC_ULP, MODE>), dim3(grid),
                            dim3(BLOCK), 0, s, a);
         break;
     case INGOT_CHAIN_VLAN_ULP:
-        hipLaunchKernelGGL((k_parse_pipe<NCH, INGOT_CHAIN_VLAN_ULP, MODE>), dim3(grid),
+        hipLaunchKernelGGL((k_parse_pipe<NCH, DEPTH, INGOT_CHAIN_VLAN_ULP, MODE>), dim3(grid),
                            dim3(BLOCK), 0, s, a);
         break;
     default:
@@ -1072,9 +1094,23 @@ uint32_t grid_for(uint64_t n, uint32_t max_blocks) {
 
 }  // namespace
 
-hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, int mode,
+hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int mode,
                         const Tuning& t, hipStream_t s) {
-    if (a.n == 0) return hipSuccess;
+    if (args.n == 0) return hipSuccess;
+    ParseArgs a = args;
+    // Cache policy (INGOT_TUNE_CACHE_POLICY; measured on MI355X, interleaved
+    // A/B): records are written once and never re-read by the
+    // kernel, so they are stored non-temporal by default (C3 609 -> 600,
+    // C3s 130 -> 127, C4 321 -> 316, C6 399 -> 395 us/step).  Frame bytes are
+    // staged non-temporal only by the ring kernel, whose window is the whole
+    // 64-B slot (C2 single stream 16.8 -> 15.1 us, two streams 13.5 -> 12.2);
+    // elsewhere bytes past the window are re-read from L2, and nt staging
+    // costs 19% (C3) / 15% (C3s).  4 = plain loads and stores.
+    const bool ring = t.pipeline != 1 && !t.window_strided && layout_kind == LAYOUT_STRIDED &&
+                      !a.len && chain != INGOT_CHAIN_GENEVE_OVER_V6 && a.stride >= 64u &&
+                      (mode == OUT_REC16 || mode == OUT_REC8);
+    if (t.cache_policy == 0) a.policy = mode == OUT_FIELDS ? 0u : ring ? 3u : 2u;
+    else a.policy = (uint32_t)t.cache_policy & 3u;
     const uint32_t g = grid_for(a.n, t.max_blocks);
     // parse_read over chunk lists: chunk 0 staged in a 4-chunk (64-B) window
     // (first mblk-style chunks are short header blocks), the rest from L2/HBM.
@@ -1099,8 +1135,7 @@ hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, int mode
     // 64 B, interleaved A/B): 16.6-16.7 vs 18.6-18.8 us per launch on one
     // stream, 13.5-13.6 vs 14.2-14.4 us per step on two; 6 or 12 tiles per
     // wave (uneven over the CUs) lose most of it.
-    if (t.pipeline != 1 && !t.window_strided && layout_kind == LAYOUT_STRIDED && !a.len && !tun &&
-        a.stride >= 64u && (mode == OUT_REC16 || mode == OUT_REC8)) {
+    if (ring) {
         const uint64_t tiles = (a.n + WAVE - 1) / WAVE;
         uint64_t blocks;
         if (t.pipeline > 1) {
@@ -1112,8 +1147,14 @@ hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, int mode
             if (blocks > cap) blocks = cap;
         }
         const uint32_t pg = (uint32_t)(blocks ? blocks : 1);
-        return mode == OUT_REC8 ? launch_pipe<4, OUT_REC8>(a, chain, pg, s)
-                                : launch_pipe<4, OUT_REC16>(a, chain, pg, s);
+        if (t.pipe_depth == 3)
+            return mode == OUT_REC8 ? launch_pipe<4, 3, OUT_REC8>(a, chain, pg, s)
+                                    : launch_pipe<4, 3, OUT_REC16>(a, chain, pg, s);
+        if (t.pipe_depth == 4)
+            return mode == OUT_REC8 ? launch_pipe<4, 4, OUT_REC8>(a, chain, pg, s)
+                                    : launch_pipe<4, 4, OUT_REC16>(a, chain, pg, s);
+        return mode == OUT_REC8 ? launch_pipe<4, 2, OUT_REC8>(a, chain, pg, s)
+                                : launch_pipe<4, 2, OUT_REC16>(a, chain, pg, s);
     }
     if (layout_kind == LAYOUT_STRIDED) {
         const int w = t.window_strided ? t.window_strided
@@ -1185,6 +1226,10 @@ bool tuning_valid(int key, int value) {
         return value >= 0;
     case INGOT_TUNE_PIPELINE:
         return value >= 0 && value <= 64;
+    case INGOT_TUNE_CACHE_POLICY:
+        return value >= 0 && value <= 4;
+    case INGOT_TUNE_PIPE_DEPTH:
+        return value == 0 || (value >= 2 && value <= 4);
     default:
         return false;
     }

@@ -1,25 +1,32 @@
-"""The double-buffered ring kernel (INGOT_TUNE_PIPELINE; on by default for
-slot rings without a length array) returns exactly the oracle's records, for
-every tiles-per-wave setting, the auto grid (0) and the one-tile kernel (1)."""
+"""The multi-tile ring kernel (INGOT_TUNE_PIPELINE; on by default for slot
+rings without a length array) returns exactly the oracle's records, for every
+tiles-per-wave setting, the auto grid (0) and the one-tile kernel (1), every
+pipeline depth (INGOT_TUNE_PIPE_DEPTH) and cache policy
+(INGOT_TUNE_CACHE_POLICY)."""
 import pytest
 
 import ingot_amd
 import oracle
 from ingot_amd import Chain, GenProfile
-from ingot_amd.abi import TUNE_PIPELINE
+from ingot_amd.abi import TUNE_CACHE_POLICY, TUNE_PIPE_DEPTH, TUNE_PIPELINE
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("tpw", [0, 1, 2, 3, 8, 16])
+@pytest.mark.parametrize("tpw,depth,pol", [(0, 0, 0), (1, 0, 0), (2, 0, 0), (3, 0, 0),
+                                           (8, 0, 0), (16, 0, 0), (0, 3, 0), (2, 3, 1),
+                                           (5, 3, 2), (0, 4, 3), (3, 4, 0), (1, 0, 3),
+                                           (0, 0, 4), (1, 0, 4)])
 @pytest.mark.parametrize("n", [1, 63, 65, 100_003, 1 << 20])
-def test_pipelined_ring_bit_exact(tpw, n):
+def test_pipelined_ring_bit_exact(tpw, depth, pol, n):
     import torch
 
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     ctx = ingot_amd.Context(0)
     ctx.set_tuning(TUNE_PIPELINE, tpw)
+    ctx.set_tuning(TUNE_PIPE_DEPTH, depth)
+    ctx.set_tuning(TUNE_CACHE_POLICY, pol)
     for prof, stride in ((GenProfile.V4UDP64, 64), (GenProfile.ADVERSARIAL, 64),
                          (GenProfile.MIXED, 128)):
         arena, _, _ = ingot_amd.gen_frames(prof, n, seed=n + tpw, stride=stride)

@@ -6,7 +6,8 @@ cross-process/device variance that looks like a kernel property).
     python tools/abtune.py --config c3 --var win_i=4 --var win_i=5 --var win_i=9
     python tools/abtune.py --config c2 --var streams=1 --var streams=2 --var rec=8
 
-A variant is a comma list of key=value: win_i, win_s, blocks, pipe, streams, rec.
+A variant is a comma list of key=value: win_i, win_s, blocks, pipe, depth, pol,
+streams, rec.
 """
 from __future__ import annotations
 
@@ -34,8 +35,8 @@ def main():
     import bench
     import ingot_amd
     from ingot_amd import Chain, GenProfile
-    from ingot_amd.abi import (TUNE_MAX_BLOCKS, TUNE_PIPELINE, TUNE_WINDOW_INDEXED,
-                               TUNE_WINDOW_STRIDED)
+    from ingot_amd.abi import (TUNE_CACHE_POLICY, TUNE_MAX_BLOCKS, TUNE_PIPE_DEPTH,
+                               TUNE_PIPELINE, TUNE_WINDOW_INDEXED, TUNE_WINDOW_STRIDED)
 
     prof, n, stride, chain_name, _ = bench.CONFIGS[args.config]
     chain = Chain[chain_name]
@@ -59,6 +60,10 @@ def main():
             ctx.set_tuning(TUNE_MAX_BLOCKS, int(kv["blocks"]))
         if "pipe" in kv:
             ctx.set_tuning(TUNE_PIPELINE, int(kv["pipe"]))
+        if "depth" in kv:
+            ctx.set_tuning(TUNE_PIPE_DEPTH, int(kv["depth"]))
+        if "pol" in kv:
+            ctx.set_tuning(TUNE_CACHE_POLICY, int(kv["pol"]))
         ns, rb = int(kv.get("streams", 1)), int(kv.get("rec", 16))
         runners[v] = (ctx, bench.Runner(torch, lib, ctx, chain, n, stride, arenas, off, lens,
                                         outs, streams[:ns], rb))

@@ -33,7 +33,7 @@ def run_pass(counter: str, config: str, outdir: Path, steps: int) -> list[float]
            "--", sys.executable, str(ROOT / "bench.py"), "--config", config, "--steps", str(steps),
            "--warmup", "2", "--streams", "1", "--no-cpu-baseline", "--no-variants"]
     env = dict(os.environ, TMPDIR="/tmp")
-    r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=900)
+    r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=180)
     (d / "rocprof.log").write_text(r.stdout + "\n" + r.stderr)
     if r.returncode != 0:
         raise RuntimeError(f"rocprofv3 failed ({r.returncode}); see {d}/rocprof.log")
@@ -41,6 +41,7 @@ def run_pass(counter: str, config: str, outdir: Path, steps: int) -> list[float]
     if not files:
         raise RuntimeError(f"no counter_collection.csv under {d}")
     vals = {}
+    names = {}
     with open(files[0]) as f:
         for row in csv.DictReader(f):
             if "k_parse" not in row.get("Kernel_Name", ""):
@@ -49,7 +50,12 @@ def run_pass(counter: str, config: str, outdir: Path, steps: int) -> list[float]
                 continue
             key = row.get("Dispatch_Id") or row.get("Correlation_Id") or str(len(vals))
             vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
+            names[key] = row["Kernel_Name"]
+    KERNELS.update(names.values())
     return list(vals.values())
+
+
+KERNELS: set = set()
 
 
 def main():
@@ -67,7 +73,7 @@ def main():
     w_kib = sorted(write)[len(write) // 2]
     res = {
         "config": args.config,
-        "kernel": "k_parse",
+        "kernels": sorted(KERNELS),
         "dispatches": [len(fetch), len(write)],
         "FETCH_SIZE_KiB_median": f_kib,
         "WRITE_SIZE_KiB_median": w_kib,
