@@ -145,3 +145,44 @@ extern "C" int gather_run(int which, const void* arena, const void* off, const v
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// --- fetch-granularity probe (config-3 frames): per packet, NSEG aligned
+// segments of SEG bytes starting at off & ~(SEG-1), read as 16-B register
+// loads; one 16-B record per packet.  Tells whether HBM traffic follows the
+// bytes requested (32/64-B sectors) or whole 128-B lines.
+template <int SEG, int NSEG>
+__global__ __launch_bounds__(256) void k_gather_seg(const uint8_t* __restrict__ arena,
+                                                    const uint64_t* __restrict__ off,
+                                                    const uint16_t* __restrict__ len,
+                                                    uint4* __restrict__ out, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t o = off[i];
+    const uint4* p = reinterpret_cast<const uint4*>(arena + (o & ~(uint64_t)(SEG - 1)));
+    uint4 acc = make_uint4(len[i], 0, 0, 0);
+#pragma unroll
+    for (int c = 0; c < SEG * NSEG / 16; ++c) {
+        const uint4 v = p[c];
+        acc.x ^= v.x; acc.y ^= v.y; acc.z ^= v.z; acc.w ^= v.w;
+    }
+    out[i] = acc;
+}
+
+extern "C" int seg_run(int which, const void* arena, const void* off, const void* len, void* out,
+                       uint64_t n, void* stream) {
+    const hipStream_t s = (hipStream_t)stream;
+    const uint32_t g1 = (uint32_t)((n + 255) / 256);
+    const auto* a = (const uint8_t*)arena;
+    const auto* o = (const uint64_t*)off;
+    const auto* l = (const uint16_t*)len;
+    auto* r = (uint4*)out;
+    switch (which) {
+    case 0: hipLaunchKernelGGL((k_gather_seg<32, 1>), dim3(g1), dim3(256), 0, s, a, o, l, r, n); break;
+    case 1: hipLaunchKernelGGL((k_gather_seg<64, 1>), dim3(g1), dim3(256), 0, s, a, o, l, r, n); break;
+    case 2: hipLaunchKernelGGL((k_gather_seg<64, 2>), dim3(g1), dim3(256), 0, s, a, o, l, r, n); break;
+    case 3: hipLaunchKernelGGL((k_gather_seg<128, 1>), dim3(g1), dim3(256), 0, s, a, o, l, r, n); break;
+    case 4: hipLaunchKernelGGL((k_gather_seg<128, 2>), dim3(g1), dim3(256), 0, s, a, o, l, r, n); break;
+    default: hipLaunchKernelGGL((k_gather_seg<32, 2>), dim3(g1), dim3(256), 0, s, a, o, l, r, n); break;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
