@@ -361,6 +361,10 @@ int ingot_gpu_ctx_device(const ingot_gpu_ctx* ctx);
  *                              non-temporal record stores (4 = neither)
  *   INGOT_TUNE_PIPE_DEPTH      the multi-tile ring kernel's tiles in flight
  *                              per wave (LDS images): 2 (default), 3 or 4
+ *                              (the rewrite ring kernel: 2 or 3)
+ *   INGOT_TUNE_WRITEBACK       ingot_gpu_parse_modify on slot rings: bytes
+ *                              written back per edited unit, 16, 32 or 64
+ *                              (0 = measured default)
  */
 #define INGOT_TUNE_WINDOW_INDEXED 1
 #define INGOT_TUNE_WINDOW_STRIDED 2
@@ -368,6 +372,7 @@ int ingot_gpu_ctx_device(const ingot_gpu_ctx* ctx);
 #define INGOT_TUNE_PIPELINE 4
 #define INGOT_TUNE_CACHE_POLICY 5
 #define INGOT_TUNE_PIPE_DEPTH 6
+#define INGOT_TUNE_WRITEBACK 7
 int ingot_gpu_ctx_set_tuning(ingot_gpu_ctx* ctx, int key, int value);
 int ingot_gpu_ctx_get_tuning(const ingot_gpu_ctx* ctx, int key);
 

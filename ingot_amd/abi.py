@@ -76,6 +76,7 @@ TUNE_MAX_BLOCKS = 3
 TUNE_PIPELINE = 4
 TUNE_CACHE_POLICY = 5
 TUNE_PIPE_DEPTH = 6
+TUNE_WRITEBACK = 7
 
 
 class IngotRec(ctypes.Structure):

@@ -161,6 +161,7 @@ int ingot_gpu_ctx_set_tuning(ingot_gpu_ctx* ctx, int key, int value) {
     case INGOT_TUNE_PIPELINE: ctx->tuning.pipeline = value; break;
     case INGOT_TUNE_CACHE_POLICY: ctx->tuning.cache_policy = value; break;
     case INGOT_TUNE_PIPE_DEPTH: ctx->tuning.pipe_depth = value; break;
+    case INGOT_TUNE_WRITEBACK: ctx->tuning.writeback = value; break;
     default: ctx->tuning.max_blocks = (uint32_t)value; break;
     }
     return INGOT_GPU_SUCCESS;
@@ -175,6 +176,7 @@ int ingot_gpu_ctx_get_tuning(const ingot_gpu_ctx* ctx, int key) {
     case INGOT_TUNE_PIPELINE: return ctx->tuning.pipeline;
     case INGOT_TUNE_CACHE_POLICY: return ctx->tuning.cache_policy;
     case INGOT_TUNE_PIPE_DEPTH: return ctx->tuning.pipe_depth;
+    case INGOT_TUNE_WRITEBACK: return ctx->tuning.writeback;
     default: return INGOT_GPU_EINVAL;
     }
 }

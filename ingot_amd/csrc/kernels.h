@@ -52,6 +52,7 @@ struct Edit {
 };
 struct ModifyArgs {
     ParseArgs p;
+    uint32_t wb = 32;  // ring kernel: write-back unit in bytes (16, 32, 64)
     uint32_t n_edits;
     Edit e[INGOT_MAX_EDITS];
 };
@@ -66,6 +67,7 @@ struct Tuning {
     uint32_t max_blocks = 0;
     int pipeline = 0;  // ring kernel: 0 = auto (2 blocks per CU), 1 = off, k = k tiles per wave
     int pipe_depth = 0;    // ring kernel: tiles in flight per wave (0 = 2)
+    int writeback = 0;     // ring rewrite kernel: write-back unit (0 = measured default)
     int cache_policy = 0;  // bit 0: nt staging loads; bit 1: nt record stores
     uint32_t cus = 256;  // compute units of the context's device (grid shaping)
 };

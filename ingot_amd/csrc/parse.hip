@@ -1024,6 +1024,143 @@ __global__ __launch_bounds__(BLOCK) void k_parse_pipe(ParseArgs a) {
     }
 }
 
+// In-place rewrite on a slot ring (C2m: the reference's parse-and-decr-v4):
+// k_parse_pipe's multi-tile staging, then the setters edit the staged copy
+// (put_staged) and mark the write-back units they touch; the wave writes the
+// dirty 16-B chunks back lane-linearly from its LDS image — the inverse of the
+// staging map, so one store instruction covers 16 consecutive slots instead
+// of 64 scattered ones.  Write-back unit `a.wb` bytes (16, 32 or 64, aligned
+// within the slot); slots >= 64 B, the whole window inside every frame.
+template <uint32_t NCH, uint32_t DEPTH, int CHAIN>
+__global__ __launch_bounds__(BLOCK) void k_modify_pipe(ModifyArgs m) {
+    const ParseArgs& a = m.p;
+    constexpr uint32_t WIN = NCH * 16u;
+    constexpr uint32_t WAVE_DW = WAVE * NCH * 4u;
+    constexpr uint32_t IMG_DW = WAVES * WAVE_DW + 16u;
+    __shared__ __attribute__((aligned(16))) uint32_t s_img[DEPTH * IMG_DW];
+    const uint32_t lane = threadIdx.x & (WAVE - 1u);
+    const uint32_t wave = threadIdx.x / WAVE;
+    uint32_t* img0 = s_img + wave * WAVE_DW;
+    const uint64_t ntiles = (a.n + WAVE - 1u) / WAVE;
+    const uint64_t step = (uint64_t)gridDim.x * WAVES;
+    const bool nt_ld = a.policy & 1u;
+    uint8_t* arena = const_cast<uint8_t*>(a.arena);
+    const uint32_t unit_ch = m.wb / 16u;  // chunks per write-back unit
+
+    auto stage = [&](uint64_t tt, uint32_t* img) {
+#pragma unroll
+        for (uint32_t k = 0; k < NCH; ++k) {
+            const uint32_t q = k * WAVE + lane;
+            const uint32_t pp = q / NCH;
+            const uint32_t c = (q - pp * NCH) ^ swz<NCH>(pp);
+            uint64_t slot = tt * WAVE + pp;
+            if (slot >= a.n) slot = a.n - 1u;
+            stage16(a.arena + slot * a.stride + 16u * c, img + k * WAVE * 4u, nt_ld);
+        }
+    };
+    auto modify = [&](uint64_t tt, uint32_t* img) {
+        const uint64_t i = tt * WAVE + lane;
+        const bool valid = i < a.n;
+        uint8_t* frame = arena + (valid ? i : 0) * a.stride;
+        Frame<NCH> fr{(const lds_u32*)img, lane, 0u, WIN, a.stride, frame};
+        Rec r;
+        walk<CHAIN, false>(fr, r, nullptr, nullptr);
+        uint32_t dirty = 0;
+        if (valid && r.status == INGOT_OK) {
+            for (uint32_t k = 0; k < m.n_edits; ++k) {
+                const Edit& e = m.e[k];
+                uint32_t h;
+                if (!header_at<CHAIN>(r, e.layer, e.kind, e.index, h)) continue;
+                // the setter (bitfield.rs:188-315): read-modify-write of the
+                // covering bytes through the staged copy
+                uint64_t w = fr.be(h + e.byte0, e.nbytes);
+                const uint32_t fm = e.bits >= 32 ? 0xffffffffu : ((1u << e.bits) - 1u);
+                const uint32_t cur = (uint32_t)(w >> e.rshift) & fm;
+                uint32_t v;
+                switch (e.op) {
+                case INGOT_OP_ADD: v = cur + e.value; break;
+                case INGOT_OP_SUB: v = cur - e.value; break;
+                case INGOT_OP_AND: v = cur & e.value; break;
+                case INGOT_OP_OR: v = cur | e.value; break;
+                case INGOT_OP_XOR: v = cur ^ e.value; break;
+                default: v = e.value; break;
+                }
+                w = (w & ~((uint64_t)fm << e.rshift)) | ((uint64_t)(v & fm) << e.rshift);
+                for (uint32_t b = 0; b < e.nbytes; ++b) {
+                    const uint32_t at = h + e.byte0 + b;
+                    const uint8_t x = (uint8_t)(w >> (8u * (e.nbytes - 1u - b)));
+                    if (at < WIN) {
+                        fr.put_staged(at, x);
+                        const uint32_t c0 = (at >> 4) & ~(unit_ch - 1u);
+                        dirty |= ((1u << unit_ch) - 1u) << c0;
+                    } else {
+                        frame[at] = x;  // past the window (slots > 64 B)
+                    }
+                }
+            }
+        }
+        if (valid && a.out) store_rec(static_cast<uint4*>(a.out) + i, pack(r), a.policy & 2u);
+        // every lane's staged edits are in LDS before any lane reads them back
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (uint32_t k = 0; k < NCH; ++k) {
+            const uint32_t q = k * WAVE + lane;
+            const uint32_t pp = q / NCH;
+            const uint32_t c = (q - pp * NCH) ^ swz<NCH>(pp);
+            const uint32_t d = (uint32_t)__shfl((int)dirty, (int)pp);
+            if ((d >> c) & 1u) {
+                const uint32_t* src = img + q * 4u;
+                const uint4 v = make_uint4(src[0], src[1], src[2], src[3]);
+                store_rec(reinterpret_cast<uint4*>(arena + (tt * WAVE + pp) * a.stride + 16u * c),
+                          v, a.policy & 2u);
+            }
+        }
+    };
+
+    uint64_t t = (uint64_t)blockIdx.x * WAVES + wave;
+    if (t >= ntiles) return;
+#pragma unroll
+    for (uint32_t d = 0; d + 1u < DEPTH; ++d)
+        if (t + d * step < ntiles) stage(t + d * step, img0 + d * IMG_DW);
+    for (uint32_t j = 0;; ++j) {
+        const uint64_t tn = t + (DEPTH - 1u) * step;
+        if (tn < ntiles) {
+            stage(tn, img0 + ((j + DEPTH - 1u) % DEPTH) * IMG_DW);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DEPTH - 1u) * NCH) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        modify(t, img0 + (j % DEPTH) * IMG_DW);
+        // the write-back's LDS reads are done before this image is restaged
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        t += step;
+        if (t >= ntiles) break;
+    }
+}
+
+template <uint32_t DEPTH>
+hipError_t launch_modify_pipe(const ModifyArgs& a, int chain, uint32_t grid, hipStream_t s) {
+    switch (chain) {
+    case INGOT_CHAIN_UDP_PARSER:
+        hipLaunchKernelGGL((k_modify_pipe<4, DEPTH, INGOT_CHAIN_UDP_PARSER>), dim3(grid),
+                           dim3(BLOCK), 0, s, a);
+        break;
+    case INGOT_CHAIN_GENERIC_ULP:
+        hipLaunchKernelGGL((k_modify_pipe<4, DEPTH, INGOT_CHAIN_GENERIC_ULP>), dim3(grid),
+                           dim3(BLOCK), 0, s, a);
+        break;
+    case INGOT_CHAIN_VLAN_ULP:
+        hipLaunchKernelGGL((k_modify_pipe<4, DEPTH, INGOT_CHAIN_VLAN_ULP>), dim3(grid),
+                           dim3(BLOCK), 0, s, a);
+        break;
+    default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 template <uint32_t NCH, uint32_t DEPTH, int MODE>
 hipError_t launch_pipe(const ParseArgs& a, int chain, uint32_t grid, hipStream_t s) {
     switch (chain) {
@@ -1178,12 +1315,38 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
     }
 }
 
+// Ring rewrite kernel defaults (k_modify_pipe; measured).
+constexpr uint32_t kModifyRingWb = 64;
+constexpr uint32_t kModifyRingPolicy = 3;  // nt staging loads + nt write-back
+
 // Parse + rewrite: the default windows of the record path.
-hipError_t launch_modify(const ModifyArgs& a, int layout_kind, int chain, const Tuning& t,
+hipError_t launch_modify(const ModifyArgs& args, int layout_kind, int chain, const Tuning& t,
                          hipStream_t s) {
-    if (a.p.n == 0) return hipSuccess;
+    if (args.p.n == 0) return hipSuccess;
+    ModifyArgs a = args;
     const uint32_t g = grid_for(a.p.n, t.max_blocks);
     const bool tun = chain == INGOT_CHAIN_GENEVE_OVER_V6;
+    // Slot rings (slots >= 64 B, no length array): the multi-tile kernel with
+    // lane-linear write-back (k_modify_pipe).  Defaults measured on MI355X
+    // (DESIGN.md §1c): write-back unit WB, plain staging loads.
+    if (t.pipeline != 1 && !t.window_strided && layout_kind == LAYOUT_STRIDED && !a.p.len &&
+        !tun && a.p.stride >= 64u) {
+        a.wb = t.writeback ? (uint32_t)t.writeback : kModifyRingWb;
+        a.p.policy = t.cache_policy ? (uint32_t)t.cache_policy & 3u : kModifyRingPolicy;
+        const uint64_t tiles = (a.p.n + WAVE - 1) / WAVE;
+        uint64_t blocks;
+        if (t.pipeline > 1) {
+            const uint64_t waves = (tiles + (uint64_t)t.pipeline - 1) / (uint64_t)t.pipeline;
+            blocks = (waves + WAVES - 1) / WAVES;
+        } else {
+            const uint64_t cap = 2ull * t.cus;
+            blocks = (tiles + WAVES - 1) / WAVES;
+            if (blocks > cap) blocks = cap;
+        }
+        const uint32_t pg = (uint32_t)(blocks ? blocks : 1);
+        return t.pipe_depth == 3 ? launch_modify_pipe<3>(a, chain, pg, s)
+                                 : launch_modify_pipe<2>(a, chain, pg, s);
+    }
     if (layout_kind == LAYOUT_STRIDED) {
         if (tun) return launch_chain<8, LAYOUT_STRIDED, OUT_MODIFY>(a, chain, g, s);
         return a.p.stride <= 64u ? launch_chain<4, LAYOUT_STRIDED, OUT_MODIFY>(a, chain, g, s)
@@ -1230,6 +1393,8 @@ bool tuning_valid(int key, int value) {
         return value >= 0 && value <= 4;
     case INGOT_TUNE_PIPE_DEPTH:
         return value == 0 || (value >= 2 && value <= 4);
+    case INGOT_TUNE_WRITEBACK:
+        return value == 0 || value == 16 || value == 32 || value == 64;
     default:
         return false;
     }

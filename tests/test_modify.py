@@ -102,3 +102,34 @@ def test_modify_strided_decr(ctx, torch):
         ingot_amd.gen_frames(GenProfile.V4UDP64, n, stride=64)[0][:n * 64].view(n, 64).cpu()
         .numpy(),
         [36, 37], axis=1).tobytes()
+
+
+@pytest.mark.parametrize("tune", [dict(), dict(wb=16), dict(wb=64), dict(depth=3, wb=64),
+                                  dict(pipe=3, pol=1), dict(pipe=1), dict(pipe=16, pol=3)])
+@pytest.mark.parametrize("n", [1, 65, 100_003])
+def test_modify_ring_bit_exact(ctx, torch, tune, n):
+    """The slot-ring rewrite kernel (k_modify_pipe: staged edits, lane-linear
+    write-back) for every write-back unit, depth, grid and cache policy, on
+    64-B and 128-B slots (edits past the 64-B window go straight to HBM)."""
+    from ingot_amd.abi import (TUNE_CACHE_POLICY, TUNE_PIPE_DEPTH, TUNE_PIPELINE,
+                               TUNE_WRITEBACK)
+
+    c = ingot_amd.Context(0)
+    c.set_tuning(TUNE_WRITEBACK, tune.get("wb", 0))
+    c.set_tuning(TUNE_PIPE_DEPTH, tune.get("depth", 0))
+    c.set_tuning(TUNE_PIPELINE, tune.get("pipe", 0))
+    c.set_tuning(TUNE_CACHE_POLICY, tune.get("pol", 0))
+    for prof, stride in ((GenProfile.V4UDP64, 64), (GenProfile.ADVERSARIAL, 64),
+                         (GenProfile.MIXED, 128), (GenProfile.VLAN_V6EH, 128)):
+        for chain in (Chain.UdpParser, Chain.GenericUlp, Chain.VlanUlp):
+            arena, _, _ = ingot_amd.gen_frames(prof, n, seed=n + stride, stride=stride)
+            want = arena.cpu().numpy().copy()
+            recs = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
+            c.parse_modify(arena, None, None, chain, EDITS[chain], stride=stride, n=n, out=recs)
+            torch.cuda.synchronize()
+            w_rec = oracle.parse_modify_batch(want, None, None, chain, EDITS[chain],
+                                              stride=stride, n=n, nthreads=8)
+            assert recs.cpu().numpy().tobytes() == w_rec.tobytes(), (prof, chain)
+            got = arena.cpu().numpy()
+            diff = np.nonzero(got != want)[0]
+            assert diff.size == 0, (prof, chain, diff[:10], got[diff[:10]], want[diff[:10]])

@@ -7,7 +7,7 @@ cross-process/device variance that looks like a kernel property).
     python tools/abtune.py --config c2 --var streams=1 --var streams=2 --var rec=8
 
 A variant is a comma list of key=value: win_i, win_s, blocks, pipe, depth, pol,
-streams, rec.
+wb, streams, rec.
 """
 from __future__ import annotations
 
@@ -36,7 +36,8 @@ def main():
     import ingot_amd
     from ingot_amd import Chain, GenProfile
     from ingot_amd.abi import (TUNE_CACHE_POLICY, TUNE_MAX_BLOCKS, TUNE_PIPE_DEPTH,
-                               TUNE_PIPELINE, TUNE_WINDOW_INDEXED, TUNE_WINDOW_STRIDED)
+                               TUNE_PIPELINE, TUNE_WINDOW_INDEXED, TUNE_WINDOW_STRIDED,
+                               TUNE_WRITEBACK)
 
     prof, n, stride, chain_name, _ = bench.CONFIGS[args.config]
     chain = Chain[chain_name]
@@ -64,9 +65,16 @@ def main():
             ctx.set_tuning(TUNE_PIPE_DEPTH, int(kv["depth"]))
         if "pol" in kv:
             ctx.set_tuning(TUNE_CACHE_POLICY, int(kv["pol"]))
+        if "wb" in kv:
+            ctx.set_tuning(TUNE_WRITEBACK, int(kv["wb"]))
         ns, rb = int(kv.get("streams", 1)), int(kv.get("rec", 16))
-        runners[v] = (ctx, bench.Runner(torch, lib, ctx, chain, n, stride, arenas, off, lens,
-                                        outs, streams[:ns], rb))
+        if bench.MODES.get(args.config) == "modify":
+            r = bench.ModifyRunner(torch, lib, ctx, chain, n, stride, arenas, off, lens,
+                                   streams[:ns])
+        else:
+            r = bench.Runner(torch, lib, ctx, chain, n, stride, arenas, off, lens, outs,
+                             streams[:ns], rb)
+        runners[v] = (ctx, r)
     res = {v: [] for v in variants}
     for _ in range(args.rounds):
         for v, (_, r) in runners.items():
