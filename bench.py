@@ -239,12 +239,17 @@ class FlowRunner:
         optr, lptr = off.data_ptr(), lens.data_ptr()
         aptrs = [a.data_ptr() for a in arenas]
 
+        # caller-owned workspace: the atomics-free histogram pass
+        wbytes = lib.ingot_gpu_flow_hist_workspace_size(n, hists[0].numel())
+        self.work = torch.empty(max(1, wbytes), dtype=torch.uint8, device=hists[0].device)
+        wptr = self.work.data_ptr()
+
         def launch(k):
             hist = hists[k % reps]
             hist.zero_()
-            rc = lib.ingot_gpu_flow_hist(h, aptrs[k % reps], optr, lptr, 0, n, c, None,
-                                         hist.numel(), flows[k % reps].data_ptr(), None,
-                                         hist.data_ptr(), sp)
+            rc = lib.ingot_gpu_flow_hist_ws(h, aptrs[k % reps], optr, lptr, 0, n, c, None,
+                                            hist.numel(), flows[k % reps].data_ptr(), None,
+                                            hist.data_ptr(), wptr, wbytes, sp)
             reduce_fn(hist)
             return rc
 
@@ -399,9 +404,9 @@ def main():
     else:
         rd, wr = algorithmic_bytes(recs_np, lens_np, stride or 0, 0 if stride else 10,
                                    args.record)
-    if flows:  # per-packet flow id (4 B) + the flow-id re-read of the histogram pass
+    if flows:  # per-packet flow id (4 B) written, read once by the histogram pass
         wr = 4 * n + FLOW_BINS * 4
-        rd += 4 * n * (FLOW_BINS // min(FLOW_BINS, 16384))
+        rd += 4 * n
     if mode == "modify":  # no records; the 2 rewritten bytes per packet
         wr = 2 * n
     bytes_launch = rd + wr
@@ -503,7 +508,7 @@ def main():
                 "traffic_detail": traffic,
                 "kernel": ("k_parse_pipe" if ring else "k_parse") + " (ingot_amd/csrc/parse.hip)" + {
                     "modify": ", OUT_MODIFY", "read": ", LAYOUT_SEGMENTED",
-                    "flows": ", OUT_FLOWS + k_flow_hist"}.get(mode, ""),
+                    "flows": ", OUT_FLOWS + k_flow_count16/k_flow_reduce16"}.get(mode, ""),
                 "launch_mean_us": round(launch_ms * 1e3, 3),
                 "launch_timing": "single-stream pass, HIP events, region/K",
                 "pipelined_GBps": round(pipelined_gbs, 1),

@@ -545,7 +545,15 @@ int ingot_gpu_parse_modify(ingot_gpu_ctx* ctx, uint8_t* d_arena,
  *           accumulated into (zero it to start a new histogram).
  * bins is a power of two <= 2^24.  d_off == NULL selects the strided layout
  * (as ingot_gpu_fields).  Two launches: parse + hash, then a contention-free
- * histogram pass over d_flow (LDS-privatised bin ranges).
+ * histogram pass over d_flow (LDS-privatised counters).
+ *
+ * ingot_gpu_flow_hist_ws: the same with a caller-owned device workspace
+ * (d_work, work_bytes >= ingot_gpu_flow_hist_workspace_size(n, bins), e.g.
+ * 16 MiB for 8 M packets x 65,536 bins): the histogram pass then stores
+ * per-block counters there and reduces them without atomics (faster; see
+ * DESIGN.md).  Size 0 = no workspace is used for (n, bins); a smaller or NULL
+ * workspace falls back to the atomic pass.  Like the arena, the workspace is
+ * borrowed for the call: calls that run concurrently need their own.
  */
 #define INGOT_FLOW_KEY_BYTES 40
 #define INGOT_FLOW_NONE 0xffffffffu
@@ -554,6 +562,13 @@ int ingot_gpu_flow_hist(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
                         uint32_t stride, uint64_t n, int chain,
                         const uint8_t* key, uint32_t bins, uint32_t* d_flow,
                         uint32_t* d_hash, uint32_t* d_hist, void* stream);
+int ingot_gpu_flow_hist_ws(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
+                           const uint64_t* d_off, const uint16_t* d_len,
+                           uint32_t stride, uint64_t n, int chain,
+                           const uint8_t* key, uint32_t bins, uint32_t* d_flow,
+                           uint32_t* d_hash, uint32_t* d_hist, void* d_work,
+                           size_t work_bytes, void* stream);
+size_t ingot_gpu_flow_hist_workspace_size(uint64_t n, uint32_t bins);
 
 /* Error strings. */
 const char* ingot_gpu_strerror(int api_code);

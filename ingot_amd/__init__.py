@@ -257,12 +257,14 @@ class Context:
 
     def flow_hist(self, arena, off, lens, chain: Chain, hist=None, bins: Optional[int] = None,
                   stride: int = 0, n: Optional[int] = None, key: Optional[bytes] = None,
-                  flow=None, hashes=None, stream=None):
-        """Flow classification (ingot_gpu_flow_hist).  Returns the per-packet
-        flow bins (n x int32; INGOT_FLOW_NONE = -1 when not counted); `hist`
-        (int32/uint32 cuda tensor of `bins` entries) is accumulated into if
-        given; optional full Toeplitz hashes into `hashes`.  key=None: the
-        standard RSS key."""
+                  flow=None, hashes=None, workspace=None, stream=None):
+        """Flow classification (ingot_gpu_flow_hist / _ws).  Returns the
+        per-packet flow bins (n x int32; INGOT_FLOW_NONE = -1 when not
+        counted); `hist` (int32/uint32 cuda tensor of `bins` entries) is
+        accumulated into if given; optional full Toeplitz hashes into
+        `hashes`.  key=None: the standard RSS key.  `workspace`: a cuda
+        tensor of >= flow_hist_workspace_size(n, bins) bytes selects the
+        atomics-free histogram pass (flow_hist_workspace() makes one)."""
         torch = _torch()
         if n is None:
             n = off.numel()
@@ -272,11 +274,26 @@ class Context:
             flow = torch.empty(n, dtype=torch.int32, device=arena.device)
         self._check_dev(arena, off, lens, hist, hashes, flow)
         kbuf = None if key is None else ctypes.create_string_buffer(bytes(key), 40)
-        _lib.check(self._lib.ingot_gpu_flow_hist(
+        wbytes = 0 if workspace is None else workspace.numel() * workspace.element_size()
+        if workspace is not None:
+            self._check_dev(workspace)
+        _lib.check(self._lib.ingot_gpu_flow_hist_ws(
             self._h, _ptr(arena), _ptr(off), _ptr(lens), int(stride), n, int(chain),
             ctypes.cast(kbuf, ctypes.c_void_p) if kbuf is not None else None, int(bins),
-            _ptr(flow), _ptr(hashes), _ptr(hist), _stream(stream)), "ingot_gpu_flow_hist")
+            _ptr(flow), _ptr(hashes), _ptr(hist), _ptr(workspace), wbytes, _stream(stream)),
+            "ingot_gpu_flow_hist_ws")
         return flow
+
+    def flow_hist_workspace_size(self, n: int, bins: int) -> int:
+        """Bytes of workspace the atomics-free histogram pass needs (0: none)."""
+        return int(self._lib.ingot_gpu_flow_hist_workspace_size(n, bins))
+
+    def flow_hist_workspace(self, n: int, bins: int):
+        """A device workspace for flow_hist(n, bins), or None when not used."""
+        b = self.flow_hist_workspace_size(n, bins)
+        if not b:
+            return None
+        return _torch().empty(b, dtype=_torch().uint8, device=f"cuda:{self.device}")
 
 
 def records_to_numpy(t):

@@ -74,6 +74,12 @@ SIGNATURES = {
         [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, ctypes.c_uint32, c_u64, ctypes.c_int, c_u8p,
          ctypes.c_uint32, c_u8p, c_u8p, c_u8p, ctypes.c_void_p],
     ),
+    "ingot_gpu_flow_hist_ws": (
+        ctypes.c_int,
+        [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, ctypes.c_uint32, c_u64, ctypes.c_int, c_u8p,
+         ctypes.c_uint32, c_u8p, c_u8p, c_u8p, c_u8p, ctypes.c_size_t, ctypes.c_void_p],
+    ),
+    "ingot_gpu_flow_hist_workspace_size": (ctypes.c_size_t, [c_u64, ctypes.c_uint32]),
     "ingot_gpu_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "ingot_parse_error_name": (ctypes.c_char_p, [ctypes.c_int]),
     "ingot_chain_layer_label": (ctypes.c_char_p, [ctypes.c_int, ctypes.c_int]),

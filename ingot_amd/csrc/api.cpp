@@ -296,10 +296,10 @@ int ingot_gpu_parse_modify(ingot_gpu_ctx* ctx, uint8_t* d_arena, const uint64_t*
     return from_hip(ingot_gpu::launch_modify(a, layout, chain, ctx->tuning, (hipStream_t)stream));
 }
 
-int ingot_gpu_flow_hist(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
-                        const uint16_t* d_len, uint32_t stride, uint64_t n, int chain,
-                        const uint8_t* key, uint32_t bins, uint32_t* d_flow, uint32_t* d_hash,
-                        uint32_t* d_hist, void* stream) {
+int ingot_gpu_flow_hist_ws(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
+                           const uint16_t* d_len, uint32_t stride, uint64_t n, int chain,
+                           const uint8_t* key, uint32_t bins, uint32_t* d_flow, uint32_t* d_hash,
+                           uint32_t* d_hist, void* d_work, size_t work_bytes, void* stream) {
     // The standard Microsoft RSS key (the one its published verification
     // vectors use; tests/test_flows.py).
     static const uint8_t kRssKey[INGOT_FLOW_KEY_BYTES] = {
@@ -335,7 +335,20 @@ int ingot_gpu_flow_hist(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64
     const hipStream_t s = (hipStream_t)stream;
     if (int e = from_hip(ingot_gpu::launch_flows(a, layout, chain, ctx->tuning, s))) return e;
     if (!d_hist) return INGOT_GPU_SUCCESS;
-    return from_hip(ingot_gpu::launch_flow_hist(d_flow, n, d_hist, bins, s));
+    return from_hip(ingot_gpu::launch_flow_hist(d_flow, n, d_hist, bins, d_work, work_bytes, s));
+}
+
+int ingot_gpu_flow_hist(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
+                        const uint16_t* d_len, uint32_t stride, uint64_t n, int chain,
+                        const uint8_t* key, uint32_t bins, uint32_t* d_flow, uint32_t* d_hash,
+                        uint32_t* d_hist, void* stream) {
+    return ingot_gpu_flow_hist_ws(ctx, d_arena, d_off, d_len, stride, n, chain, key, bins, d_flow,
+                                  d_hash, d_hist, nullptr, 0, stream);
+}
+
+size_t ingot_gpu_flow_hist_workspace_size(uint64_t n, uint32_t bins) {
+    if (bins == 0 || (bins & (bins - 1)) != 0 || bins > (1u << 24)) return 0;
+    return ingot_gpu::flow_hist_workspace(n, bins);
 }
 
 const char* ingot_gpu_strerror(int code) {

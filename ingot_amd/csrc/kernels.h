@@ -58,7 +58,8 @@ struct ModifyArgs {
 };
 // Histogram pass over flow bins (flow.hip).
 hipError_t launch_flow_hist(const uint32_t* flow, uint64_t n, uint32_t* hist, uint32_t bins,
-                            hipStream_t s);
+                            void* work, size_t work_bytes, hipStream_t s);
+size_t flow_hist_workspace(uint64_t n, uint32_t bins);
 
 // Per-context tuning (0 = measured default); see INGOT_TUNE_* in ingot_gpu.h.
 struct Tuning {

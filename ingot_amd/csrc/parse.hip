@@ -766,15 +766,22 @@ __device__ __forceinline__ void apply_edit(const FR& f, EditSink& sink, uint32_t
 // RSS Toeplitz over one 32-bit input word (MSB first) whose first bit is
 // input bit B: XOR in the key window W[B + k] for every set bit k.  W is
 // lane-uniform (kernel argument), so only the data bits are per lane.
-// RSS Toeplitz with nibble tables in LDS: tab[p*16 + v] = XOR of the key
-// windows of the set bits of nibble value v at input nibble position p
-// (FLOW_INPUT_BITS/4 = 72 positions, 4.5 KiB per block, built once per block
-// from the 32-bit key windows).  A 32-bit input word = 8 LDS lookups.
-constexpr uint32_t FLOW_TAB = FLOW_INPUT_BITS / 4 * 16;
+// Nibble tables in LDS: entry (p, v) = XOR of the key windows of the set bits
+// of nibble value v at input nibble position p (FLOW_INPUT_BITS/4 = 72
+// positions), so a 32-bit input word = 8 LDS lookups.  Every instruction of
+// the hash reads one position p (all lanes), i.e. 16 entries; ds_read_b32
+// banks are (dword mod 32) per 32-lane group, so 16 entries stored once sit
+// in 16 banks (2-way+ conflicts).  Stored 2x interleaved — entry (p, v) copy
+// c at dword 32p + 2v + c, lane L reading copy L & 1 — each of the 32 banks
+// holds one address per instruction: conflict-free (lanes that share a bank
+// share the address: broadcast).  9 KiB per block, built once per block (the
+// flows grid is persistent).
+constexpr uint32_t FLOW_POS = FLOW_INPUT_BITS / 4;
+constexpr uint32_t FLOW_TAB = FLOW_POS * 32;
 
 __device__ __forceinline__ void build_flow_table(uint32_t* tab, const uint32_t* W) {
     for (uint32_t e = threadIdx.x; e < FLOW_TAB; e += BLOCK) {
-        const uint32_t p = e >> 4, v = e & 15u;
+        const uint32_t p = e >> 5, v = (e >> 1) & 15u;
         uint32_t acc = 0;
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) acc ^= ((v >> (3u - k)) & 1u) ? W[4u * p + k] : 0u;
@@ -782,17 +789,13 @@ __device__ __forceinline__ void build_flow_table(uint32_t* tab, const uint32_t* 
     }
 }
 
-template <uint32_t NIB0>  // first nibble position of the word
-__device__ __forceinline__ uint32_t toeplitz_word(uint32_t word, const uint32_t* tab) {
-    uint32_t h = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 8; ++j) h ^= tab[(NIB0 + j) * 16u + ((word >> (28u - 4u * j)) & 15u)];
-    return h;
-}
-
 // Flow classification (ingot_gpu_flow_hist): hash of src|dst|ports.
 // Appending zero ports leaves a Toeplitz hash unchanged, so ICMP/other L4 use
-// the same word positions with a zero port word.
+// the same word positions with a zero port word — and an IPv4 input
+// (src|dst|ports, 3 words) is the IPv6 word sequence with zero words after
+// its ports.  Every lane therefore hashes 9 words at the same table positions:
+// no v4/v6 divergence in the LDS lookups (72 per packet, not 24 + 72 per
+// mixed wave).
 template <class FR>
 __device__ __forceinline__ bool flow_hash(const FR& f, const Rec& r, const uint32_t* tab,
                                           uint32_t& h) {
@@ -800,16 +803,18 @@ __device__ __forceinline__ bool flow_hash(const FR& f, const Rec& r, const uint3
     if (r.status != INGOT_OK || r.l3_kind == INGOT_L3_NONE) return false;
     const bool ports = r.l4_kind == INGOT_L4_TCP || r.l4_kind == INGOT_L4_UDP;
     const uint32_t pw = ports ? f.be(r.l4_off, 4) : 0u;
-    if (r.l3_kind == INGOT_L3_IPV4) {
-        h = toeplitz_word<0>(f.be(r.l3_off + 12u, 4), tab) ^
-            toeplitz_word<8>(f.be(r.l3_off + 16u, 4), tab) ^ toeplitz_word<16>(pw, tab);
-    } else {
-        const uint32_t a = r.l3_off + ipv6::SOURCE_BYTE;
-        h = toeplitz_word<0>(f.be(a, 4), tab) ^ toeplitz_word<8>(f.be(a + 4u, 4), tab) ^
-            toeplitz_word<16>(f.be(a + 8u, 4), tab) ^ toeplitz_word<24>(f.be(a + 12u, 4), tab) ^
-            toeplitz_word<32>(f.be(a + 16u, 4), tab) ^ toeplitz_word<40>(f.be(a + 20u, 4), tab) ^
-            toeplitz_word<48>(f.be(a + 24u, 4), tab) ^ toeplitz_word<56>(f.be(a + 28u, 4), tab) ^
-            toeplitz_word<64>(pw, tab);
+    const bool v6 = r.l3_kind == INGOT_L3_IPV6;
+    const uint32_t a = r.l3_off + (v6 ? ipv6::SOURCE_BYTE : 12u);  // source address
+    const uint32_t naddr = v6 ? 8u : 2u;                            // address words
+    const uint32_t cp = threadIdx.x & 1u;                           // table copy
+#pragma unroll
+    for (uint32_t k = 0; k < 9; ++k) {
+        uint32_t w = 0;
+        if (k < naddr) w = f.be(a + 4u * k, 4);
+        else if (k == naddr) w = pw;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j)
+            h ^= tab[(8u * k + j) * 32u + ((w >> (28u - 4u * j)) & 15u) * 2u + cp];
     }
     return true;
 }
@@ -1361,7 +1366,10 @@ hipError_t launch_modify(const ModifyArgs& args, int layout_kind, int chain, con
 hipError_t launch_flows(const FlowArgs& a, int layout_kind, int chain, const Tuning& t,
                         hipStream_t s) {
     if (a.p.n == 0) return hipSuccess;
-    const uint32_t g = grid_for(a.p.n, t.max_blocks);
+    // Each block builds the 4.5 KiB nibble table once: a grid of 4 blocks per
+    // CU walking the tiles amortises it (C5 546 -> 486 us/step measured vs one
+    // tile per wave).
+    const uint32_t g = grid_for(a.p.n, t.max_blocks ? t.max_blocks : 4u * t.cus);
     if (layout_kind == LAYOUT_STRIDED) {
         switch (t.window_strided ? t.window_strided : (a.p.stride <= 64u ? 4 : 5)) {
         case 3: return launch_chain<3, LAYOUT_STRIDED, OUT_FLOWS>(a, chain, g, s);

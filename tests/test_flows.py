@@ -88,7 +88,7 @@ def test_flow_hist_bit_exact(profile, chain, stride):
     hist = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")
     hashes = torch.zeros(n, dtype=torch.int32, device="cuda")
     flow = ctx.flow_hist(arena, off, lens, Chain[chain], hist=hist, stride=stride or 0, n=n,
-                         hashes=hashes)
+                         hashes=hashes, workspace=ctx.flow_hist_workspace(n, 1 << 16))
     torch.cuda.synchronize()
     host = lambda t: None if t is None else t.cpu().numpy()  # noqa: E731
     w_hist, w_hash = oracle.flow_hist(host(arena), host(off), host(lens), Chain[chain],
@@ -111,3 +111,63 @@ def test_flow_hist_bit_exact(profile, chain, stride):
     if profile == "FLOWS":
         # Zipf(1.1) head: the top bin holds a large share
         assert w_hist.max() > 0.05 * w_hist.sum()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ws", [False, True])
+@pytest.mark.parametrize("bins", [1, 2, 4096, 1 << 16, 1 << 17, 1 << 20])
+def test_flow_hist_bin_regimes(bins, ws):
+    """Every histogram regime (workspace rows + reduce for <= 65,536 bins, LDS
+    bin ranges, wave-aggregated atomics) equals the bincount of the flow ids,
+    which the test above pins to the oracle; accumulation into a non-zero
+    histogram too."""
+    import torch
+
+    import ingot_amd
+    from ingot_amd import GenProfile
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    n = 300_000
+    ctx = ingot_amd.Context(0)
+    arena, off, lens = ingot_amd.gen_frames(GenProfile.FLOWS, n, seed=11)
+    hist = torch.full((bins,), 3, dtype=torch.int32, device="cuda")
+    work = ctx.flow_hist_workspace(n, bins) if ws else None
+    assert (work is not None) == (ws and bins <= 65536)
+    flow = ctx.flow_hist(arena, off, lens, Chain.VlanUlp, hist=hist, n=n, workspace=work)
+    torch.cuda.synchronize()
+    f = flow.cpu().numpy().view(np.uint32)
+    want = np.bincount(f[f != 0xFFFFFFFF], minlength=bins) + 3
+    assert (hist.cpu().numpy().view(np.uint32) == want).all()
+
+
+@pytest.mark.gpu
+def test_flow_hist_many_slices():
+    """> 256 x 65,535 flow ids: the 16-bit pass splits into more slices than
+    CUs so no per-block counter can wrap, even for a single hot flow."""
+    import torch
+
+    import ingot_amd
+    from ingot_amd import GenProfile
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ctx = ingot_amd.Context(0)
+    big = 256 * 65535 + 4097
+    assert ctx.flow_hist_workspace_size(big, 1 << 16) == 0  # > 256 slices: range pass
+    arena, _, _ = ingot_amd.gen_frames(GenProfile.V4UDP64, big, stride=64)
+    for n in (256 * 65535, big, 129 * 65535 + 1):
+        work = ctx.flow_hist_workspace(n, 1 << 16)
+        hist = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")
+        flow = ctx.flow_hist(arena, None, None, Chain.UdpParser, hist=hist, stride=64, n=n,
+                             workspace=work)
+        torch.cuda.synchronize()
+        f = flow.cpu().numpy().view(np.uint32)
+        want = np.bincount(f[f != 0xFFFFFFFF], minlength=1 << 16)
+        assert (hist.cpu().numpy().view(np.uint32) == want).all()
+        # one flow for every packet: a single bin counts them all without wrapping
+        h1 = torch.zeros(1, dtype=torch.int32, device="cuda")
+        ctx.flow_hist(arena, None, None, Chain.UdpParser, hist=h1, stride=64, n=n,
+                      workspace=ctx.flow_hist_workspace(n, 1))
+        torch.cuda.synchronize()
+        assert int(h1.cpu()[0]) == int((f != 0xFFFFFFFF).sum())

@@ -7,7 +7,7 @@ cross-process/device variance that looks like a kernel property).
     python tools/abtune.py --config c2 --var streams=1 --var streams=2 --var rec=8
 
 A variant is a comma list of key=value: win_i, win_s, blocks, pipe, depth, pol,
-wb, streams, rec.
+wb, streams, rec, mode (parse|flows|modify: the runner; default the config's).
 """
 from __future__ import annotations
 
@@ -68,7 +68,14 @@ def main():
         if "wb" in kv:
             ctx.set_tuning(TUNE_WRITEBACK, int(kv["wb"]))
         ns, rb = int(kv.get("streams", 1)), int(kv.get("rec", 16))
-        if bench.MODES.get(args.config) == "modify":
+        mode = kv.get("mode", bench.MODES.get(args.config, "parse"))
+        if mode == "flows":
+            hists = [torch.zeros(bench.FLOW_BINS, dtype=torch.int32, device="cuda")
+                     for _ in range(reps)]
+            fids = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(reps)]
+            r = bench.FlowRunner(torch, lib, ctx, chain, n, arenas, off, lens, hists, fids,
+                                 streams[0], lambda h: None)
+        elif mode == "modify":
             r = bench.ModifyRunner(torch, lib, ctx, chain, n, stride, arenas, off, lens,
                                    streams[:ns])
         else:
