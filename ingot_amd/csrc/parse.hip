@@ -29,6 +29,8 @@
 // No MFMA: this is integer field extraction bounded by HBM bandwidth.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <type_traits>
 
 #include "../../include/ingot_gpu.h"
@@ -124,6 +126,25 @@ struct Frame {
             v = beyond(i, n);
         }
         return v;
+    }
+
+    // NW consecutive big-endian words at frame offset i, all from LDS: NW+1
+    // aligned dwords and one v_perm each (align + byte swap).  The caller
+    // keeps only words below `avail`; reads past it stay inside this packet's
+    // image (chunk index clamped) and are discarded.
+    template <uint32_t NW>
+    __device__ __forceinline__ void be_words(uint32_t i, uint32_t* out) const {
+        const uint32_t b = sh + i;
+        const uint32_t sel = (b & 3u) * 0x01010101u + 0x00010203u;
+        uint32_t d[NW + 1];
+#pragma unroll
+        for (uint32_t k = 0; k <= NW; ++k) {
+            const uint32_t q = (b >> 2) + k;  // dword of the staged bytes
+            const uint32_t c = (q >> 2) < NCH - 1u ? (q >> 2) : NCH - 1u;
+            d[k] = win[slot_of<NCH>(p, c) * 4u + (q & 3u)];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < NW; ++k) out[k] = __builtin_amdgcn_perm(d[k + 1], d[k], sel);
     }
 
     // Bytes past the staged window (long option / EH chains), read straight
@@ -796,27 +817,83 @@ __device__ __forceinline__ void build_flow_table(uint32_t* tab, const uint32_t* 
 // its ports.  Every lane therefore hashes 9 words at the same table positions:
 // no v4/v6 divergence in the LDS lookups (72 per packet, not 24 + 72 per
 // mixed wave).
+struct FlowWords {
+    uint32_t w[9];
+};
+
+// The hash input words of a parsed-Ok packet with an L3 layer (false: not
+// counted).  The address block (2 words for IPv4, 8 for IPv6, contiguous)
+// normally lies in the staged window: one burst of 9 LDS dwords and one
+// v_perm (align + byte swap) per word, instead of a bounds check, two reads
+// and a wait per word.  Otherwise (a window smaller than the L3 header, or
+// a deep VLAN stack) word by word through Frame::be, which falls back to
+// L2/HBM.  The port word may lie past the window (IPv6 EH chains).
 template <class FR>
-__device__ __forceinline__ bool flow_hash(const FR& f, const Rec& r, const uint32_t* tab,
-                                          uint32_t& h) {
-    h = 0;
+__device__ __forceinline__ bool flow_words(const FR& f, const Rec& r, FlowWords& x) {
+#pragma unroll
+    for (uint32_t k = 0; k < 9; ++k) x.w[k] = 0;
     if (r.status != INGOT_OK || r.l3_kind == INGOT_L3_NONE) return false;
     const bool ports = r.l4_kind == INGOT_L4_TCP || r.l4_kind == INGOT_L4_UDP;
     const uint32_t pw = ports ? f.be(r.l4_off, 4) : 0u;
     const bool v6 = r.l3_kind == INGOT_L3_IPV6;
     const uint32_t a = r.l3_off + (v6 ? ipv6::SOURCE_BYTE : 12u);  // source address
     const uint32_t naddr = v6 ? 8u : 2u;                            // address words
-    const uint32_t cp = threadIdx.x & 1u;                           // table copy
+    uint32_t w[8];
+    if (a + 4u * naddr <= f.avail) {
+        f.template be_words<8>(a, w);
+    } else {
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) w[k] = k < naddr ? f.be(a + 4u * k, 4) : 0u;
+    }
 #pragma unroll
     for (uint32_t k = 0; k < 9; ++k) {
-        uint32_t w = 0;
-        if (k < naddr) w = f.be(a + 4u * k, 4);
-        else if (k == naddr) w = pw;
-#pragma unroll
-        for (uint32_t j = 0; j < 8; ++j)
-            h ^= tab[(8u * k + j) * 32u + ((w >> (28u - 4u * j)) & 15u) * 2u + cp];
+        const uint32_t ak = k < 8 ? w[k] : 0u;
+        x.w[k] = k < naddr ? ak : (k == naddr ? pw : 0u);
     }
     return true;
+}
+
+// a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96; the
+// compiler does not form it from two XORs).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// Toeplitz of the 9 words from the LDS nibble tables (LDS only).  Lookup
+// (position q, nibble v, copy cp) is at byte 128q + 8v + 4cp of the table; the
+// table is 128-B aligned, so the per-lane part (8v | 4cp | base) is one
+// shift + one v_and_or and the position rides in the ds_read offset.
+__device__ __forceinline__ uint32_t toeplitz9(const FlowWords& x, const uint32_t* tab) {
+    uint32_t base =
+        (uint32_t)(size_t)(const lds_u32*)tab + ((threadIdx.x & 1u) << 2);  // + table copy
+    // opaque to the optimiser: otherwise it folds the position into the OR
+    // (one extra v_or per lookup) instead of the ds_read offset
+    asm volatile("" : "+v"(base));
+    uint32_t h = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 9; ++k) {
+        uint32_t t[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t s = 28u - 4u * j;  // nibble j (MSB first) -> nibble * 8
+            const uint32_t v8 = s >= 3u ? (x.w[k] >> (s - 3u)) : (x.w[k] << (3u - s));
+            const lds_u32* e = (const lds_u32*)(size_t)((v8 & 0x78u) | base);
+            t[j] = e[(8u * k + j) * 32u];
+        }
+        h = xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), xor3(t[6], t[7], h));
+    }
+    return h;
+}
+
+template <class FR>
+__device__ __forceinline__ bool flow_hash(const FR& f, const Rec& r, const uint32_t* tab,
+                                          uint32_t& h) {
+    FlowWords x;
+    const bool ok = flow_words(f, r, x);
+    h = ok ? toeplitz9(x, tab) : 0u;
+    return ok;
 }
 
 template <uint32_t NCH, int LAYOUT, int CHAIN, int MODE, class ARGS>
@@ -828,7 +905,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
     // +16 dwords: the second dword of a pair read may run past the last image.
     // NCH = 0: no staging, every read goes to L2/HBM.
     __shared__ __attribute__((aligned(16))) uint32_t s_win[WAVES * WAVE_DW + 16];
-    __shared__ uint32_t s_tab[MODE == OUT_FLOWS ? FLOW_TAB : 1];
+    __shared__ __attribute__((aligned(128))) uint32_t s_tab[MODE == OUT_FLOWS ? FLOW_TAB : 1];
     if constexpr (MODE == OUT_FLOWS) {
         build_flow_table(s_tab, args.w);
         __syncthreads();
@@ -1187,27 +1264,49 @@ hipError_t launch_pipe(const ParseArgs& a, int chain, uint32_t grid, hipStream_t
     return hipGetLastError();
 }
 
+// Blocks of `kernel` one CU holds at once (its LDS / VGPR footprint), queried
+// once per kernel instance.
+template <class K>
+uint32_t resident_per_cu(K kernel) {
+    static std::atomic<int> occ{0};
+    int v = occ.load(std::memory_order_relaxed);
+    if (!v) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kernel, BLOCK, 0) != hipSuccess ||
+            v < 1)
+            v = 1;
+        occ.store(v, std::memory_order_relaxed);
+    }
+    return (uint32_t)v;
+}
+
+// persist_cus != 0: a persistent grid, capped at the blocks the device holds
+// at once (cus x resident_per_cu), so no CU runs a second partial round.
 template <uint32_t NCH, int LAYOUT, int MODE, class ARGS>
-hipError_t launch_chain(const ARGS& a, int chain, uint32_t grid, hipStream_t s) {
+hipError_t launch_chain(const ARGS& a, int chain, uint32_t grid, hipStream_t s,
+                        uint32_t persist_cus = 0) {
+    auto go = [&](auto kernel) {
+        uint32_t g = grid;
+        if (persist_cus) {
+            const uint32_t cap = persist_cus * resident_per_cu(kernel);
+            if (g > cap) g = cap;
+        }
+        hipLaunchKernelGGL(kernel, dim3(g), dim3(BLOCK), 0, s, a);
+    };
     switch (chain) {
     case INGOT_CHAIN_UDP_PARSER:
-        hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_UDP_PARSER, MODE, ARGS>), dim3(grid),
-                           dim3(BLOCK), 0, s, a);
+        go(k_parse<NCH, LAYOUT, INGOT_CHAIN_UDP_PARSER, MODE, ARGS>);
         break;
     case INGOT_CHAIN_GENERIC_ULP:
-        hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_GENERIC_ULP, MODE, ARGS>),
-                           dim3(grid), dim3(BLOCK), 0, s, a);
+        go(k_parse<NCH, LAYOUT, INGOT_CHAIN_GENERIC_ULP, MODE, ARGS>);
         break;
     case INGOT_CHAIN_VLAN_ULP:
-        hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_VLAN_ULP, MODE, ARGS>), dim3(grid),
-                           dim3(BLOCK), 0, s, a);
+        go(k_parse<NCH, LAYOUT, INGOT_CHAIN_VLAN_ULP, MODE, ARGS>);
         break;
     default:
         if constexpr (MODE == OUT_REC8) {
             return hipErrorInvalidValue;  // not offered for the tunnel (api.cpp)
         } else {
-            hipLaunchKernelGGL((k_parse<NCH, LAYOUT, INGOT_CHAIN_GENEVE_OVER_V6, MODE, ARGS>),
-                               dim3(grid), dim3(BLOCK), 0, s, a);
+            go(k_parse<NCH, LAYOUT, INGOT_CHAIN_GENEVE_OVER_V6, MODE, ARGS>);
         }
         break;
     }
@@ -1366,23 +1465,28 @@ hipError_t launch_modify(const ModifyArgs& args, int layout_kind, int chain, con
 hipError_t launch_flows(const FlowArgs& a, int layout_kind, int chain, const Tuning& t,
                         hipStream_t s) {
     if (a.p.n == 0) return hipSuccess;
-    // Each block builds the 4.5 KiB nibble table once: a grid of 4 blocks per
-    // CU walking the tiles amortises it (C5 546 -> 486 us/step measured vs one
-    // tile per wave).
-    const uint32_t g = grid_for(a.p.n, t.max_blocks ? t.max_blocks : 4u * t.cus);
+    // Each block builds the table once, so the grid is persistent: exactly the
+    // blocks the device holds at once (5 per CU at the default window: LDS),
+    // each wave walking tiles.  Measured on C5 (parse+hash+histogram, us per
+    // step): one tile per wave 546, 4 blocks per CU 434, 5 per CU 402, 6 / 8
+    // per CU (a second partial round) 511 / 443.  A double-buffered variant
+    // (next tile staged while hashing, 3 blocks per CU for its two images)
+    // measured 526 vs 454 at the time.
+    const uint32_t g = grid_for(a.p.n, t.max_blocks);
+    const uint32_t pc = t.max_blocks ? 0u : t.cus;
     if (layout_kind == LAYOUT_STRIDED) {
         switch (t.window_strided ? t.window_strided : (a.p.stride <= 64u ? 4 : 5)) {
-        case 3: return launch_chain<3, LAYOUT_STRIDED, OUT_FLOWS>(a, chain, g, s);
-        case 4: return launch_chain<4, LAYOUT_STRIDED, OUT_FLOWS>(a, chain, g, s);
-        case 8: return launch_chain<8, LAYOUT_STRIDED, OUT_FLOWS>(a, chain, g, s);
-        default: return launch_chain<5, LAYOUT_STRIDED, OUT_FLOWS>(a, chain, g, s);
+        case 3: return launch_chain<3, LAYOUT_STRIDED, OUT_FLOWS>(a, chain, g, s, pc);
+        case 4: return launch_chain<4, LAYOUT_STRIDED, OUT_FLOWS>(a, chain, g, s, pc);
+        case 8: return launch_chain<8, LAYOUT_STRIDED, OUT_FLOWS>(a, chain, g, s, pc);
+        default: return launch_chain<5, LAYOUT_STRIDED, OUT_FLOWS>(a, chain, g, s, pc);
         }
     }
     switch (t.window_indexed ? t.window_indexed : 5) {
-    case 3: return launch_chain<3, LAYOUT_INDEXED, OUT_FLOWS>(a, chain, g, s);
-    case 4: return launch_chain<4, LAYOUT_INDEXED, OUT_FLOWS>(a, chain, g, s);
-    case 6: return launch_chain<6, LAYOUT_INDEXED, OUT_FLOWS>(a, chain, g, s);
-    default: return launch_chain<5, LAYOUT_INDEXED, OUT_FLOWS>(a, chain, g, s);
+    case 3: return launch_chain<3, LAYOUT_INDEXED, OUT_FLOWS>(a, chain, g, s, pc);
+    case 4: return launch_chain<4, LAYOUT_INDEXED, OUT_FLOWS>(a, chain, g, s, pc);
+    case 6: return launch_chain<6, LAYOUT_INDEXED, OUT_FLOWS>(a, chain, g, s, pc);
+    default: return launch_chain<5, LAYOUT_INDEXED, OUT_FLOWS>(a, chain, g, s, pc);
     }
 }
 

@@ -114,6 +114,48 @@ def test_flow_hist_bit_exact(profile, chain, stride):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("tune", [{}, {"win": 3}, {"win": 4}, {"win": 5}, {"win": 8},
+                                  {"blocks": 7}, {"blocks": 1, "win": 3}])
+@pytest.mark.parametrize("profile,chain,stride", [
+    ("FLOWS", "VlanUlp", None), ("ADVERSARIAL", "GenericUlp", None),
+    ("GENEVE_ADVERSARIAL", "GeneveOverV6Tunnel", None), ("VLAN_V6EH", "VlanUlp", 256),
+])
+def test_flow_kernels_every_setting(tune, profile, chain, stride):
+    """Every staged window (so both the LDS burst and the word-by-word
+    fallback of the hash input read) and tiny grid caps (many tiles per wave,
+    ragged tail): flow ids and hashes bit-exact against the oracle."""
+    import torch
+
+    import ingot_amd
+    from ingot_amd import GenProfile
+    from ingot_amd.abi import TUNE_MAX_BLOCKS, TUNE_WINDOW_INDEXED, TUNE_WINDOW_STRIDED
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    n = 100_003
+    ctx = ingot_amd.Context(0)
+    if "win" in tune:
+        ctx.set_tuning(TUNE_WINDOW_STRIDED if stride else TUNE_WINDOW_INDEXED, tune["win"])
+    if "blocks" in tune:
+        ctx.set_tuning(TUNE_MAX_BLOCKS, tune["blocks"])
+    arena, off, lens = ingot_amd.gen_frames(GenProfile[profile], n, seed=13, stride=stride)
+    hist = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")
+    hashes = torch.zeros(n, dtype=torch.int32, device="cuda")
+    flow = ctx.flow_hist(arena, off, lens, Chain[chain], hist=hist, stride=stride or 0, n=n,
+                         hashes=hashes, workspace=ctx.flow_hist_workspace(n, 1 << 16))
+    torch.cuda.synchronize()
+    host = lambda t: None if t is None else t.cpu().numpy()  # noqa: E731
+    w_hist, w_hash = oracle.flow_hist(host(arena), host(off), host(lens), Chain[chain],
+                                      stride=stride or 0, n=n)
+    w_flow = oracle.flow_hist.last_flows
+    g_hash = hashes.cpu().numpy().view(np.uint32)
+    bad = np.nonzero(g_hash != w_hash)[0]
+    assert bad.size == 0, (bad[:5], g_hash[bad[:5]], w_hash[bad[:5]])
+    assert (flow.cpu().numpy().view(np.uint32) == w_flow).all()
+    assert (hist.cpu().numpy().view(np.uint32) == w_hist).all()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("ws", [False, True])
 @pytest.mark.parametrize("bins", [1, 2, 4096, 1 << 16, 1 << 17, 1 << 20])
 def test_flow_hist_bin_regimes(bins, ws):
