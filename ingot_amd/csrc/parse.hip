@@ -792,17 +792,22 @@ __device__ __forceinline__ void apply_edit(const FR& f, EditSink& sink, uint32_t
 // positions), so a 32-bit input word = 8 LDS lookups.  Every instruction of
 // the hash reads one position p (all lanes), i.e. 16 entries; ds_read_b32
 // banks are (dword mod 32) per 32-lane group, so 16 entries stored once sit
-// in 16 banks (2-way+ conflicts).  Stored 2x interleaved — entry (p, v) copy
-// c at dword 32p + 2v + c, lane L reading copy L & 1 — each of the 32 banks
-// holds one address per instruction: conflict-free (lanes that share a bank
-// share the address: broadcast).  9 KiB per block, built once per block (the
-// flows grid is persistent).
+// in 16 banks (2-way+ conflicts).  FLOW_COPIES = 2 stores the table 2x
+// interleaved (entry (p, v) copy c at dword 32p + 2v + c, lane L reading copy
+// L & 1): conflict-free, 9 KiB.  One copy (4.5 KiB, the default) measured
+// faster on config 5 (390 vs 400 us/step): the smaller footprint fits 6
+// blocks per CU instead of 5, worth more than the conflicts cost.  Built once
+// per block (the flows grid is persistent).
 constexpr uint32_t FLOW_POS = FLOW_INPUT_BITS / 4;
-constexpr uint32_t FLOW_TAB = FLOW_POS * 32;
+#ifndef INGOT_FLOW_COPIES
+#define INGOT_FLOW_COPIES 1
+#endif
+constexpr uint32_t FLOW_COPIES = INGOT_FLOW_COPIES;
+constexpr uint32_t FLOW_TAB = FLOW_POS * 16 * FLOW_COPIES;
 
 __device__ __forceinline__ void build_flow_table(uint32_t* tab, const uint32_t* W) {
     for (uint32_t e = threadIdx.x; e < FLOW_TAB; e += BLOCK) {
-        const uint32_t p = e >> 5, v = (e >> 1) & 15u;
+        const uint32_t p = e / (16u * FLOW_COPIES), v = (e / FLOW_COPIES) & 15u;
         uint32_t acc = 0;
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) acc ^= ((v >> (3u - k)) & 1u) ? W[4u * p + k] : 0u;
@@ -862,12 +867,13 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 }
 
 // Toeplitz of the 9 words from the LDS nibble tables (LDS only).  Lookup
-// (position q, nibble v, copy cp) is at byte 128q + 8v + 4cp of the table; the
-// table is 128-B aligned, so the per-lane part (8v | 4cp | base) is one
-// shift + one v_and_or and the position rides in the ds_read offset.
+// (position q, nibble v, copy cp) is at byte 64C q + 4C v + 4cp of the table
+// (C = FLOW_COPIES); the table is 64C-B aligned, so the per-lane part
+// (4C v | 4cp | base) is one shift + one v_and_or and the position rides in
+// the ds_read offset.
 __device__ __forceinline__ uint32_t toeplitz9(const FlowWords& x, const uint32_t* tab) {
-    uint32_t base =
-        (uint32_t)(size_t)(const lds_u32*)tab + ((threadIdx.x & 1u) << 2);  // + table copy
+    uint32_t base = (uint32_t)(size_t)(const lds_u32*)tab +
+                    (FLOW_COPIES == 2 ? (threadIdx.x & 1u) << 2 : 0u);  // + table copy
     // opaque to the optimiser: otherwise it folds the position into the OR
     // (one extra v_or per lookup) instead of the ds_read offset
     asm volatile("" : "+v"(base));
@@ -877,10 +883,12 @@ __device__ __forceinline__ uint32_t toeplitz9(const FlowWords& x, const uint32_t
         uint32_t t[8];
 #pragma unroll
         for (uint32_t j = 0; j < 8; ++j) {
-            const uint32_t s = 28u - 4u * j;  // nibble j (MSB first) -> nibble * 8
-            const uint32_t v8 = s >= 3u ? (x.w[k] >> (s - 3u)) : (x.w[k] << (3u - s));
-            const lds_u32* e = (const lds_u32*)(size_t)((v8 & 0x78u) | base);
-            t[j] = e[(8u * k + j) * 32u];
+            // nibble j (MSB first) -> byte offset nibble * 4 * FLOW_COPIES
+            constexpr uint32_t L = FLOW_COPIES == 2 ? 3u : 2u;
+            const uint32_t s = 28u - 4u * j;
+            const uint32_t v8 = s >= L ? (x.w[k] >> (s - L)) : (x.w[k] << (L - s));
+            const lds_u32* e = (const lds_u32*)(size_t)((v8 & (15u << L)) | base);
+            t[j] = e[(8u * k + j) * 16u * FLOW_COPIES];
         }
         h = xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), xor3(t[6], t[7], h));
     }
@@ -905,7 +913,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
     // +16 dwords: the second dword of a pair read may run past the last image.
     // NCH = 0: no staging, every read goes to L2/HBM.
     __shared__ __attribute__((aligned(16))) uint32_t s_win[WAVES * WAVE_DW + 16];
-    __shared__ __attribute__((aligned(128))) uint32_t s_tab[MODE == OUT_FLOWS ? FLOW_TAB : 1];
+    __shared__ __attribute__((aligned(64 * FLOW_COPIES))) uint32_t s_tab[MODE == OUT_FLOWS ? FLOW_TAB : 1];
     if constexpr (MODE == OUT_FLOWS) {
         build_flow_table(s_tab, args.w);
         __syncthreads();
