@@ -48,25 +48,57 @@ __global__ __launch_bounds__(THREADS) void k_flow_hist(const uint32_t* __restric
 }
 
 constexpr uint32_t WORDS16 = 32768;  // packed 16-bit counters for 65,536 bins: 128 KiB
-constexpr uint64_t SLICE16 = 65535;  // flow ids per block: no counter wraps
+constexpr uint64_t SLICE16 = 65532;  // flow ids per block (a multiple of 4): no counter wraps
 
 __global__ __launch_bounds__(THREADS) void k_flow_count16(const uint32_t* __restrict__ flow,
                                                           uint64_t n, uint32_t bins,
-                                                          uint64_t slice,
+                                                          uint64_t slice, bool vec,
                                                           uint32_t* __restrict__ rows) {
-    __shared__ uint32_t cnt[WORDS16];
+    __shared__ __attribute__((aligned(16))) uint32_t cnt[WORDS16];
     const uint32_t words = (bins + 1u) / 2u;
-    for (uint32_t b = threadIdx.x; b < words; b += THREADS) cnt[b] = 0;
+    for (uint32_t b = 4u * threadIdx.x; b < words; b += 4u * THREADS)
+        *reinterpret_cast<uint4*>(cnt + b) = make_uint4(0, 0, 0, 0);
     __syncthreads();
+    auto count = [&](uint32_t d) {
+        if (d < bins) atomicAdd(&cnt[d >> 1], 1u << ((d & 1u) * 16u));
+    };
     const uint64_t lo = (uint64_t)blockIdx.x * slice;
     const uint64_t hi = lo + slice < n ? lo + slice : n;
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += THREADS) {
-        const uint32_t d = flow[i];
-        if (d < bins) atomicAdd(&cnt[d >> 1], 1u << ((d & 1u) * 16u));
+    // slices start 16-B aligned (slice % 4 == 0; vec: flow 16-B aligned): 16-B
+    // loads, UNROLL of them in flight per thread before the LDS atomics
+    constexpr uint32_t UNROLL = 4;
+    const uint64_t nv = vec && lo < hi ? (hi - lo) / 4u : 0u;
+    const uint4* fv = reinterpret_cast<const uint4*>(flow + lo);
+    uint64_t v = threadIdx.x;
+    for (; v + (UNROLL - 1u) * THREADS < nv; v += UNROLL * THREADS) {
+        uint4 x[UNROLL];
+#pragma unroll
+        for (uint32_t u = 0; u < UNROLL; ++u) x[u] = fv[v + u * THREADS];
+#pragma unroll
+        for (uint32_t u = 0; u < UNROLL; ++u) {
+            count(x[u].x);
+            count(x[u].y);
+            count(x[u].z);
+            count(x[u].w);
+        }
     }
+    for (; v < nv; v += THREADS) {
+        const uint4 x = fv[v];
+        count(x.x);
+        count(x.y);
+        count(x.z);
+        count(x.w);
+    }
+    for (uint64_t i = lo + 4u * nv + threadIdx.x; i < hi; i += THREADS) count(flow[i]);
     __syncthreads();
     uint32_t* row = rows + (uint64_t)blockIdx.x * words;
-    for (uint32_t b = threadIdx.x; b < words; b += THREADS) row[b] = cnt[b];
+    for (uint32_t b = 4u * threadIdx.x; b < words; b += 4u * THREADS) {
+        if (b + 4u <= words) {
+            *reinterpret_cast<uint4*>(row + b) = *reinterpret_cast<const uint4*>(cnt + b);
+        } else {
+            for (uint32_t q = b; q < words; ++q) row[q] = cnt[q];
+        }
+    }
 }
 
 // hist[bin] += sum over the g rows.  Block: 64 words x 4 row groups; every
@@ -80,6 +112,7 @@ __global__ __launch_bounds__(256) void k_flow_reduce16(const uint32_t* __restric
     const uint32_t w = blockIdx.x * 64u + lw;
     uint32_t a0 = 0, a1 = 0;
     if (w < words) {
+#pragma unroll 8
         for (uint32_t r = grp; r < g; r += 4) {
             const uint32_t c = rows[(uint64_t)r * words + w];
             a0 += c & 0xffffu;
@@ -148,10 +181,11 @@ hipError_t launch_flow_hist(const uint32_t* flow, uint64_t n, uint32_t* hist, ui
     if (need && work && work_bytes >= need) {
         const uint32_t g = rows_grid(n);
         const uint32_t words = (bins + 1u) / 2u;
-        const uint64_t slice = (n + g - 1) / g;
+        const uint64_t slice = ((n + g - 1) / g + 3u) & ~(uint64_t)3u;  // <= SLICE16
         auto* rows = static_cast<uint32_t*>(work);
+        const bool vec = ((uintptr_t)flow & 15u) == 0;
         hipLaunchKernelGGL(k_flow_count16, dim3(g), dim3(THREADS), 0, s, flow, n, bins, slice,
-                           rows);
+                           vec, rows);
         hipLaunchKernelGGL(k_flow_reduce16, dim3((words + 63u) / 64u), dim3(256), 0, s,
                            (const uint32_t*)rows, g, words, hist, bins);
         return hipGetLastError();
