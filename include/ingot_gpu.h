@@ -341,6 +341,23 @@ void ingot_gpu_ctx_destroy(ingot_gpu_ctx* ctx);
 int ingot_gpu_ctx_device(const ingot_gpu_ctx* ctx);
 
 /*
+ * Zero-copy host rings.  The path often starts and ends in host memory (a NIC
+ * or loopback ring).  ingot_gpu_host_map makes host memory [host, host+bytes)
+ * device-addressable — memory already pinned by hipHostMalloc is used as it
+ * is, pageable memory is page-locked and mapped (hipHostRegister, mapped) —
+ * and returns the device address of `host` in *d_ptr.  That address may be
+ * passed as any device pointer of the calls below (d_arena, descriptors,
+ * d_out ...): the kernels then read only the header bytes they touch across
+ * PCIe (LDS-DMA staging from host memory) instead of a whole-frame
+ * hipMemcpy, and can write records straight into host memory.  Results are
+ * identical to a device-resident arena.  ingot_gpu_host_unmap undoes a
+ * registration made by ingot_gpu_host_map (a no-op for hipHostMalloc memory).
+ * The caller keeps the bytes stable while a call that reads them runs.
+ */
+int ingot_gpu_host_map(ingot_gpu_ctx* ctx, void* host, size_t bytes, void** d_ptr);
+int ingot_gpu_host_unmap(ingot_gpu_ctx* ctx, void* host);
+
+/*
  * Tuning knobs (results never depend on them).  Defaults are the measured
  * best on MI355X; value 0 restores the default.
  *   INGOT_TUNE_WINDOW_INDEXED  16-B chunks staged in LDS per packed frame:

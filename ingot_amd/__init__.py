@@ -120,6 +120,24 @@ class Context:
     def get_tuning(self, key: int) -> int:
         return int(self._lib.ingot_gpu_ctx_get_tuning(self._h, int(key)))
 
+    def host_map(self, host) -> int:
+        """ingot_gpu_host_map: the device address of host memory (a pinned
+        torch tensor, or any C-contiguous numpy array / writable buffer, which
+        is then page-locked).  Pass it as a raw pointer to the C ABI: the
+        kernels read only the header bytes they touch across PCIe."""
+        if hasattr(host, "data_ptr"):
+            ptr, nbytes = host.data_ptr(), host.numel() * host.element_size()
+        else:
+            ptr, nbytes = host.ctypes.data, host.nbytes
+        d = ctypes.c_void_p()
+        _lib.check(self._lib.ingot_gpu_host_map(self._h, ptr, nbytes, ctypes.byref(d)),
+                   "ingot_gpu_host_map")
+        return int(d.value)
+
+    def host_unmap(self, host) -> None:
+        ptr = host.data_ptr() if hasattr(host, "data_ptr") else host.ctypes.data
+        _lib.check(self._lib.ingot_gpu_host_unmap(self._h, ptr), "ingot_gpu_host_unmap")
+
     def _check_dev(self, *tensors) -> None:
         for t in tensors:
             if t is not None and (not t.is_cuda or t.device.index != self.device):

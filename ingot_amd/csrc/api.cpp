@@ -9,7 +9,9 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
+#include <vector>
 
 #include "../../include/ingot_gpu.h"
 #include "kernels.h"
@@ -17,6 +19,9 @@
 struct ingot_gpu_ctx {
     int device;
     ingot_gpu::Tuning tuning;
+    // device address ranges of host memory mapped by ingot_gpu_host_map
+    std::mutex mu;
+    std::vector<std::pair<uintptr_t, uintptr_t>> host;
 };
 
 namespace {
@@ -46,6 +51,17 @@ int enter(const ingot_gpu_ctx* ctx) {
     return INGOT_GPU_SUCCESS;
 }
 
+// The context's tuning for a call over `arena`: frames in mapped host memory
+// get the host-arena window defaults (launch_parse).
+ingot_gpu::Tuning tuning_for(ingot_gpu_ctx* ctx, const void* arena) {
+    ingot_gpu::Tuning t = ctx->tuning;
+    const uintptr_t a = (uintptr_t)arena;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    for (const auto& r : ctx->host)
+        if (a >= r.first && a < r.second) t.host_arena = true;
+    return t;
+}
+
 int stride_ok(const uint8_t* d_arena, uint32_t stride) {
     if (stride == 0 || stride % 16u != 0 || stride > 65535u) return INGOT_GPU_ERANGE;
     if (((uintptr_t)d_arena & 15u) != 0) return INGOT_GPU_EINVAL;
@@ -61,7 +77,7 @@ int parse_indexed(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_
     if (int e = enter(ctx)) return e;
     ingot_gpu::ParseArgs a{d_arena, d_off, d_len, 0, n, d_out};
     return from_hip(ingot_gpu::launch_parse(a, ingot_gpu::LAYOUT_INDEXED, chain, mode,
-                                            ctx->tuning, (hipStream_t)stream));
+                                            tuning_for(ctx, d_arena), (hipStream_t)stream));
 }
 
 int parse_strided(ingot_gpu_ctx* ctx, const uint8_t* d_arena, uint32_t stride,
@@ -74,7 +90,7 @@ int parse_strided(ingot_gpu_ctx* ctx, const uint8_t* d_arena, uint32_t stride,
     if (int e = enter(ctx)) return e;
     ingot_gpu::ParseArgs a{d_arena, nullptr, d_len, stride, n, d_out};
     return from_hip(ingot_gpu::launch_parse(a, ingot_gpu::LAYOUT_STRIDED, chain, mode,
-                                            ctx->tuning, (hipStream_t)stream));
+                                            tuning_for(ctx, d_arena), (hipStream_t)stream));
 }
 
 // ingot_field -> (header kind, first bit, width): the setters' BE geometry
@@ -118,7 +134,7 @@ int parse_segmented(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* 
     if (int e = enter(ctx)) return e;
     ingot_gpu::ParseArgs a{d_arena, d_seg_off, d_seg_len, 0, n, d_out, d_pkt_seg, d_chunk};
     return from_hip(ingot_gpu::launch_parse(a, ingot_gpu::LAYOUT_SEGMENTED, chain, mode,
-                                            ctx->tuning, (hipStream_t)stream));
+                                            tuning_for(ctx, d_arena), (hipStream_t)stream));
 }
 
 }  // namespace
@@ -152,6 +168,45 @@ int ingot_gpu_ctx_create(int device, ingot_gpu_ctx** out) {
 void ingot_gpu_ctx_destroy(ingot_gpu_ctx* ctx) { delete ctx; }
 
 int ingot_gpu_ctx_device(const ingot_gpu_ctx* ctx) { return ctx ? ctx->device : -1; }
+
+int ingot_gpu_host_map(ingot_gpu_ctx* ctx, void* host, size_t bytes, void** d_ptr) {
+    if (!ctx || !host || !d_ptr || bytes == 0) return INGOT_GPU_EINVAL;
+    *d_ptr = nullptr;
+    if (int e = enter(ctx)) return e;
+    // already pinned and mapped (hipHostMalloc): use it as it is
+    hipPointerAttribute_t attr;
+    if (!(hipPointerGetAttributes(&attr, host) == hipSuccess && attr.type == hipMemoryTypeHost &&
+          hipHostGetDevicePointer(d_ptr, host, 0) == hipSuccess)) {
+        (void)hipGetLastError();  // clear the probe's error
+        if (hipHostRegister(host, bytes, hipHostRegisterMapped) != hipSuccess)
+            return INGOT_GPU_EHIP;
+        if (hipHostGetDevicePointer(d_ptr, host, 0) != hipSuccess) {
+            (void)hipHostUnregister(host);
+            *d_ptr = nullptr;
+            return INGOT_GPU_EHIP;
+        }
+    }
+    const uintptr_t d = (uintptr_t)*d_ptr;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    ctx->host.emplace_back(d, d + bytes);
+    return INGOT_GPU_SUCCESS;
+}
+
+int ingot_gpu_host_unmap(ingot_gpu_ctx* ctx, void* host) {
+    if (!ctx || !host) return INGOT_GPU_EINVAL;
+    if (int e = enter(ctx)) return e;
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, host, 0) == hipSuccess) {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        for (size_t i = 0; i < ctx->host.size(); ++i)
+            if (ctx->host[i].first == (uintptr_t)d) {
+                ctx->host.erase(ctx->host.begin() + (long)i);
+                break;
+            }
+    }
+    if (hipHostUnregister(host) != hipSuccess) (void)hipGetLastError();  // not registered by us
+    return INGOT_GPU_SUCCESS;
+}
 
 int ingot_gpu_ctx_set_tuning(ingot_gpu_ctx* ctx, int key, int value) {
     if (!ctx || !ingot_gpu::tuning_valid(key, value)) return INGOT_GPU_EINVAL;
@@ -293,7 +348,8 @@ int ingot_gpu_parse_modify(ingot_gpu_ctx* ctx, uint8_t* d_arena, const uint64_t*
     }
     if (int e = enter(ctx)) return e;
     a.p = ingot_gpu::ParseArgs{d_arena, d_off, d_len, stride, n, d_out};
-    return from_hip(ingot_gpu::launch_modify(a, layout, chain, ctx->tuning, (hipStream_t)stream));
+    return from_hip(ingot_gpu::launch_modify(a, layout, chain, tuning_for(ctx, d_arena),
+                                             (hipStream_t)stream));
 }
 
 int ingot_gpu_flow_hist_ws(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
@@ -333,7 +389,8 @@ int ingot_gpu_flow_hist_ws(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uin
         a.w[b] = w;
     }
     const hipStream_t s = (hipStream_t)stream;
-    if (int e = from_hip(ingot_gpu::launch_flows(a, layout, chain, ctx->tuning, s))) return e;
+    if (int e = from_hip(ingot_gpu::launch_flows(a, layout, chain, tuning_for(ctx, d_arena), s)))
+        return e;
     if (!d_hist) return INGOT_GPU_SUCCESS;
     return from_hip(ingot_gpu::launch_flow_hist(d_flow, n, d_hist, bins, d_work, work_bytes, s));
 }

@@ -71,6 +71,7 @@ struct Tuning {
     int writeback = 0;     // ring rewrite kernel: write-back unit (0 = measured default)
     int cache_policy = 0;  // bit 0: nt staging loads; bit 1: nt record stores
     uint32_t cus = 256;  // compute units of the context's device (grid shaping)
+    bool host_arena = false;  // per call: the arena is host memory (ingot_gpu_host_map)
 };
 
 hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, int mode,

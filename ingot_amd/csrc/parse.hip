@@ -1357,6 +1357,7 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
     // costs 19% (C3) / 15% (C3s).  4 = plain loads and stores.
     const bool ring = t.pipeline != 1 && !t.window_strided && layout_kind == LAYOUT_STRIDED &&
                       !a.len && chain != INGOT_CHAIN_GENEVE_OVER_V6 && a.stride >= 64u &&
+                      (a.stride == 64u || !t.host_arena) &&
                       (mode == OUT_REC16 || mode == OUT_REC8);
     if (t.cache_policy == 0) a.policy = mode == OUT_FIELDS ? 0u : ring ? 3u : 2u;
     else a.policy = (uint32_t)t.cache_policy & 3u;
@@ -1405,9 +1406,15 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
         return mode == OUT_REC8 ? launch_pipe<4, 2, OUT_REC8>(a, chain, pg, s)
                                 : launch_pipe<4, 2, OUT_REC16>(a, chain, pg, s);
     }
+    // Frames in mapped host memory (ingot_gpu_host_map, zero-copy over
+    // PCIe): a read past the window is a PCIe round trip per byte, so larger
+    // windows win there (measured, tools/hostpath.py --zero-copy, Mpkt/s:
+    // packed C3 202 / 221 / 230 / 211 at 3 / 4 / 5 / 8 chunks; 2048-B slots
+    // C3s 256 / 270 / 311 / 317 at 3 / 4 / 5 / 8).
+    const bool host = t.host_arena;
     if (layout_kind == LAYOUT_STRIDED) {
         const int w = t.window_strided ? t.window_strided
-                                       : tun ? 8 : (a.stride <= 64u ? 4 : 3);
+                      : tun ? 8 : (a.stride <= 64u ? 4 : host ? 8 : 3);
         if (w == 100) return launch_mode<0, LAYOUT_STRIDED>(a, chain, mode, g, s);
         if (w == 2) return launch_mode<2, LAYOUT_STRIDED>(a, chain, mode, g, s);
         if (w == 3) return launch_mode<3, LAYOUT_STRIDED>(a, chain, mode, g, s);
@@ -1415,7 +1422,7 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
         if (w == 5) return launch_mode<5, LAYOUT_STRIDED>(a, chain, mode, g, s);
         return launch_mode<8, LAYOUT_STRIDED>(a, chain, mode, g, s);
     }
-    switch (t.window_indexed ? t.window_indexed : tun ? 8 : 3) {
+    switch (t.window_indexed ? t.window_indexed : tun ? 8 : host ? 5 : 3) {
     case 100: return launch_mode<0, LAYOUT_INDEXED>(a, chain, mode, g, s);
     case 2: return launch_mode<2, LAYOUT_INDEXED>(a, chain, mode, g, s);
     case 3: return launch_mode<3, LAYOUT_INDEXED>(a, chain, mode, g, s);

@@ -1,0 +1,101 @@
+"""Zero-copy host rings (ingot_gpu_host_map): the kernels read frames straight
+from pinned host memory across PCIe and may write records into host memory.
+Results must be bit-identical to the device-resident path (which
+test_gpu_parity.py pins to the oracle) and to the oracle itself.  Needs an
+MI355X: `pytest -m gpu`."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import ingot_amd
+import oracle
+from ingot_amd import Chain, GenProfile
+from ingot_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.fixture(scope="module")
+def ctx(torch):
+    return ingot_amd.Context(0)
+
+
+def _pinned(torch, t):
+    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    h.copy_(t)
+    return h
+
+
+@pytest.mark.parametrize("profile,chain,stride", [
+    ("MIXED", Chain.GenericUlp, None), ("ADVERSARIAL", Chain.VlanUlp, None),
+    ("GENEVE_ADVERSARIAL", Chain.GeneveOverV6Tunnel, None),
+    ("V4UDP64", Chain.UdpParser, 64), ("VLAN_V6EH", Chain.VlanUlp, 256),
+])
+def test_parse_from_pinned_host_ring(torch, ctx, profile, chain, stride):
+    """Arena (and descriptors) in hipHostMalloc memory, records written into
+    pinned host memory: equal to the device-resident records and the oracle."""
+    n = 50_001
+    lib = _lib.load()
+    arena, off, lens = ingot_amd.gen_frames(GenProfile[profile], n, seed=21, stride=stride)
+    want = (ctx.parse_strided(arena, stride, n, chain, lens=lens) if stride
+            else ctx.parse(arena, off, lens, chain))
+    torch.cuda.synchronize()
+    h_arena = _pinned(torch, arena)
+    h_out = torch.zeros((n, 16), dtype=torch.uint8, pin_memory=True)
+    d_arena, d_out = ctx.host_map(h_arena), ctx.host_map(h_out)
+    if stride:
+        h_lens = _pinned(torch, lens) if lens is not None else None
+        d_lens = ctx.host_map(h_lens) if h_lens is not None else None
+        rc = lib.ingot_gpu_parse_strided(ctx._h, d_arena, stride, d_lens, n, int(chain), d_out,
+                                         None)
+    else:
+        h_off, h_lens = _pinned(torch, off), _pinned(torch, lens)
+        rc = lib.ingot_gpu_parse(ctx._h, d_arena, ctx.host_map(h_off), ctx.host_map(h_lens), n,
+                                 int(chain), d_out, None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert h_out.numpy().tobytes() == want.cpu().numpy().tobytes()
+    w = oracle.parse_batch(h_arena.numpy(), None if stride else off.cpu().numpy(),
+                           None if lens is None else lens.cpu().numpy(), chain,
+                           stride=stride or 0, n=n, nthreads=8)
+    assert h_out.numpy().tobytes() == w.tobytes()
+
+
+def test_parse_from_registered_pageable_memory(torch, ctx):
+    """Pageable numpy memory is page-locked and mapped by ingot_gpu_host_map
+    (hipHostRegister) and released by ingot_gpu_host_unmap."""
+    n = 20_000
+    lib = _lib.load()
+    arena, off, lens = ingot_amd.gen_frames(GenProfile.MIXED, n, seed=5)
+    want = ctx.parse(arena, off, lens, Chain.GenericUlp)
+    torch.cuda.synchronize()
+    raw = np.zeros(arena.numel() + 8192, dtype=np.uint8)
+    a = raw[(-raw.ctypes.data) % 4096:][:arena.numel()]  # page-aligned view
+    a[:] = arena.cpu().numpy()
+    d_arena = ctx.host_map(a)
+    out = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
+    assert lib.ingot_gpu_parse(ctx._h, d_arena, off.data_ptr(), lens.data_ptr(), n,
+                               int(Chain.GenericUlp), out.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    ctx.host_unmap(a)
+    assert out.cpu().numpy().tobytes() == want.cpu().numpy().tobytes()
+
+
+def test_host_map_rejects_bad_arguments(ctx):
+    lib = _lib.load()
+    d = ctypes.c_void_p()
+    assert lib.ingot_gpu_host_map(ctx._h, None, 64, ctypes.byref(d)) == -1
+    buf = np.zeros(64, np.uint8)
+    assert lib.ingot_gpu_host_map(ctx._h, buf.ctypes.data, 0, ctypes.byref(d)) == -1
+    assert lib.ingot_gpu_host_map(None, buf.ctypes.data, 64, ctypes.byref(d)) == -1
+    assert lib.ingot_gpu_host_unmap(ctx._h, None) == -1

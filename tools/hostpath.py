@@ -5,7 +5,12 @@ parse -> records D2H into pinned host memory.  Steps are pipelined over S
 streams (copy of batch k+1 overlaps the parse of batch k).  Reported in
 DESIGN.md; never the bench `value` (which is device-resident).
 
-    python tools/hostpath.py [--config c2|c3] [--streams 3] [--steps 200]
+    python tools/hostpath.py [--config c2|c3] [--streams 3] [--steps 200] [--zero-copy]
+
+--zero-copy: no copies at all.  The arena, its descriptors and the records
+stay in pinned host memory mapped for the device (ingot_gpu_host_map); the
+kernels read only the header bytes they touch across PCIe and write records
+straight back.
 """
 from __future__ import annotations
 
@@ -25,6 +30,8 @@ def main():
     ap.add_argument("--frames", type=int, default=1 << 20)
     ap.add_argument("--streams", type=int, default=3)
     ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--zero-copy", action="store_true")
+    ap.add_argument("--win", type=int, default=0, help="staged window (INGOT_TUNE_WINDOW_*)")
     args = ap.parse_args()
 
     import torch
@@ -37,6 +44,9 @@ def main():
     n = args.frames
     chain = Chain[chain_name]
     ctx = ingot_amd.Context(0)
+    if args.win:
+        from ingot_amd.abi import TUNE_WINDOW_INDEXED, TUNE_WINDOW_STRIDED
+        ctx.set_tuning(TUNE_WINDOW_STRIDED if stride else TUNE_WINDOW_INDEXED, args.win)
     arena, off, lens = ingot_amd.gen_frames(GenProfile[prof], n, stride=stride)
     S = args.streams
     streams = [torch.cuda.Stream() for _ in range(S)]
@@ -47,9 +57,14 @@ def main():
     host_recs = [torch.empty((n, 16), dtype=torch.uint8, pin_memory=True) for _ in range(R)]
     dev_arena = [torch.empty_like(arena) for _ in range(S)]
     dev_recs = [torch.empty((n, 16), dtype=torch.uint8, device="cuda") for _ in range(S)]
-    # descriptors live on the device (a ring's descriptor table would be
-    # copied too: add 10 B/pkt; counted below)
-    desc_bytes = 0 if stride else n * 10
+    # descriptors travel with the frames: 10 B/pkt (u64 off + u16 len) for
+    # packed frames, 2 B/pkt (u16 len) for slots with a length table
+    desc_bytes = (2 * n if lens is not None else 0) if stride else n * 10
+    host_slot_lens = None
+    if stride and lens is not None:
+        host_slot_lens = torch.empty(n, dtype=torch.uint16, pin_memory=True)
+        host_slot_lens.copy_(lens)
+        dev_slot_lens = [torch.empty_like(lens) for _ in range(S)]
     host_desc = None
     if off is not None:
         host_desc = (torch.empty(n, dtype=torch.int64, pin_memory=True),
@@ -58,7 +73,27 @@ def main():
         host_desc[1].copy_(lens)
         dev_desc = [(torch.empty_like(off), torch.empty_like(lens)) for _ in range(S)]
 
+    lib = ingot_amd.load_library()
+    if args.zero_copy:
+        d_arena = [ctx.host_map(h) for h in host_arena]
+        d_recs = [ctx.host_map(h) for h in host_recs]
+        d_off = ctx.host_map(host_desc[0]) if host_desc is not None else None
+        d_len = ctx.host_map(host_desc[1]) if host_desc is not None else None
+        d_slot_lens = ctx.host_map(host_slot_lens) if host_slot_lens is not None else None
+
+    def step_zc(k):
+        s = streams[k % S].cuda_stream
+        if host_desc is not None:
+            rc = lib.ingot_gpu_parse(ctx._h, d_arena[k % R], d_off, d_len, n, int(chain),
+                                     d_recs[k % R], s)
+        else:
+            rc = lib.ingot_gpu_parse_strided(ctx._h, d_arena[k % R], stride, d_slot_lens, n,
+                                             int(chain), d_recs[k % R], s)
+        assert rc == 0
+
     def step(k):
+        if args.zero_copy:
+            return step_zc(k)
         s = streams[k % S]
         with torch.cuda.stream(s):
             dev_arena[k % S].copy_(host_arena[k % R], non_blocking=True)
@@ -68,8 +103,12 @@ def main():
                 ln.copy_(host_desc[1], non_blocking=True)
                 ctx.parse(dev_arena[k % S], o, ln, chain, out=dev_recs[k % S], stream=s)
             else:
-                ctx.parse_strided(dev_arena[k % S], stride, n, chain, out=dev_recs[k % S],
-                                  stream=s)
+                sl = None
+                if host_slot_lens is not None:
+                    sl = dev_slot_lens[k % S]
+                    sl.copy_(host_slot_lens, non_blocking=True)
+                ctx.parse_strided(dev_arena[k % S], stride, n, chain, lens=sl,
+                                  out=dev_recs[k % S], stream=s)
             host_recs[k % R].copy_(dev_recs[k % S], non_blocking=True)
 
     for k in range(2 * S):
@@ -89,15 +128,20 @@ def main():
     torch.cuda.synchronize()
     h2d_gbs = 50 * arena.numel() / (time.perf_counter() - t1) / 1e9
     res = {
-        "config": args.config, "frames_per_batch": n, "streams": S, "steps": args.steps,
+        "config": args.config, "mode": "zero-copy" if args.zero_copy else "memcpy",
+        "window": args.win or "default",
+        "frames_per_batch": n, "streams": S, "steps": args.steps,
         "host_inclusive_Mpkt_s": round(n * args.steps / dt / 1e6, 1),
         "ms_per_batch": round(dt / args.steps * 1e3, 4),
         "bytes_h2d_per_batch": h2d, "bytes_d2h_per_batch": d2h,
         "pcie_GBps_effective": round((h2d + d2h) * args.steps / dt / 1e9, 2),
         "h2d_copy_only_GBps": round(h2d_gbs, 2),
     }
+    if args.zero_copy:
+        res["note"] = ("zero-copy: nothing is copied; bytes_h2d/pcie_GBps_effective count what "
+                       "the memcpy path would move for the same batch")
     print(json.dumps(res))
-    out = ROOT / "gpurun_out" / f"hostpath_{args.config}.json"
+    out = ROOT / "gpurun_out" / f"hostpath_{args.config}{'_zc' if args.zero_copy else ''}.json"
     out.parent.mkdir(exist_ok=True)
     out.write_text(json.dumps(res, indent=1))
 
