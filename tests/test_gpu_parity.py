@@ -328,3 +328,78 @@ def test_config3_full_size_properties(ctx, torch):
         assert got[k].tobytes() == orec.tobytes(), idx[k]
     del arena, off, lens, recs, recs2
     torch.cuda.empty_cache()
+
+
+def test_config4_shard_full_size_and_shard_consistency(ctx, torch):
+    """Config 4 at its per-GPU size: one 8,388,608-frame shard of the 64 M
+    VLAN/QinQ + IPv6-EH batch (VlanUlp).  Properties over the whole shard, a
+    sampled oracle re-check, and shard consistency: the generator is pure in
+    (seed, index), so rank r's shard equals frames [r*n, (r+1)*n) of one
+    larger generation — the 8-GPU batch is the 1-GPU batch cut in eight."""
+    from ingot_amd import dist as idist
+
+    n = 8 * (1 << 20)
+    first, n = idist.shard(3, 8, n)
+    arena, off, lens = ingot_amd.gen_frames(GenProfile.VLAN_V6EH, n, first=first)
+    recs = ctx.parse(arena, off, lens, Chain.VlanUlp)
+    torch.cuda.synchronize()
+    assert int((recs[:, 0] != 0).sum()) == 0
+    nvlan = recs[:, 4].to(torch.int64)
+    assert 0.45 < float((nvlan > 0).double().mean()) < 0.55
+    assert int((nvlan > 2).sum()) == 0
+    v6 = recs[:, 2] == 2
+    assert 0.45 < float(v6.double().mean()) < 0.55
+    assert int((recs[:, 5][v6] > 0).sum()) > 0  # extension headers occur
+    idx = np.random.default_rng(1).choice(n, 2048, replace=False)
+    offs, ls = host(off)[idx], host(lens)[idx]
+    got = ingot_amd.records_to_numpy(recs[torch.as_tensor(idx, device=recs.device)])
+    for k, (o, ln) in enumerate(zip(offs, ls)):
+        orec, _ = oracle.parse_one(host(arena[int(o):int(o) + int(ln)]).tobytes(), Chain.VlanUlp)
+        assert got[k].tobytes() == orec.tobytes(), idx[k]
+    # shard consistency: the first 1000 frames of this shard, regenerated as
+    # part of a batch that starts 1000 frames earlier, have the same lengths,
+    # header bytes and records (payload filler depends on the arena position)
+    a2, o2, l2 = ingot_amd.gen_frames(GenProfile.VLAN_V6EH, 2000, first=first - 1000)
+    assert torch.equal(l2[1000:].cpu(), lens[:1000].cpu())
+    r2 = ctx.parse(a2, o2, l2, Chain.VlanUlp)
+    torch.cuda.synchronize()
+    assert torch.equal(r2[1000:], recs[:1000])
+    poff = ingot_amd.records_to_numpy(recs[:1000])["payload_off"]
+    for k in range(0, 1000, 7):
+        f1 = arena[int(off[k]):int(off[k]) + int(poff[k])]
+        f2 = a2[int(o2[1000 + k]):int(o2[1000 + k]) + int(poff[k])]
+        assert torch.equal(f1, f2), k
+    del arena, off, lens, recs
+    torch.cuda.empty_cache()
+
+
+def test_config5_full_size_flow_histogram(ctx, torch):
+    """Config 5 at its per-GPU size (8,388,608 frames, 65,536 bins): the
+    histogram is the bincount of the per-packet flow ids, counts every Ok
+    packet with an L3 layer exactly once, and sampled flow ids equal the
+    oracle's hash of the frame."""
+    n = 8 * (1 << 20)
+    arena, off, lens = ingot_amd.gen_frames(GenProfile.FLOWS, n)
+    hist = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")
+    hashes = torch.zeros(n, dtype=torch.int32, device="cuda")
+    flow = ctx.flow_hist(arena, off, lens, Chain.VlanUlp, hist=hist, n=n, hashes=hashes,
+                         workspace=ctx.flow_hist_workspace(n, 1 << 16))
+    recs = ctx.parse(arena, off, lens, Chain.VlanUlp)
+    torch.cuda.synchronize()
+    f = flow.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    counted = f != 0xFFFFFFFF
+    want = torch.bincount(f[counted], minlength=1 << 16)
+    assert torch.equal(hist.to(torch.int64), want)
+    ok_l3 = (recs[:, 0] == 0) & (recs[:, 2] != 0)
+    assert torch.equal(counted, ok_l3)
+    assert int(hist.to(torch.int64).sum()) == int(ok_l3.sum())
+    idx = np.random.default_rng(2).choice(n, 2048, replace=False)
+    offs, ls = host(off)[idx], host(lens)[idx]
+    g_hash = hashes.cpu().numpy().view(np.uint32)[idx]
+    for k, (o, ln) in enumerate(zip(offs, ls)):
+        fr = host(arena[int(o):int(o) + int(ln)])
+        _, w = oracle.flow_hist(np.concatenate([fr, np.zeros(8, np.uint8)]), np.array([0]),
+                                np.array([int(ln)]), Chain.VlanUlp)
+        assert g_hash[k] == w[0], idx[k]
+    del arena, off, lens, recs, flow, hashes
+    torch.cuda.empty_cache()
