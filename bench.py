@@ -31,6 +31,7 @@ launch streams.  `cpu_baseline` = the C restatement of ingot's parse
 from __future__ import annotations
 
 import argparse
+import collections
 import json
 import os
 import sys
@@ -227,17 +228,22 @@ class ReadRunner:
 
 
 class FlowRunner:
-    """Config 5 step: zero the histogram, parse + hash + histogram kernel,
-    then the RCCL all-reduce of the histogram (one stream: the reduce of step k
-    must see step k's counts)."""
+    """Config 5 step: zero the histogram, parse + hash + histogram kernels,
+    then the RCCL all-reduce of that step's histogram.  The all-reduce runs on
+    RCCL's stream and overlaps the next step's kernels (histograms rotate over
+    the arena copies, so a step's buffer is reused only after its reduce has
+    been waited for, at most two steps later); the timed region ends after
+    every reduce has completed."""
 
     def __init__(self, torch, lib, ctx, chain, n, arenas, off, lens, hists, flows, stream,
                  reduce_fn):
         self.torch, self.streams = torch, [stream]
         reps = len(arenas)
+        assert reps >= 4
         h, sp, c = ctx._h, stream.cuda_stream, int(chain)
         optr, lptr = off.data_ptr(), lens.data_ptr()
         aptrs = [a.data_ptr() for a in arenas]
+        pending = collections.deque()
 
         # caller-owned workspace: the atomics-free histogram pass
         wbytes = lib.ingot_gpu_flow_hist_workspace_size(n, hists[0].numel())
@@ -246,22 +252,33 @@ class FlowRunner:
 
         def launch(k):
             hist = hists[k % reps]
+            while len(pending) > 1:  # the reduce of step k-2 before its buffer returns
+                pending.popleft().wait()
             hist.zero_()
             rc = lib.ingot_gpu_flow_hist_ws(h, aptrs[k % reps], optr, lptr, 0, n, c, None,
                                             hist.numel(), flows[k % reps].data_ptr(), None,
                                             hist.data_ptr(), wptr, wbytes, sp)
-            reduce_fn(hist)
+            with torch.cuda.stream(stream):
+                w = reduce_fn(hist)
+            if w is not None:
+                pending.append(w)
             return rc
 
-        self.launch = launch
+        def finish():
+            with torch.cuda.stream(stream):
+                while pending:
+                    pending.popleft().wait()
+
+        self.launch, self.finish = launch, finish
 
     def run(self, steps):
-        return _timed(self.torch, self.streams, self.launch, steps)
+        return _timed(self.torch, self.streams, self.launch, steps, self.finish)
 
 
-def _timed(torch, streams, launch, steps):
+def _timed(torch, streams, launch, steps, finish=None):
     """Run `steps` launches between two HIP events on streams[0]; the other
-    streams fork from the start event and join before the end event."""
+    streams fork from the start event and join before the end event (as does
+    `finish`'s outstanding work)."""
     s0 = streams[0]
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
@@ -273,6 +290,8 @@ def _timed(torch, streams, launch, steps):
         rc = launch(k)
         if rc:
             raise RuntimeError(f"launch failed: {rc}")
+    if finish is not None:
+        finish()
     for s in streams[1:]:
         ev = torch.cuda.Event()
         ev.record(s)
@@ -361,7 +380,7 @@ def main():
     def runner(nstreams, record):
         if flows:
             return FlowRunner(torch, lib, ctx, chain, n, arenas, off, lens, hists, flow_ids,
-                              streams[0], idist.reduce_histogram)
+                              streams[0], idist.reduce_histogram_async)
         if mode == "modify":
             return ModifyRunner(torch, lib, ctx, chain, n, stride, arenas, off, lens,
                                 streams[:nstreams])

@@ -65,3 +65,25 @@ def reduce_histogram(hist):
     else:
         dist.all_reduce(view, op=dist.ReduceOp.SUM)
     return hist
+
+
+class _Done:
+    def wait(self):
+        return None
+
+
+def reduce_histogram_async(hist):
+    """As reduce_histogram, without making the caller's stream wait: returns
+    a handle whose wait() orders the caller's current stream after the
+    all-reduce (RCCL: the collective runs on its own stream, so the next
+    batch's kernels overlap it).  The gloo rehearsal path completes at once."""
+    import torch
+    import torch.distributed as dist
+
+    if not _active():
+        return _Done()
+    view = hist.view(torch.int32) if hist.dtype != torch.int32 else hist
+    if _gloo():
+        reduce_histogram(hist)
+        return _Done()
+    return dist.all_reduce(view, op=dist.ReduceOp.SUM, async_op=True)

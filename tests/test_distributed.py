@@ -35,7 +35,11 @@ def _worker(rank, world, port, q):
         arena, off, lens = pack(frames[first:first + n])
         hist, _ = oracle.flow_hist(arena, off, lens, Chain.VlanUlp, bins=4096)
         t = torch.from_numpy(hist.astype(np.uint32).view(np.int32).copy())
+        t2 = t.clone()
         idist.reduce_histogram(t)
+        # the overlapped form bench.py uses: a handle, then wait()
+        idist.reduce_histogram_async(t2).wait()
+        assert torch.equal(t, t2)
         slowest = idist.max_over_ranks(0.5 + rank)
         if rank == 0:
             q.put((t.numpy().view(np.uint32).copy(), slowest))

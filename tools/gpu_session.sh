@@ -1,4 +1,5 @@
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-tools/gpu_step.sh 600 pytest_gpu python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread
+tools/gpu_step.sh 300 ab_c5 python tools/abtune.py --config c5 --rounds 3 --var mode=flows --var mode=parse --out gpurun_out/ab_c5.json
+tools/gpu_step.sh 300 ab_c2 python tools/abtune.py --config c2 --rounds 3 --var streams=2 --var streams=1 --out gpurun_out/ab_c2.json
