@@ -489,6 +489,67 @@ inline std::vector<ReadResult> parse_read_batch(Context& ctx, const std::vector<
     return out;
 }
 
+// ingot's generated setters (`set_<field>`, packet/mod.rs:2097-2255; BE
+// bitfield set paths, bitfield.rs:188-315), batched: every frame is parsed as
+// `chain` and, when Ok, the edit list is applied in order in place
+// (ingot_gpu_parse_modify).  Returns the rewritten frames and their records.
+inline ingot_edit edit(uint8_t layer, int field, int op, uint32_t value, uint8_t index = 0) {
+    ingot_edit e;
+    e.layer = layer;
+    e.field = (uint8_t)field;
+    e.op = (uint8_t)op;
+    e.index = index;
+    e.value = value;
+    return e;
+}
+
+struct Modified {
+    std::vector<uint8_t> frame;
+    ingot_rec rec;
+};
+
+inline std::vector<Modified> modify_batch(Context& ctx,
+                                          const std::vector<std::vector<uint8_t>>& frames,
+                                          int chain, const std::vector<ingot_edit>& edits) {
+    const size_t n = frames.size();
+    std::vector<uint64_t> off(n);
+    std::vector<uint16_t> len(n);
+    size_t total = 0;
+    for (size_t i = 0; i < n; ++i) {
+        if (frames[i].size() > 65535) throw std::length_error("frame longer than 65535 bytes");
+        off[i] = total;
+        len[i] = (uint16_t)frames[i].size();
+        total += (frames[i].size() + 15) / 16 * 16 + 16;
+    }
+    std::vector<uint8_t> arena(total + 64, 0);
+    for (size_t i = 0; i < n; ++i)
+        if (!frames[i].empty()) std::memcpy(arena.data() + off[i], frames[i].data(), frames[i].size());
+    uint8_t* d_arena = nullptr;
+    uint64_t* d_off = nullptr;
+    uint16_t* d_len = nullptr;
+    ingot_rec* d_rec = nullptr;
+    hip_check(hipMalloc(&d_arena, arena.size()), "hipMalloc");
+    hip_check(hipMalloc(&d_off, n * 8 + 8), "hipMalloc");
+    hip_check(hipMalloc(&d_len, n * 2 + 8), "hipMalloc");
+    hip_check(hipMalloc(&d_rec, n * sizeof(ingot_rec) + 16), "hipMalloc");
+    hip_check(hipMemcpy(d_arena, arena.data(), arena.size(), hipMemcpyHostToDevice), "H2D");
+    hip_check(hipMemcpy(d_off, off.data(), n * 8, hipMemcpyHostToDevice), "H2D");
+    hip_check(hipMemcpy(d_len, len.data(), n * 2, hipMemcpyHostToDevice), "H2D");
+    check(ingot_gpu_parse_modify(ctx.get(), d_arena, d_off, d_len, 0, n, chain, edits.data(),
+                                 (uint32_t)edits.size(), d_rec, nullptr),
+          "ingot_gpu_parse_modify");
+    std::vector<ingot_rec> rec(n);
+    hip_check(hipMemcpy(arena.data(), d_arena, arena.size(), hipMemcpyDeviceToHost), "D2H");
+    hip_check(hipMemcpy(rec.data(), d_rec, n * sizeof(ingot_rec), hipMemcpyDeviceToHost), "D2H");
+    std::vector<Modified> out(n);
+    for (size_t i = 0; i < n; ++i) {
+        out[i].frame.assign(arena.begin() + (long)off[i], arena.begin() + (long)(off[i] + len[i]));
+        out[i].rec = rec[i];
+    }
+    for (void* p : {(void*)d_arena, (void*)d_off, (void*)d_len, (void*)d_rec}) (void)hipFree(p);
+    return out;
+}
+
 inline Context& default_context() {
     static Context ctx(0);
     return ctx;
@@ -572,6 +633,8 @@ inline std::vector<uint8_t> remainder(const Packet& p) {
 // The Packet is shared so the views outlive the temporary batch.
 struct UdpParser {
     static constexpr int CHAIN = INGOT_CHAIN_UDP_PARSER;
+    // edit layers = label indices (eth, l3, l4)
+    static constexpr uint8_t ETH_LAYER = 0, L3_LAYER = 1, L4_LAYER = 2;
     std::shared_ptr<const Packet> pkt;
     ValidEthernet eth;
     L3 l3;
@@ -611,6 +674,7 @@ struct UdpParser {
 // inner_l3: Option<L3>, inner_ulp: Option<Ulp>.
 struct GenericUlp {
     static constexpr int CHAIN = INGOT_CHAIN_GENERIC_ULP;
+    static constexpr uint8_t INNER_ETH_LAYER = 0, INNER_L3_LAYER = 1, INNER_ULP_LAYER = 2;
     std::shared_ptr<const Packet> pkt;
     ValidEthernet inner_eth;
     std::optional<L3> inner_l3;
@@ -656,6 +720,9 @@ struct GenericUlp {
 // outer_udp: from L4 -> Udp, outer_encap: Geneve, then GenericUlp's layers.
 struct GeneveOverV6Tunnel {
     static constexpr int CHAIN = INGOT_CHAIN_GENEVE_OVER_V6;
+    static constexpr uint8_t OUTER_ETH_LAYER = 0, OUTER_V6_LAYER = 1, OUTER_UDP_LAYER = 2,
+                             OUTER_ENCAP_LAYER = 3, INNER_ETH_LAYER = 4, INNER_L3_LAYER = 5,
+                             INNER_ULP_LAYER = 6;
     std::shared_ptr<const Packet> pkt;
     ValidEthernet outer_eth;
     ValidOuterIpv6 outer_v6;

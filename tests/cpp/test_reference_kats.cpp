@@ -357,6 +357,78 @@ TEST(straddle_failure) {
     ASSERT_EQ(std::string(e.header()), "inner_l3");
 }
 
+// ingot-examples/benches/packet.rs:15-35 (pkt_body_v4) and :139-145
+// (parse-and-decr-v4: l4.set_destination(l4.destination() - 1)), over a batch.
+static std::vector<uint8_t> pkt_body_v4() {
+    std::vector<uint8_t> f(14, 0);
+    for (int i = 6; i < 12; ++i) f[i] = 0xff;
+    f[12] = 0x08;
+    const uint8_t v4[20] = {0x45, 0, 0, 28 + 8, 0, 0, 0, 0, 0xf0, 0x11, 0, 0,
+                            192, 168, 0, 1, 192, 168, 0, 255};
+    const uint8_t udp[8] = {0x00, 0x80, 0x17, 0xc1, 0x00, 0x08, 0x00, 0x00};
+    f.insert(f.end(), v4, v4 + 20);
+    f.insert(f.end(), udp, udp + 8);
+    for (uint8_t b = 0; b < 8; ++b) f.push_back(b);
+    return f;
+}
+
+TEST(parse_and_decr_v4) {
+    const auto f = pkt_body_v4();
+    std::vector<std::vector<uint8_t>> batch(1000, f);
+    auto out = gpu::modify_batch(
+        gpu::default_context(), batch, UdpParser::CHAIN,
+        {gpu::edit(UdpParser::L4_LAYER, INGOT_F_UDP_DESTINATION, INGOT_OP_SUB, 1)});
+    ASSERT_EQ(out.size(), 1000u);
+    for (const auto& m : out) {
+        ASSERT_EQ((int)m.rec.status, (int)INGOT_OK);
+        auto [h, hint, rest] = UdpParser::parse(m.frame).unwrap();
+        (void)hint;
+        (void)rest;
+        ASSERT_EQ(h.l4.destination(), 0x17c0);
+        ASSERT_EQ(h.l4.source(), 0x0080);
+        std::vector<uint8_t> want = f;
+        want[37] = 0xc0;
+        ASSERT_EQ(m.frame, want);
+    }
+}
+
+// ingot/src/tests.rs:223-294 — setting each bitfield of the IPv6 header to
+// the value it already holds (cumulatively, iterations 0..4) leaves every
+// other field, and the bytes, unchanged.
+TEST(bitset_fields_do_not_disturb_neighbours) {
+    const uint8_t golden[4] = {0x6A, 0x61, 0xe2, 0x40};
+    const uint8_t v6[40] = {0x6A, 0x61, 0xe2, 0x40, 0x00, 0x10, 0x11, 0xf0,
+                            0xFD, 0x00, 0x00, 0x00, 0x00, 0xF7, 0x01, 0x01,
+                            0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x02,
+                            0xFD, 0x00, 0x00, 0x00, 0x00, 0xF7, 0x01, 0x01,
+                            0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x01};
+    std::vector<uint8_t> pkt(14, 0);
+    put16(pkt, 12, ethernet::Ethertype::IPV6);
+    pkt.insert(pkt.end(), v6, v6 + 40);
+    pkt.insert(pkt.end(), {0, 7, 0, 9, 0, 8, 0, 0});  // UDP (v6 next_header 0x11)
+    const uint8_t L = UdpParser::L3_LAYER;
+    const std::vector<ingot_edit> setters = {
+        gpu::edit(L, INGOT_F_V6_VERSION, INGOT_OP_SET, 6),
+        gpu::edit(L, INGOT_F_V6_DSCP, INGOT_OP_SET, 41),
+        gpu::edit(L, INGOT_F_V6_ECN, INGOT_OP_SET, (uint32_t)ip::Ecn::Capable1),
+        gpu::edit(L, INGOT_F_V6_FLOW_LABEL, INGOT_OP_SET, 123456),
+    };
+    for (size_t i = 0; i < 5; ++i) {
+        std::vector<ingot_edit> upto(setters.begin(), setters.begin() + (i ? i : 0));
+        auto m = gpu::modify_batch(gpu::default_context(), {pkt}, UdpParser::CHAIN, upto)[0];
+        auto [h, hint, rest] = UdpParser::parse(m.frame).unwrap();
+        (void)hint;
+        (void)rest;
+        ASSERT_TRUE(h.l3.ipv6.has_value());
+        ASSERT_EQ(h.l3.ipv6->version(), 6);
+        ASSERT_EQ(h.l3.ipv6->dscp(), 41);
+        ASSERT_EQ(h.l3.ipv6->ecn(), ip::Ecn::Capable1);
+        ASSERT_EQ(h.l3.ipv6->flow_label(), 123456u);
+        for (int k = 0; k < 4; ++k) ASSERT_EQ(m.frame[14 + k], golden[k]);
+        ASSERT_EQ(m.frame, pkt);
+    }
+}
+
 int main() {
     for (auto& [name, fn] : registry()) {
         ++g_run;
