@@ -1,0 +1,174 @@
+"""bench.py's accounting, on CPU: the SURVEY §8d algorithmic bytes behind
+`roofline.achieved`, the config table, and the C5 runner's overlap of the
+per-step histogram all-reduce (every reduce waited before the timed region
+ends; a buffer reused only after its reduce)."""
+import numpy as np
+
+import bench
+import oracle
+from ingot_amd import REC_DTYPE, Chain
+from tests.frames import build_frames, pack
+
+
+def test_algorithmic_bytes_c2_shape():
+    """C2: 64-B slots, 42-B header span -> R = 64, W = 16: 80 B per packet."""
+    n = 1000
+    recs = np.zeros(n, dtype=REC_DTYPE)
+    recs["payload_off"] = 42
+    rd, wr = bench.algorithmic_bytes(recs, None, 64, 0, 16)
+    assert (rd, wr) == (64 * n, 16 * n)
+    assert bench.algorithmic_bytes(recs, None, 64, 0, 8) == (64 * n, 8 * n)
+
+
+def test_algorithmic_bytes_rule():
+    """R_i = min(len_i, 128) + max(0, H_i - 128) + D, per packet."""
+    recs = np.zeros(4, dtype=REC_DTYPE)
+    recs["payload_off"] = [42, 128, 200, 90]
+    lens = np.array([60, 1500, 1500, 100], dtype=np.uint16)
+    rd, wr = bench.algorithmic_bytes(recs, lens, 0, 10, 16)
+    assert rd == (60 + 10) + (128 + 10) + (128 + 72 + 10) + (100 + 10)
+    assert wr == 64
+
+
+def test_algorithmic_bytes_of_oracle_records():
+    """On real records: the header span never exceeds the frame, so
+    R_i <= len_i + D, and R_i >= min(len_i, 128)."""
+    frames = build_frames(500, seed=3)
+    arena, off, lens = pack(frames)
+    recs = oracle.parse_batch(arena, off, lens, Chain.GenericUlp).view(REC_DTYPE)
+    rd, _ = bench.algorithmic_bytes(recs, lens, 0, 10, 16)
+    L = lens.astype(np.int64)
+    assert np.minimum(L, 128).sum() + 10 * len(L) <= rd <= L.sum() + 10 * len(L)
+
+
+def test_config_table():
+    for name, (prof, n, stride, chain, desc) in bench.CONFIGS.items():
+        assert n > 0 and desc
+        assert stride is None or (stride % 16 == 0 and stride >= 64)
+        Chain[chain]
+    # the metric's configuration (BASELINE.json configs[1]) is the default
+    assert bench.CONFIGS["c2"][:4] == ("V4UDP64", 1 << 20, 64, "UdpParser")
+    assert set(bench.MODES.values()) <= {"flows", "modify", "read"}
+
+
+class _Work:
+    def __init__(self, log, k):
+        self.log, self.k = log, k
+
+    def wait(self):
+        self.log.append(("wait", self.k))
+
+
+class _Stream:
+    cuda_stream = 0
+
+    def wait_event(self, ev):
+        pass
+
+
+class _FakeTorch:
+    """Just enough of torch for FlowRunner/_timed without a GPU."""
+
+    class cuda:  # noqa: N801
+        class Event:
+            def __init__(self, enable_timing=False):
+                pass
+
+            def record(self, s=None):
+                pass
+
+            def elapsed_time(self, other):
+                return 1.0
+
+        @staticmethod
+        def synchronize():
+            pass
+
+        class stream:  # noqa: N801
+            def __init__(self, s):
+                pass
+
+            def __enter__(self):
+                return self
+
+            def __exit__(self, *a):
+                return False
+
+    uint8 = "u8"
+
+    @staticmethod
+    def empty(n, dtype=None, device=None):
+        class _T:
+            def data_ptr(self):
+                return 0
+        return _T()
+
+
+class _Hist:
+    def __init__(self, log, i):
+        self.log, self.i = log, i
+
+    def zero_(self):
+        self.log.append(("zero", self.i))
+
+    def numel(self):
+        return 16
+
+    def data_ptr(self):
+        return 0
+
+    device = "cpu"
+
+
+class _Lib:
+    def __init__(self, log):
+        self.log = log
+
+    def ingot_gpu_flow_hist_workspace_size(self, n, bins):
+        return 0
+
+    def ingot_gpu_flow_hist_ws(self, h, arena, *a):
+        self.log.append(("kernel", arena))
+        return 0
+
+
+class _Ctx:
+    _h = None
+
+
+def test_flow_runner_overlaps_reduce_and_waits_before_reuse():
+    log = []
+    reps = 4
+
+    class _Buf:
+        def __init__(self, i):
+            self.i = i
+
+        def data_ptr(self):
+            return self.i
+
+    arenas = [_Buf(i) for i in range(reps)]
+    hists = [_Hist(log, i) for i in range(reps)]
+    issued = []
+
+    def reduce_fn(h):
+        k = len(issued)
+        issued.append(h.i)
+        log.append(("reduce", k))
+        return _Work(log, k)
+
+    r = bench.FlowRunner(_FakeTorch, _Lib(log), _Ctx(), Chain.VlanUlp, 8, arenas, _Buf(0),
+                         _Buf(0), hists, [_Buf(0)] * reps, _Stream(), reduce_fn)
+    r.run(7)
+    waits = [k for op, k in log if op == "wait"]
+    assert sorted(waits) == list(range(7))  # every reduce waited inside run()
+    # step k's reduce is waited before the histogram of step k + reps - 2 is
+    # zeroed (at most two reduces in flight)
+    for k in range(7):
+        z = [i for i, e in enumerate(log) if e == ("zero", (k + 2) % reps)]
+        w = log.index(("wait", k))
+        later = [i for i in z if i > log.index(("reduce", k))]
+        if later:
+            assert w < later[0]
+    # reduces overlap the next step: reduce k is issued before wait k
+    assert log.index(("reduce", 1)) < log.index(("wait", 0))
