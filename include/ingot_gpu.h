@@ -587,6 +587,56 @@ int ingot_gpu_flow_hist_ws(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
                            size_t work_bytes, void* stream);
 size_t ingot_gpu_flow_hist_workspace_size(uint64_t n, uint32_t bins);
 
+/* ---------------------------------------------------------------------------
+ * Single-header parse, batched: `HeaderParse::parse(slice)` of one header kind
+ * at the start of every slice (ingot-types/src/lib.rs:137-147; the generated
+ * bodies, packet/mod.rs:1831-2005) — ValidEthernet::parse, ValidIpv4::parse
+ * ... as the reference's `ingot/benches/modify.rs:79-104` parse benches — or
+ * a choice's `parse_choice(slice, hint)` (ingot-macros/src/choice.rs:231-246:
+ * no hint -> NeedsHint, a hint no variant takes -> Unwanted), as
+ * `ValidL3::parse_choice` in `ingot-examples/benches/choice.rs`.
+ *
+ * Per slice one 8-B ingot_hdr: status (0 Ok, else 1 + ParseError), the header
+ * parsed (for a choice: the variant taken), `used` = its HeaderLen (the
+ * remainder starts there) and `hint` = its NextLayer hint (ethertype /
+ * IpProtocol; INGOT_HINT_NONE = None: TCP, UDP, ICMP, Geneve).  Choices take
+ * d_hint[i] when d_hint is non-NULL, else `hint` for every slice
+ * (INGOT_HINT_NONE = None).  Slices: (d_off[i], d_len[i]) or fixed slots of
+ * `stride` bytes (d_off NULL; d_len optional).
+ * ------------------------------------------------------------------------- */
+enum ingot_header_kind {
+    INGOT_HDR_ETHERNET = 0,  /* ethernet.rs:46-55 */
+    INGOT_HDR_VLAN = 1,      /* ethernet.rs:57-65 (VlanBody) */
+    INGOT_HDR_IPV4 = 2,      /* ip.rs:63-93 */
+    INGOT_HDR_IPV6 = 3,      /* ip.rs:159-182, with its extension-header chain */
+    INGOT_HDR_TCP = 4,       /* tcp.rs:9-30 */
+    INGOT_HDR_UDP = 5,       /* udp.rs:8-15 */
+    INGOT_HDR_ICMP = 6,      /* icmp.rs:42-50 (v4 and v6 share the layout) */
+    INGOT_HDR_REPEATED_UDP = 7, /* Repeated<Udp> over the whole slice (util.rs:189-228) */
+    INGOT_HDR_GENEVE = 8,    /* geneve.rs:16-44, options subparsed */
+    INGOT_HDR_L3 = 16,       /* choice L3 (ingot-examples/src/choices.rs:17-21) */
+    INGOT_HDR_L4 = 17,       /* choice L4 (choices.rs:25-29) */
+    INGOT_HDR_ULP = 18       /* choice Ulp (choices.rs:32-38) */
+};
+#define INGOT_HINT_NONE 0xffffffffu
+
+typedef struct ingot_hdr {
+    uint8_t status;  /* 0 = Ok, else 1 + ParseError */
+    uint8_t kind;    /* enum ingot_header_kind parsed (a choice's variant) */
+    uint16_t used;   /* HeaderLen: bytes consumed from the slice start */
+    uint32_t hint;   /* NextLayer hint, INGOT_HINT_NONE = None */
+} ingot_hdr;
+
+#ifdef __cplusplus
+static_assert(sizeof(ingot_hdr) == 8, "ingot_hdr is 8 bytes");
+#endif
+
+int ingot_gpu_parse_header(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
+                           const uint64_t* d_off, const uint16_t* d_len,
+                           uint32_t stride, uint64_t n, int kind,
+                           const uint32_t* d_hint, uint32_t hint,
+                           ingot_hdr* d_out, void* stream);
+
 /* Error strings. */
 const char* ingot_gpu_strerror(int api_code);
 /* ParseError name as ingot prints it (error.rs:49-60): "Unwanted", ... ;

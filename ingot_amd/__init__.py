@@ -35,8 +35,11 @@ from .abi import (  # noqa: F401  (re-exports)
     REC_BYTES,
     REC_DTYPE,
     STATUS_OK,
+    HDR_DTYPE,
+    HINT_NONE,
     Chain,
     GenProfile,
+    HeaderKind,
     IngotFields,
     IngotRec,
     IngotRec8,
@@ -119,6 +122,25 @@ class Context:
 
     def get_tuning(self, key: int) -> int:
         return int(self._lib.ingot_gpu_ctx_get_tuning(self._h, int(key)))
+
+    def parse_header(self, arena, off, lens, kind, hint=None, hints=None, stride: int = 0,
+                     n: Optional[int] = None, out=None, stream=None):
+        """ingot_gpu_parse_header: `ValidX::parse(slice)` of header `kind`
+        (HeaderKind) at every slice start, or a choice's `parse_choice(slice,
+        hint)` (HeaderKind.L3 / L4 / Ulp; `hints` per slice or one `hint`,
+        None = no hint).  Returns an (n, 8) uint8 tensor of ingot_hdr."""
+        torch = _torch()
+        if n is None:
+            n = off.numel()
+        if out is None:
+            out = torch.empty((n, HDR_DTYPE.itemsize), dtype=torch.uint8, device=arena.device)
+        self._check_dev(arena, off, lens, hints, out)
+        h = HINT_NONE if hint is None else int(hint)
+        _lib.check(self._lib.ingot_gpu_parse_header(self._h, _ptr(arena), _ptr(off), _ptr(lens),
+                                                    int(stride), n, int(kind), _ptr(hints), h,
+                                                    _ptr(out), _stream(stream)),
+                   "ingot_gpu_parse_header")
+        return out
 
     def host_map(self, host) -> int:
         """ingot_gpu_host_map: the device address of host memory (a pinned

@@ -21,6 +21,11 @@ SIGNATURES = {
     "ingot_gpu_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "ingot_gpu_ctx_destroy": (None, [ctypes.c_void_p]),
     "ingot_gpu_ctx_device": (ctypes.c_int, [ctypes.c_void_p]),
+    "ingot_gpu_parse_header": (
+        ctypes.c_int,
+        [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, ctypes.c_uint32, c_u64, ctypes.c_int, c_u8p,
+         ctypes.c_uint32, c_u8p, ctypes.c_void_p],
+    ),
     "ingot_gpu_host_map": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                           ctypes.POINTER(ctypes.c_void_p)]),
     "ingot_gpu_host_unmap": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),

@@ -245,7 +245,33 @@ assert ctypes.sizeof(IngotGeneveOpt) == 8
 assert ctypes.sizeof(IngotTunnelFields) == 128
 assert ctypes.sizeof(IngotGeneveFields) == 384
 
+class HeaderKind(enum.IntEnum):
+    """Single-header parse kinds (include/ingot_gpu.h enum ingot_header_kind)."""
+
+    Ethernet = 0      # ethernet.rs:46-55
+    VlanBody = 1      # ethernet.rs:57-65
+    Ipv4 = 2          # ip.rs:63-93
+    Ipv6 = 3          # ip.rs:159-182 (+ extension headers)
+    Tcp = 4           # tcp.rs:9-30
+    Udp = 5           # udp.rs:8-15
+    Icmp = 6          # icmp.rs:42-50
+    RepeatedUdp = 7   # Repeated<Udp> (util.rs:189-228)
+    Geneve = 8        # geneve.rs:16-44
+    L3 = 16           # choice, ingot-examples/src/choices.rs:17-21
+    L4 = 17           # choices.rs:25-29
+    Ulp = 18          # choices.rs:32-38
+
+
+HINT_NONE = 0xFFFFFFFF
+
+
+class IngotHdr(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_uint8), ("kind", ctypes.c_uint8), ("used", ctypes.c_uint16),
+                ("hint", ctypes.c_uint32)]
+
+
 REC_DTYPE = np.dtype(IngotRec)
+HDR_DTYPE = np.dtype(IngotHdr)
 FIELDS_DTYPE = np.dtype(IngotFields)
 REC8_DTYPE = np.dtype(IngotRec8)
 GENEVE_FIELDS_DTYPE = np.dtype(IngotGeneveFields)

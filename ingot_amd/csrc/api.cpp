@@ -169,6 +169,26 @@ void ingot_gpu_ctx_destroy(ingot_gpu_ctx* ctx) { delete ctx; }
 
 int ingot_gpu_ctx_device(const ingot_gpu_ctx* ctx) { return ctx ? ctx->device : -1; }
 
+int ingot_gpu_parse_header(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
+                           const uint16_t* d_len, uint32_t stride, uint64_t n, int kind,
+                           const uint32_t* d_hint, uint32_t hint, ingot_hdr* d_out,
+                           void* stream) {
+    const bool kind_ok = (kind >= INGOT_HDR_ETHERNET && kind <= INGOT_HDR_GENEVE) ||
+                         (kind >= INGOT_HDR_L3 && kind <= INGOT_HDR_ULP);
+    if (!ctx || !kind_ok) return INGOT_GPU_EINVAL;
+    if (n == 0) return INGOT_GPU_SUCCESS;
+    if (!d_arena || !d_out) return INGOT_GPU_EINVAL;
+    if (d_off) {
+        if (!d_len) return INGOT_GPU_EINVAL;
+        stride = 0;
+    } else if (stride == 0 || stride > 65535u) {
+        return INGOT_GPU_ERANGE;
+    }
+    if (int e = enter(ctx)) return e;
+    ingot_gpu::HeaderArgs a{d_arena, d_off, d_len, stride, n, kind, d_hint, hint, d_out};
+    return from_hip(ingot_gpu::launch_header(a, (hipStream_t)stream));
+}
+
 int ingot_gpu_host_map(ingot_gpu_ctx* ctx, void* host, size_t bytes, void** d_ptr) {
     if (!ctx || !host || !d_ptr || bytes == 0) return INGOT_GPU_EINVAL;
     *d_ptr = nullptr;

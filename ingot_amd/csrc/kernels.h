@@ -61,6 +61,20 @@ hipError_t launch_flow_hist(const uint32_t* flow, uint64_t n, uint32_t* hist, ui
                             void* work, size_t work_bytes, hipStream_t s);
 size_t flow_hist_workspace(uint64_t n, uint32_t bins);
 
+// Single-header parse (ingot_gpu_parse_header, header.hip).
+struct HeaderArgs {
+    const uint8_t* arena;
+    const uint64_t* off;  // NULL: slots of `stride`
+    const uint16_t* len;
+    uint32_t stride;
+    uint64_t n;
+    int kind;              // enum ingot_header_kind
+    const uint32_t* hints;  // per-slice choice hints, or NULL: `hint`
+    uint32_t hint;
+    ingot_hdr* out;
+};
+hipError_t launch_header(const HeaderArgs& a, hipStream_t s);
+
 // Per-context tuning (0 = measured default); see INGOT_TUNE_* in ingot_gpu.h.
 struct Tuning {
     int window_indexed = 0;

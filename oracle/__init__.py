@@ -285,3 +285,29 @@ def parse_header(kind: str, data: bytes):
                                  ctypes.byref(hint))
     h = None if hint.value == 0xFFFFFFFF else hint.value
     return st, used.value, h
+
+
+def parse_header_batch(arena, off, lens, kind: int, hint=None, hints=None, stride: int = 0,
+                       n: int | None = None) -> np.ndarray:
+    """ingot_gpu_parse_header semantics: one ingot_hdr (8 B, as raw bytes
+    per row) per slice."""
+    lib = load()
+    lib.oracle_parse_header_batch.argtypes = [ctypes.c_void_p] * 3 + [
+        ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32,
+        ctypes.c_void_p]
+    lib.oracle_parse_header_batch.restype = ctypes.c_int
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    if off is not None:
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        n = len(off) if n is None else n
+    if lens is not None:
+        lens = np.ascontiguousarray(lens, dtype=np.uint16)
+    if hints is not None:
+        hints = np.ascontiguousarray(hints, dtype=np.uint32)
+    out = np.zeros((n, 8), dtype=np.uint8)
+    h = 0xFFFFFFFF if hint is None else int(hint)
+    rc = lib.oracle_parse_header_batch(_p(arena), _p(off), _p(lens), stride, n, int(kind),
+                                       _p(hints), h, _p(out))
+    if rc != 0:
+        raise ValueError("oracle_parse_header_batch: bad arguments")
+    return out

@@ -1052,6 +1052,53 @@ int oracle_parse_header(int kind, const uint8_t* s, uint32_t n, uint32_t* used,
     return e;
 }
 
+/* Choices (ingot-macros/src/choice.rs:231-246): `hint None -> NeedsHint`;
+ * variants tried in declaration order (choice.rs:104-112); no match ->
+ * Unwanted.  L3 (choices.rs:17-21): IPV4 -> Ipv4, IPV6 -> Ipv6.  L4
+ * (choices.rs:25-29): TCP -> Tcp, UDP -> Udp.  Ulp (choices.rs:32-38): + ICMP
+ * and ICMPv6 (one 8-B layout, icmp.rs:42-50). */
+int oracle_parse_choice(int kind, uint32_t hint, const uint8_t* s, uint32_t n, uint32_t* used,
+                        uint32_t* hint_out, uint32_t* variant) {
+    *variant = (uint32_t)kind;
+    if (hint == 0xffffffffu) return PE_NEEDS_HINT;
+    int v = -1;
+    if (kind == 16) {
+        if (hint == 0x0800) v = 2;
+        else if (hint == 0x86dd) v = 3;
+    } else if (kind == 17 || kind == 18) {
+        if (hint == 6) v = 4;
+        else if (hint == 17) v = 5;
+        else if (kind == 18 && (hint == 1 || hint == 58)) v = 6;
+    } else {
+        return PE_UNWANTED;
+    }
+    if (v < 0) return PE_UNWANTED;
+    *variant = (uint32_t)v;
+    return oracle_parse_header(v, s, n, used, hint_out);
+}
+
+int oracle_parse_header_batch(const uint8_t* arena, const uint64_t* off, const uint16_t* len,
+                              uint32_t stride, uint64_t n, int kind, const uint32_t* hints,
+                              uint32_t hint, ingot_hdr* out) {
+    if (!off && !stride) return -1;
+    for (uint64_t i = 0; i < n; ++i) {
+        uint64_t o = off ? off[i] : i * (uint64_t)stride;
+        uint32_t l = len ? len[i] : stride;
+        if (!off && l > stride) l = stride;
+        uint32_t used = 0, h = 0xffffffffu, variant = (uint32_t)kind;
+        int st;
+        if (kind >= 16) st = oracle_parse_choice(kind, hints ? hints[i] : hint, arena + o, l,
+                                                 &used, &h, &variant);
+        else st = oracle_parse_header(kind, arena + o, l, &used, &h);
+        ingot_hdr* r = &out[i];
+        r->status = (uint8_t)st;
+        r->kind = (uint8_t)variant;
+        r->used = st ? 0 : (uint16_t)used;
+        r->hint = st ? 0xffffffffu : h;
+    }
+    return 0;
+}
+
 /* ------------------------------------------------------------------------
  * Flow classification (build-defined; ingot has no flow hash): Toeplitz over
  * src | dst (| sport | dport for TCP/UDP) of frames that parse Ok with an L3.

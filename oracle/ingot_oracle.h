@@ -76,6 +76,16 @@ int oracle_v6eh_class(uint8_t proto);
 /* Header-level parse (ValidX::parse); see ingot_oracle.c. */
 int oracle_parse_header(int kind, const uint8_t* s, uint32_t n, uint32_t* used,
                         uint32_t* hint_out);
+/* A choice's parse_choice(slice, hint) (choice.rs:231-246): kind 16 = L3,
+ * 17 = L4, 18 = Ulp (choices.rs:17-38); hint 0xffffffff = None.  *variant =
+ * the header kind taken (0-8 numbering of oracle_parse_header). */
+int oracle_parse_choice(int kind, uint32_t hint, const uint8_t* s, uint32_t n, uint32_t* used,
+                        uint32_t* hint_out, uint32_t* variant);
+/* ingot_gpu_parse_header semantics over a batch of slices ((off, len) or
+ * slots of `stride`), one ingot_hdr each. */
+int oracle_parse_header_batch(const uint8_t* arena, const uint64_t* off, const uint16_t* len,
+                              uint32_t stride, uint64_t n, int kind, const uint32_t* hints,
+                              uint32_t hint, ingot_hdr* out);
 
 /* Toeplitz (RSS) hash of `n` input bytes with a key of >= n+4 bytes. */
 uint32_t oracle_toeplitz(const uint8_t* key, uint32_t key_len,

@@ -570,6 +570,40 @@ def header_kats():
     ]
 
 
+def choice_kats():
+    """Choice-level vectors: `parse_choice(slice, hint)` of L3 / L4 / Ulp.
+    The first two are the reference's choice bench (ingot-examples/benches/
+    choice.rs:12-44: ValidL3 over pkt_body_v4[14..] with IPV4 = success, LLDP
+    = fail); the rest are derived from the choice semantics
+    (ingot-macros/src/choice.rs:231-246: None -> NeedsHint, no variant ->
+    Unwanted) and the choice declarations (choices.rs:17-38)."""
+    l3 = PKT_BODY_V4[14:]
+    udp = PKT_BODY_V4[34:]
+    v6 = PKT_BODY_V6[14:]
+    return [
+        dict(name="choice_l3_success", source="ingot-examples/benches/choice.rs:32-39",
+             choice="L3", hint=0x0800, bytes=hexs(l3),
+             expect=dict(ok=True, variant="ipv4", used=20, hint=17)),
+        dict(name="choice_l3_fail", source="ingot-examples/benches/choice.rs:40-46",
+             choice="L3", hint=0x88CC, bytes=hexs(l3), expect=dict(ok=False, error="Unwanted")),
+        dict(name="choice_l3_needs_hint", source="ingot-macros/src/choice.rs:231-246",
+             choice="L3", hint=None, bytes=hexs(l3), expect=dict(ok=False, error="NeedsHint")),
+        dict(name="choice_l3_v6", source="ingot-examples/src/choices.rs:17-21", choice="L3",
+             hint=0x86DD, bytes=hexs(v6), expect=dict(ok=True, variant="ipv6", used=40, hint=17)),
+        dict(name="choice_l3_v4_truncated", source="ingot-examples/src/choices.rs:17-21",
+             choice="L3", hint=0x0800, bytes=hexs(l3[:19]),
+             expect=dict(ok=False, error="TooSmall")),
+        dict(name="choice_l4_udp", source="ingot-examples/src/choices.rs:25-29", choice="L4",
+             hint=17, bytes=hexs(udp), expect=dict(ok=True, variant="udp", used=8)),
+        dict(name="choice_l4_icmp_unwanted", source="ingot-examples/src/choices.rs:25-29",
+             choice="L4", hint=1, bytes=hexs(udp), expect=dict(ok=False, error="Unwanted")),
+        dict(name="choice_ulp_icmp", source="ingot-examples/src/choices.rs:32-38", choice="Ulp",
+             hint=1, bytes=hexs(udp), expect=dict(ok=True, variant="icmp", used=8)),
+        dict(name="choice_ulp_icmpv6", source="ingot-examples/src/choices.rs:32-38",
+             choice="Ulp", hint=58, bytes=hexs(udp), expect=dict(ok=True, variant="icmp", used=8)),
+    ]
+
+
 def bitfield_kats():
     # ingot/src/tests.rs:27-55 layout of TestFunFields (BE members only; the LE
     # forms are out of scope: LE bitfields are unsupported, ingot/README.md:23).
@@ -619,6 +653,7 @@ def main() -> None:
         generator="tests/golden/make_golden.py",
         chain_kats=chain_frames() + geneve_frames(),
         header_kats=header_kats(),
+        choice_kats=choice_kats(),
         read_kats=read_kats(),
         modify_kats=modify_kats(),
         setter_kats=setter_kats(),

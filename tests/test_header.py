@@ -1,0 +1,107 @@
+"""Single-header parse on the device (ingot_gpu_parse_header): `ValidX::parse`
+per header kind and `parse_choice` of the L3 / L4 / Ulp choices, batched.
+Bit-exact against the oracle (tests/test_oracle_golden.py pins the oracle to
+the reference's header-level vectors and the choice bench).  Needs an MI355X:
+`pytest -m gpu`."""
+import numpy as np
+import pytest
+
+import ingot_amd
+import oracle
+from ingot_amd import GenProfile, HeaderKind
+
+pytestmark = pytest.mark.gpu
+
+KINDS = list(HeaderKind)
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.fixture(scope="module")
+def ctx(torch):
+    return ingot_amd.Context(0)
+
+
+def _dev(torch, a):
+    return None if a is None else torch.from_numpy(np.array(a)).cuda()
+
+
+def test_header_and_choice_kats_on_device(torch, ctx, kats):
+    choice = {"L3": HeaderKind.L3, "L4": HeaderKind.L4, "Ulp": HeaderKind.Ulp}
+    cases = [(oracle.HEADER_KINDS[k["header"]], None, k["bytes"]) for k in kats["header_kats"]]
+    cases += [(int(choice[k["choice"]]), k["hint"], k["bytes"]) for k in kats["choice_kats"]]
+    for kind, hint, hx in cases:
+        b = bytes.fromhex(hx)
+        arena = np.frombuffer(b + bytes(16), np.uint8)
+        off, lens = np.array([0], np.int64), np.array([len(b)], np.uint16)
+        got = ctx.parse_header(_dev(torch, arena), _dev(torch, off), _dev(torch, lens), kind,
+                               hint=hint)
+        torch.cuda.synchronize()
+        want = oracle.parse_header_batch(arena, off, lens, kind, hint=hint)
+        assert got.cpu().numpy().tobytes() == want.tobytes(), (kind, hint, hx)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_header_fuzz_bit_exact(torch, ctx, kind):
+    """Slices starting at every layer boundary and at random offsets of
+    adversarial frames (truncations, ihl / data_offset 0-15, EH chains, Geneve
+    options), with per-slice hints for the choices drawn from the values
+    every variant takes, values none takes, and None."""
+    n = 60_000
+    arena, off, lens = ingot_amd.gen_frames(GenProfile.ADVERSARIAL, n, seed=31)
+    a_np, o_np, l_np = arena.cpu().numpy(), off.cpu().numpy(), lens.cpu().numpy()
+    rng = np.random.default_rng(int(kind))
+    skip = rng.choice([0, 12, 14, 18, 22, 34, 54], n) + rng.integers(0, 3, n) * (
+        rng.random(n) < 0.2)
+    skip = np.minimum(skip, l_np).astype(np.int64)
+    s_off = o_np.astype(np.int64) + skip
+    s_len = (l_np - skip).astype(np.uint16)
+    pool = np.array([0x0800, 0x86DD, 0x88CC, 0x8100, 6, 17, 1, 58, 0, 44, 0xFFFFFFFF],
+                    dtype=np.uint32)
+    hints = pool[rng.integers(0, len(pool), n)]
+    got = ctx.parse_header(arena, _dev(torch, s_off), _dev(torch, s_len), int(kind),
+                           hints=_dev(torch, hints.view(np.int32)))
+    torch.cuda.synchronize()
+    want = oracle.parse_header_batch(a_np, s_off.view(np.uint64), s_len, int(kind), hints=hints)
+    g = got.cpu().numpy()
+    bad = np.nonzero((g != want).any(axis=1))[0]
+    assert bad.size == 0, (bad[:5], g[bad[:3]], want[bad[:3]])
+    st = want[:, 0]
+    assert (st == 0).any()  # both outcomes occur
+    if kind not in (HeaderKind.Udp, HeaderKind.Icmp):
+        assert (st != 0).any()
+
+
+def test_header_strided_and_scalar_hint(torch, ctx):
+    """Fixed slots (no offsets), with and without a length table; one hint
+    for every slice; an empty batch; bad kinds are API errors."""
+    n = 10_001
+    arena, _, lens = ingot_amd.gen_frames(GenProfile.MIXED, n, stride=256, seed=5)
+    a_np, l_np = arena.cpu().numpy(), lens.cpu().numpy()
+    for kind, hint in ((HeaderKind.Ethernet, None), (HeaderKind.L3, 0x0800),
+                       (HeaderKind.L3, 0x86DD), (HeaderKind.Ulp, 17)):
+        for ln in (lens, None):
+            # the choices parse whatever starts each slot (Ethernet bytes
+            # here): a parity check of the layout, not a meaningful parse
+            got = ctx.parse_header(arena, None, ln, int(kind), hint=hint, stride=256, n=n)
+            torch.cuda.synchronize()
+            want = oracle.parse_header_batch(a_np, None, None if ln is None else l_np,
+                                             int(kind), hint=hint, stride=256, n=n)
+            assert got.cpu().numpy().tobytes() == want.tobytes(), (kind, hint, ln is None)
+    out = torch.empty((0, 8), dtype=torch.uint8, device="cuda")
+    ctx.parse_header(arena, None, None, int(HeaderKind.Udp), stride=256, n=0, out=out)
+    from ingot_amd import _lib
+
+    lib = _lib.load()
+    out = torch.empty((4, 8), dtype=torch.uint8, device="cuda")
+    assert lib.ingot_gpu_parse_header(ctx._h, arena.data_ptr(), None, None, 256, 4, 9, None,
+                                      0, out.data_ptr(), None) == -1  # no such kind
+    assert lib.ingot_gpu_parse_header(ctx._h, arena.data_ptr(), None, None, 0, 4, 0, None,
+                                      0, out.data_ptr(), None) == -5  # no offsets, no stride

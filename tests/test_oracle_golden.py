@@ -210,3 +210,44 @@ def test_batch_matches_single_and_threads():
             rr, ff = oracle.parse_one(fr, chain)
             assert rr.tobytes() == r1[i].tobytes()
             assert ff.tobytes() == f1[i].tobytes()
+
+
+CHOICE_KINDS = {"L3": 16, "L4": 17, "Ulp": 18}
+VARIANTS = {"ethernet": 0, "vlan": 1, "ipv4": 2, "ipv6": 3, "tcp": 4, "udp": 5, "icmp": 6}
+
+
+def test_choice_kats(kats):
+    """parse_choice of the L3 / L4 / Ulp choices (ingot-examples/benches/
+    choice.rs and the choice semantics), through the batched header oracle."""
+    assert len(kats["choice_kats"]) >= 6
+    for kat in kats["choice_kats"]:
+        data = np.frombuffer(bytes.fromhex(kat["bytes"]) + bytes(8), np.uint8)
+        n = len(bytes.fromhex(kat["bytes"]))
+        out = oracle.parse_header_batch(data, np.array([0]), np.array([n]),
+                                        CHOICE_KINDS[kat["choice"]], hint=kat["hint"])
+        st, kind = int(out[0, 0]), int(out[0, 1])
+        used = int(out[0, 2]) | int(out[0, 3]) << 8
+        hint = int(out[0, 4:8].view(np.uint32)[0])
+        e = kat["expect"]
+        if e["ok"]:
+            assert st == 0, kat["name"]
+            assert kind == VARIANTS[e["variant"]], kat["name"]
+            assert used == e["used"], kat["name"]
+            assert hint == e.get("hint", 0xFFFFFFFF), kat["name"]
+        else:
+            assert ParseError(st).name == e["error"], kat["name"]
+            assert used == 0 and hint == 0xFFFFFFFF, kat["name"]
+
+
+def test_header_batch_agrees_with_header_kats(kats):
+    """The batched header oracle (ingot_gpu_parse_header's checker) returns
+    what the per-header oracle pinned by the reference's vectors returns."""
+    for kat in kats["header_kats"]:
+        b = bytes.fromhex(kat["bytes"])
+        out = oracle.parse_header_batch(np.frombuffer(b + bytes(8), np.uint8), np.array([0]),
+                                        np.array([len(b)]), oracle.HEADER_KINDS[kat["header"]])
+        st, used, hint = oracle.parse_header(kat["header"], b)
+        assert int(out[0, 0]) == st, kat["name"]
+        if st == 0:
+            assert int(out[0, 2]) | int(out[0, 3]) << 8 == used
+            assert int(out[0, 4:8].view(np.uint32)[0]) == (0xFFFFFFFF if hint is None else hint)
