@@ -51,7 +51,7 @@ def test_layouts_match_c(tmp_path):
     structs = {"ingot_rec": IngotRec, "ingot_rec8": IngotRec8, "ingot_v6eh": abi.IngotV6Eh,
                "ingot_fields": IngotFields, "ingot_geneve_opt": abi.IngotGeneveOpt,
                "ingot_tunnel_fields": abi.IngotTunnelFields,
-               "ingot_geneve_fields": abi.IngotGeneveFields}
+               "ingot_geneve_fields": abi.IngotGeneveFields, "ingot_hdr": abi.IngotHdr}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "ingot_gpu.h"',
              "int main(void){"]
     for c, py in structs.items():
@@ -67,7 +67,8 @@ def test_layouts_match_c(tmp_path):
     got = dict(line.split() for line in subprocess.run([str(exe)], capture_output=True,
                                                        text=True).stdout.splitlines())
     sizes = {"ingot_rec": 16, "ingot_rec8": 8, "ingot_v6eh": 12, "ingot_fields": 256,
-             "ingot_geneve_opt": 8, "ingot_tunnel_fields": 128, "ingot_geneve_fields": 384}
+             "ingot_geneve_opt": 8, "ingot_tunnel_fields": 128, "ingot_geneve_fields": 384,
+             "ingot_hdr": 8}
     for c, py in structs.items():
         assert int(got[c]) == ctypes.sizeof(py) == sizes[c], c
         for f in (f[0] for f in py._fields_):
@@ -102,6 +103,9 @@ def test_argument_validation_without_gpu(lib):
     assert lib.ingot_gpu_parse_compact(null, None, None, None, 10, 0, None, None) == -1
     assert lib.ingot_gpu_parse_strided_compact(null, None, 64, None, 10, 0, None, None) == -1
     assert lib.ingot_pktgen_fill(0, 1, 0, 1, None, 0, None, None, 0, None) == -1
+    assert lib.ingot_gpu_parse_header(null, None, None, None, 64, 10, 0, None, 0, None,
+                                      None) == -1
+    assert lib.ingot_gpu_host_map(null, None, 64, ctypes.byref(ctypes.c_void_p())) == -1
     assert lib.ingot_gpu_strerror(-1) == b"invalid argument"
 
 
