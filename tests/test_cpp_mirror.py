@@ -31,3 +31,22 @@ def test_cpp_reference_kats_on_device():
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert " 0 failed" in r.stdout
+
+
+@pytest.mark.gpu
+def test_cpp_host_ring_example_on_device():
+    """tests/cpp/example_host_ring.cpp: a C++ consumer of the ABI parsing
+    frames in pageable host memory, zero-copy."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    exe = ROOT / "tests" / "cpp" / "build" / "example_host_ring"
+    if not exe.exists():
+        from ingot_amd.build import build_cpp_tests
+
+        build_cpp_tests()
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 mismatches" in r.stdout
