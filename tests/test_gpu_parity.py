@@ -403,3 +403,69 @@ def test_config5_full_size_flow_histogram(ctx, torch):
         assert g_hash[k] == w[0], idx[k]
     del arena, off, lens, recs, flow, hashes
     torch.cuda.empty_cache()
+
+
+# ---------------------------------------------------------------------------
+# maximum sizes: 65,535-byte frames, offsets near the u16 limit
+# ---------------------------------------------------------------------------
+def _max_frames():
+    """Frames at the ABI's size limits, built field by field: an IPv6 frame
+    whose extension-header chain (31 x 2,048-B RFC 6564 headers) puts the UDP
+    header ~63.5 KB in; a 65,535-byte IPv4 frame with ihl 15 and TCP
+    data_offset 15; the same two cut inside the last header; and a frame that
+    ends exactly at its last header."""
+    eth6 = bytes(12) + b"\x86\xdd"
+    eh = []
+    for k in range(31):
+        nh = 60 if k < 30 else 17  # Destination Options ... -> UDP
+        eh.append(bytes([nh, 255]) + bytes(6 + 8 * 255))
+    v6 = bytes([0x60, 0, 0, 0, 0, 0, 60, 64]) + bytes(32)
+    udp = b"\x12\x34\x56\x78\x00\x08\x00\x00"
+    f1 = eth6 + v6 + b"".join(eh) + udp
+    f1 = f1 + bytes(65535 - len(f1))
+    v4 = bytes([0x4F, 0, 0, 0, 0, 0, 0, 0, 64, 6, 0, 0]) + bytes(8) + bytes(40)
+    tcp = b"\x00\x50\x01\xbb" + bytes(8) + bytes([0xF0, 0x18]) + bytes(6) + bytes(40)
+    f2 = bytes(12) + b"\x08\x00" + v4 + tcp
+    f2 = f2 + bytes(65535 - len(f2))
+    hdr1 = 14 + 40 + 31 * 2048 + 8
+    return [f1, f2, f1[:hdr1 - 3], f1[:14 + 40 + 30 * 2048 + 100], f2[:14 + 60 + 59],
+            f1[:hdr1], f2[:14 + 60 + 60]]
+
+
+@pytest.mark.parametrize("chain", BASE_CHAINS)
+def test_maximum_size_frames(ctx, torch, chain):
+    """Records and every getter of 65,535-byte frames (offsets near the u16
+    limit, headers ~63 KB past the staged window) equal the oracle's, in the
+    packed layout and in 65,520-byte slots."""
+    from tests.frames import pack
+
+    frames = _max_frames() * 70  # > one 64-packet tile
+    a_np, o_np, l_np = pack(frames)
+    arena = torch.from_numpy(a_np).cuda()
+    off = torch.from_numpy(o_np.astype(np.int64)).cuda()
+    lens = torch.from_numpy(l_np.astype(np.uint16)).cuda()
+    r = ctx.parse(arena, off, lens, chain)
+    f = dev_fields(ctx, arena, off, lens, chain)
+    torch.cuda.synchronize()
+    w_rec, w_fld = oracle_all(arena, off, lens, chain)
+    assert r.cpu().numpy().tobytes() == w_rec.tobytes()
+    assert f.cpu().numpy().tobytes() == w_fld.tobytes()
+    if chain == Chain.GenericUlp:
+        rr = ingot_amd.records_to_numpy(r)
+        assert int(rr["payload_off"][0]) == 14 + 40 + 31 * 2048 + 8  # 63,558
+        assert int(rr["status"][0]) == 0 and int(rr["n_v6ext"][0]) == 31
+    # fixed slots of the largest stride the ABI takes (65,520 B)
+    stride = 65520
+    n = 14
+    slots = np.zeros(stride * n + 256, np.uint8)
+    sl = np.zeros(n, np.uint16)
+    for i, fr in enumerate(frames[:n]):
+        b = fr[:stride]
+        slots[i * stride:i * stride + len(b)] = np.frombuffer(b, np.uint8)
+        sl[i] = len(b)
+    sarena = torch.from_numpy(slots).cuda()
+    slens = torch.from_numpy(sl).cuda()
+    rs = ctx.parse_strided(sarena, stride, n, chain, lens=slens)
+    torch.cuda.synchronize()
+    ws = oracle.parse_batch(slots, None, sl, chain, stride=stride, n=n)
+    assert rs.cpu().numpy().tobytes() == ws.tobytes()
