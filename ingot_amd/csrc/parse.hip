@@ -147,6 +147,45 @@ struct Frame {
         for (uint32_t k = 0; k < NW; ++k) out[k] = __builtin_amdgcn_perm(d[k + 1], d[k], sel);
     }
 
+    // As be_words, for a block NOT in the window: the 16-B-aligned chunks
+    // holding block bytes (at most 3, from L2 — the staging just fetched
+    // their 128-B lines) instead of 4 byte loads per word; then a dword
+    // select + one v_perm per word.  Only chunks holding block bytes are
+    // read, so nothing past the frame's last 16-B chunk is touched.
+    __device__ __forceinline__ void be_words_global8(uint32_t i, uint32_t nw,
+                                                     uint32_t* out) const {
+        const uintptr_t at = (uintptr_t)(g + i);
+        const uint4* q = reinterpret_cast<const uint4*>(at & ~(uintptr_t)15);
+        const uint32_t r = (uint32_t)(at & 15u);
+        const uint32_t end = r + 4u * nw;
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        const uint4 c0 = q[0];
+        const uint4 c1 = end > 16u ? q[1] : z;
+        const uint4 c2 = end > 32u ? q[2] : z;
+        const uint32_t d[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y,
+                                c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
+        const uint32_t s = r >> 2;
+        uint32_t e[9];
+#pragma unroll
+        for (uint32_t j = 0; j < 9; ++j)
+            e[j] = s == 0u ? d[j] : s == 1u ? d[j + 1] : s == 2u ? d[j + 2] : d[j + 3];
+        const uint32_t sel = (r & 3u) * 0x01010101u + 0x00010203u;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) out[k] = __builtin_amdgcn_perm(e[k + 1], e[k], sel);
+    }
+
+    // A big-endian word at frame offset i (i + 4 <= len): LDS when staged,
+    // else one or two aligned dword loads (never past the word's own dwords).
+    __device__ __forceinline__ uint32_t be32(uint32_t i) const {
+        if (i + 4u <= avail) return be(i, 4);
+        const uintptr_t at = (uintptr_t)(g + i);
+        const uint32_t* d = reinterpret_cast<const uint32_t*>(at & ~(uintptr_t)3);
+        const uint32_t r = (uint32_t)(at & 3u);
+        const uint32_t d0 = d[0];
+        const uint32_t d1 = r ? d[1] : 0u;
+        return __builtin_amdgcn_perm(d1, d0, r * 0x01010101u + 0x00010203u);
+    }
+
     // Bytes past the staged window (long option / EH chains), read straight
     // from HBM by the lanes that need them.  Byte loads: measured faster on
     // config 3 than aligned 16-B loads + lane selects (566 vs 659 us/step),
@@ -828,28 +867,25 @@ struct FlowWords {
 
 // The hash input words of a parsed-Ok packet with an L3 layer (false: not
 // counted).  The address block (2 words for IPv4, 8 for IPv6, contiguous)
-// normally lies in the staged window: one burst of 9 LDS dwords and one
-// v_perm (align + byte swap) per word, instead of a bounds check, two reads
-// and a wait per word.  Otherwise (a window smaller than the L3 header, or
-// a deep VLAN stack) word by word through Frame::be, which falls back to
-// L2/HBM.  The port word may lie past the window (IPv6 EH chains).
+// is read in one burst and one v_perm (align + byte swap) per word: 9 LDS
+// dwords when the staged window holds it, else the (at most 3) 16-B chunks
+// holding it from L2 — instead of a bounds check, two reads and a wait (or 4
+// byte loads) per word.  The port word: LDS, or aligned dwords past the
+// window (IPv6 EH chains).
 template <class FR>
 __device__ __forceinline__ bool flow_words(const FR& f, const Rec& r, FlowWords& x) {
 #pragma unroll
     for (uint32_t k = 0; k < 9; ++k) x.w[k] = 0;
     if (r.status != INGOT_OK || r.l3_kind == INGOT_L3_NONE) return false;
     const bool ports = r.l4_kind == INGOT_L4_TCP || r.l4_kind == INGOT_L4_UDP;
-    const uint32_t pw = ports ? f.be(r.l4_off, 4) : 0u;
+    const uint32_t pw = ports ? f.be32(r.l4_off) : 0u;
     const bool v6 = r.l3_kind == INGOT_L3_IPV6;
     const uint32_t a = r.l3_off + (v6 ? ipv6::SOURCE_BYTE : 12u);  // source address
     const uint32_t naddr = v6 ? 8u : 2u;                            // address words
     uint32_t w[8];
-    if (a + 4u * naddr <= f.avail) {
-        f.template be_words<8>(a, w);
-    } else {
-#pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) w[k] = k < naddr ? f.be(a + 4u * k, 4) : 0u;
-    }
+    // one path per wave: a wave split between the two runs both
+    if (__all(a + 4u * naddr <= f.avail)) f.template be_words<8>(a, w);
+    else f.be_words_global8(a, naddr, w);
 #pragma unroll
     for (uint32_t k = 0; k < 9; ++k) {
         const uint32_t ak = k < 8 ? w[k] : 0u;

@@ -1,9 +1,5 @@
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-tools/gpu_step.sh 200 prof_c5a rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_c5a -o run -- python3 bench.py --config c5 --steps 50 --warmup 5 --no-cpu-baseline --no-variants --streams 1
-cp ingot_amd/lib/libingot_gpu.so /tmp/keep.so
-cp tools/alt/libingot_gpu_h256.so ingot_amd/lib/libingot_gpu.so
-tools/gpu_step.sh 200 prof_c5b rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_c5b -o run -- python3 bench.py --config c5 --steps 50 --warmup 5 --no-cpu-baseline --no-variants --streams 1
-cp /tmp/keep.so ingot_amd/lib/libingot_gpu.so
-tools/gpu_step.sh 200 prof_c5c rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_c5c -o run -- python3 bench.py --config c5 --steps 50 --warmup 5 --no-cpu-baseline --no-variants --streams 1
+tools/gpu_step.sh 300 pytest_flows python -u -m pytest tests/test_flows.py tests/test_gpu_parity.py -x -q -m gpu -k "flow or config5" --timeout 120 --timeout-method thread
+tools/gpu_step.sh 300 ab_c5 python tools/abtune.py --config c5 --rounds 3 --var mode=flows --var mode=flows,win_i=3 --var mode=flows,win_i=4 --var mode=flows,win_i=2 --var mode=flows,win_i=6 --var mode=parse --out gpurun_out/ab_c5.json
