@@ -30,6 +30,16 @@ def ctx(torch):
     return ingot_amd.Context(0)
 
 
+def _page_aligned(a):
+    """A copy of numpy array `a` in its own page-aligned, page-padded buffer
+    (pageable memory; no two arrays share a page when registered)."""
+    raw = np.zeros(a.nbytes + 2 * 4096, np.uint8)
+    start = (-raw.ctypes.data) % 4096
+    out = raw[start:start + a.nbytes].view(a.dtype).reshape(a.shape)
+    out[...] = a
+    return out
+
+
 def _pinned(torch, t):
     h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
     h.copy_(t)
@@ -99,3 +109,41 @@ def test_host_map_rejects_bad_arguments(ctx):
     assert lib.ingot_gpu_host_map(ctx._h, buf.ctypes.data, 0, ctypes.byref(d)) == -1
     assert lib.ingot_gpu_host_map(None, buf.ctypes.data, 64, ctypes.byref(d)) == -1
     assert lib.ingot_gpu_host_unmap(ctx._h, None) == -1
+
+
+def test_parse_read_over_mblk_chains_in_host_memory(torch, ctx):
+    """OPTE's real input: packets as chains of chunks (mblk_t) in host
+    memory.  The chunk pool and its tables stay in pageable host memory
+    (page-locked and mapped by ingot_gpu_host_map), parse_read runs over PCIe,
+    records and remainder-chunk indices land in mapped host memory; equal to
+    the oracle's parse_read."""
+    lib = _lib.load()
+    from tests.frames import build_frames
+
+    frames = build_frames(3000, seed=17, vlan=False)
+    rng = np.random.default_rng(3)
+    packets = []
+    for f in frames:  # 1-3 chunks, cut at random points (headers may straddle)
+        cuts = sorted(rng.integers(1, max(2, len(f)), rng.integers(0, 3)))
+        parts, prev = [], 0
+        for c in cuts:
+            if c > prev:
+                parts.append(f[prev:c])
+                prev = c
+        parts.append(f[prev:])
+        packets.append(parts)
+    arena, so, sl, ps = (_page_aligned(x) for x in ingot_amd.chunk_tables(packets))
+    n = len(packets)
+    recs = _page_aligned(np.zeros((n, 16), np.uint8))
+    chunk = _page_aligned(np.zeros(n, np.uint16))
+    d = [ctx.host_map(x) for x in (arena, so, sl, ps, recs, chunk)]
+    for chain in (Chain.GenericUlp, Chain.UdpParser):
+        recs[:] = 0xEE
+        assert lib.ingot_gpu_parse_read(ctx._h, d[0], d[1], d[2], d[3], n, int(chain), d[4],
+                                        d[5], None) == 0
+        torch.cuda.synchronize()
+        w_rec, _, w_chunk = oracle.parse_read_batch(arena, so, sl, ps, chain)
+        assert recs.tobytes() == np.asarray(w_rec).tobytes(), chain
+        assert (chunk == np.asarray(w_chunk).astype(np.uint16)).all(), chain
+    for x in (arena, so, sl, ps, recs, chunk):
+        ctx.host_unmap(x)
