@@ -147,3 +147,42 @@ def test_parse_read_over_mblk_chains_in_host_memory(torch, ctx):
         assert (chunk == np.asarray(w_chunk).astype(np.uint16)).all(), chain
     for x in (arena, so, sl, ps, recs, chunk):
         ctx.host_unmap(x)
+
+
+@pytest.mark.parametrize("stride", [None, 64, 128])
+def test_parse_modify_in_host_memory(torch, ctx, stride):
+    """ingot's setters applied in place to frames that stay in mapped host
+    memory (the reference's parse-and-decr-v4 and a multi-field edit list):
+    the host bytes afterwards equal the oracle's rewrite."""
+    from ingot_amd import EditOp, Field, edits_array
+
+    lib = _lib.load()
+    n = 20_003
+    prof = GenProfile.V4UDP64 if stride == 64 else GenProfile.MIXED
+    arena, off, lens = ingot_amd.gen_frames(prof, n, seed=8, stride=stride)
+    edits = [(2, Field.UDP_DESTINATION, EditOp.SUB, 1), (1, Field.V4_HOP_LIMIT, EditOp.SUB, 1),
+             (1, Field.V6_HOP_LIMIT, EditOp.SUB, 1)]
+    h_arena = _pinned(torch, arena)
+    want = h_arena.numpy().copy()
+    e = edits_array(edits)
+    d_arena = ctx.host_map(h_arena)
+    if stride:
+        h_lens = _pinned(torch, lens) if lens is not None else None
+        d_lens = ctx.host_map(h_lens) if h_lens is not None else None
+        rc = lib.ingot_gpu_parse_modify(ctx._h, d_arena, None, d_lens, stride, n,
+                                        int(Chain.UdpParser), e.ctypes.data, len(e), None, None)
+        l_np = None if lens is None else lens.cpu().numpy()
+        oracle.parse_modify_batch(want, None, l_np, Chain.UdpParser, edits, stride=stride, n=n)
+    else:
+        h_off, h_lens = _pinned(torch, off), _pinned(torch, lens)
+        rc = lib.ingot_gpu_parse_modify(ctx._h, d_arena, ctx.host_map(h_off),
+                                        ctx.host_map(h_lens), 0, n, int(Chain.UdpParser),
+                                        e.ctypes.data, len(e), None, None)
+        oracle.parse_modify_batch(want, off.cpu().numpy(), lens.cpu().numpy(), Chain.UdpParser,
+                                  edits)
+    assert rc == 0
+    torch.cuda.synchronize()
+    got = h_arena.numpy()
+    diff = np.nonzero(got != want)[0]
+    assert diff.size == 0, (diff[:10], got[diff[:10]], want[diff[:10]])
+    assert (got != arena.cpu().numpy()).any()  # something was rewritten
