@@ -1,4 +1,6 @@
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-tools/gpu_step.sh 300 pytest_hostmap python -u -m pytest tests/test_hostmap.py -x -q -m gpu --timeout 120 --timeout-method thread
+tools/gpu_step.sh 200 hdrsplit_128 python tools/hdrsplit.py --head 128
+tools/gpu_step.sh 200 hdrsplit_192 python tools/hdrsplit.py --head 192
+tools/gpu_step.sh 200 hdrsplit_128_s6 python tools/hdrsplit.py --head 128 --streams 6
