@@ -1,4 +1,4 @@
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-tools/gpu_step.sh 300 prof_bench_default rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_bench_default -o run -- python3 bench.py
+tools/gpu_step.sh 300 pytest_err python -u -m pytest tests/test_api_errors.py -x -q -m gpu --timeout 120 --timeout-method thread
