@@ -229,45 +229,50 @@ class ReadRunner:
 
 class FlowRunner:
     """Config 5 step: zero the histogram, parse + hash + histogram kernels,
-    then the RCCL all-reduce of that step's histogram.  The all-reduce runs on
-    RCCL's stream and overlaps the next step's kernels (histograms rotate over
-    the arena copies, so a step's buffer is reused only after its reduce has
-    been waited for, at most two steps later); the timed region ends after
+    then the RCCL all-reduce of that step's histogram.  Step k runs on stream
+    k % S with its own histogram workspace, so the next step's flow kernel
+    fills the CUs the histogram passes leave idle; the all-reduce runs on
+    RCCL's stream and overlaps later steps.  Histograms rotate over the arena
+    copies: a step's buffer is reused `reps` steps later, after its reduce has
+    been waited for on the reusing step's stream; the timed region ends after
     every reduce has completed."""
 
-    def __init__(self, torch, lib, ctx, chain, n, arenas, off, lens, hists, flows, stream,
+    def __init__(self, torch, lib, ctx, chain, n, arenas, off, lens, hists, flows, streams,
                  reduce_fn):
-        self.torch, self.streams = torch, [stream]
-        reps = len(arenas)
+        self.torch, self.streams = torch, list(streams)
+        reps, S = len(arenas), len(self.streams)
         assert reps >= 4
-        h, sp, c = ctx._h, stream.cuda_stream, int(chain)
+        h, c = ctx._h, int(chain)
         optr, lptr = off.data_ptr(), lens.data_ptr()
         aptrs = [a.data_ptr() for a in arenas]
-        pending = collections.deque()
+        works = {}
 
-        # caller-owned workspace: the atomics-free histogram pass
+        # caller-owned workspaces (one per stream): the atomics-free histogram pass
         wbytes = lib.ingot_gpu_flow_hist_workspace_size(n, hists[0].numel())
-        self.work = torch.empty(max(1, wbytes), dtype=torch.uint8, device=hists[0].device)
-        wptr = self.work.data_ptr()
+        self.work = [torch.empty(max(1, wbytes), dtype=torch.uint8, device=hists[0].device)
+                     for _ in range(S)]
 
         def launch(k):
+            st = self.streams[k % S]
             hist = hists[k % reps]
-            while len(pending) > 1:  # the reduce of step k-2 before its buffer returns
-                pending.popleft().wait()
-            hist.zero_()
-            rc = lib.ingot_gpu_flow_hist_ws(h, aptrs[k % reps], optr, lptr, 0, n, c, None,
-                                            hist.numel(), flows[k % reps].data_ptr(), None,
-                                            hist.data_ptr(), wptr, wbytes, sp)
-            with torch.cuda.stream(stream):
+            with torch.cuda.stream(st):
+                w = works.pop(k - reps, None)  # the last reduce of this buffer
+                if w is not None:
+                    w.wait()
+                hist.zero_()
+                rc = lib.ingot_gpu_flow_hist_ws(h, aptrs[k % reps], optr, lptr, 0, n, c, None,
+                                                hist.numel(), flows[k % reps].data_ptr(), None,
+                                                hist.data_ptr(), self.work[k % S].data_ptr(),
+                                                wbytes, st.cuda_stream)
                 w = reduce_fn(hist)
             if w is not None:
-                pending.append(w)
+                works[k] = w
             return rc
 
         def finish():
-            with torch.cuda.stream(stream):
-                while pending:
-                    pending.popleft().wait()
+            with torch.cuda.stream(self.streams[0]):
+                for k in sorted(works):
+                    works.pop(k).wait()
 
         self.launch, self.finish = launch, finish
 
@@ -380,7 +385,7 @@ def main():
     def runner(nstreams, record):
         if flows:
             return FlowRunner(torch, lib, ctx, chain, n, arenas, off, lens, hists, flow_ids,
-                              streams[0], idist.reduce_histogram_async)
+                              streams[:nstreams], idist.reduce_histogram_async)
         if mode == "modify":
             return ModifyRunner(torch, lib, ctx, chain, n, stride, arenas, off, lens,
                                 streams[:nstreams])
@@ -391,7 +396,7 @@ def main():
                       streams[:nstreams], record)
 
     if flows:
-        args.streams, args.no_variants = 1, True
+        args.no_variants = True
     if mode in ("modify", "read") and args.record == 8:
         ap.error("8-B records are not offered for this config")
     if chain == Chain.GeneveOverV6Tunnel and args.record == 8:

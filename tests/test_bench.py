@@ -1,7 +1,7 @@
 """bench.py's accounting, on CPU: the SURVEY §8d algorithmic bytes behind
 `roofline.achieved`, the config table, and the C5 runner's overlap of the
 per-step histogram all-reduce (every reduce waited before the timed region
-ends; a buffer reused only after its reduce)."""
+ends; a buffer reused only after its reduce) over several streams."""
 import numpy as np
 
 import bench
@@ -158,17 +158,16 @@ def test_flow_runner_overlaps_reduce_and_waits_before_reuse():
         return _Work(log, k)
 
     r = bench.FlowRunner(_FakeTorch, _Lib(log), _Ctx(), Chain.VlanUlp, 8, arenas, _Buf(0),
-                         _Buf(0), hists, [_Buf(0)] * reps, _Stream(), reduce_fn)
+                         _Buf(0), hists, [_Buf(0)] * reps, [_Stream(), _Stream()], reduce_fn)
     r.run(7)
     waits = [k for op, k in log if op == "wait"]
     assert sorted(waits) == list(range(7))  # every reduce waited inside run()
-    # step k's reduce is waited before the histogram of step k + reps - 2 is
-    # zeroed (at most two reduces in flight)
+    # step k's buffer is zeroed again at step k + reps: only after reduce k
+    # has been waited for
     for k in range(7):
-        z = [i for i, e in enumerate(log) if e == ("zero", (k + 2) % reps)]
-        w = log.index(("wait", k))
-        later = [i for i in z if i > log.index(("reduce", k))]
-        if later:
-            assert w < later[0]
-    # reduces overlap the next step: reduce k is issued before wait k
+        zeros = [i for i, e in enumerate(log) if e == ("zero", k % reps)]
+        after = [i for i in zeros if i > log.index(("reduce", k))]
+        if after:
+            assert log.index(("wait", k)) < after[0]
+    # reduces overlap later steps: reduce k is still in flight at step k + 1
     assert log.index(("reduce", 1)) < log.index(("wait", 0))

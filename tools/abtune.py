@@ -74,7 +74,7 @@ def main():
                      for _ in range(reps)]
             fids = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(reps)]
             r = bench.FlowRunner(torch, lib, ctx, chain, n, arenas, off, lens, hists, fids,
-                                 streams[0], lambda h: None)
+                                 streams[:ns], lambda h: None)
         elif mode == "modify":
             r = bench.ModifyRunner(torch, lib, ctx, chain, n, stride, arenas, off, lens,
                                    streams[:ns])
