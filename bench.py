@@ -74,6 +74,11 @@ CONFIGS = {
 }
 # configs that time something other than the batched parse_slice records
 MODES = {"c5": "flows", "c2m": "modify", "c3r": "read"}
+# Streams the steps alternate over, measured per config (tools/abtune.py,
+# DESIGN.md §5): short launches overlap their ramp-up/drain on 2 (C2 12.3 vs
+# 15.2 us, C2m 20.5 vs 25.0) or 3 (C3s 112.5 vs 115.1); long gather-bound
+# launches gain nothing (C3 606 / 618, C4 324 / 324, C6 392 / 393 us on 1 / 2).
+STREAMS = {"c2": 2, "c2m": 2, "c3": 1, "c3r": 2, "c3s": 3, "c4": 1, "c5": 2, "c6": 1}
 FLOW_BINS = 1 << 16
 
 
@@ -312,7 +317,8 @@ def main():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--streams", type=int, default=2)
+    ap.add_argument("--streams", type=int, default=0,
+                    help="streams the steps alternate over (0 = the config's measured best)")
     ap.add_argument("--record", type=int, default=16, choices=(16, 8))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true")
@@ -322,6 +328,8 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl = RCCL over xGMI (default); gloo only to rehearse N>1 on one GPU")
     args = ap.parse_args()
+    if args.streams <= 0:
+        args.streams = STREAMS.get(args.config, 2)
 
     import torch
     import torch.distributed as dist
