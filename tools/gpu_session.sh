@@ -1,5 +1,4 @@
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-tools/gpu_step.sh 300 bench_c2 python bench.py
-tools/gpu_step.sh 300 bench_c3s python bench.py --config c3s --steps 200 --warmup 10
+tools/gpu_step.sh 900 bigfuzz python -u tools/bigfuzz.py --frames 30000000 --seed 777
