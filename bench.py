@@ -71,14 +71,18 @@ CONFIGS = {
     "c3r": ("MIXED", 1 << 24, None, "GenericUlp",
             "C3 frames as 2-chunk packets (header chunk + payload chunk, mblk-style), "
             "parse_read over chunk lists (SURVEY 8f-3), 16,777,216 per GPU, GenericUlp"),
+    "c3p": ("MIXED", 1 << 24, None, "GenericUlp",
+            "C3 frames back to back with only a length array (capture-buffer layout): "
+            "offsets scanned on the device, 16,777,216 per GPU, GenericUlp"),
 }
 # configs that time something other than the batched parse_slice records
-MODES = {"c5": "flows", "c2m": "modify", "c3r": "read"}
+MODES = {"c5": "flows", "c2m": "modify", "c3r": "read", "c3p": "packed"}
 # Streams the steps alternate over, measured per config (tools/abtune.py,
 # DESIGN.md §5): short launches overlap their ramp-up/drain on 2 (C2 12.3 vs
 # 15.2 us, C2m 20.5 vs 25.0) or 3 (C3s 112.5 vs 115.1); long gather-bound
 # launches gain nothing (C3 606 / 618, C4 324 / 324, C6 392 / 393 us on 1 / 2).
-STREAMS = {"c2": 2, "c2m": 2, "c3": 1, "c3r": 2, "c3s": 3, "c4": 1, "c5": 2, "c6": 1}
+STREAMS = {"c2": 2, "c2m": 2, "c3": 1, "c3p": 1, "c3r": 2, "c3s": 3, "c4": 1, "c5": 2,
+           "c6": 1}
 FLOW_BINS = 1 << 16
 
 
@@ -185,6 +189,29 @@ class Runner:
 
     def run(self, steps):
         """Time `steps` launches: fork all streams from streams[0], join back."""
+        return _timed(self.torch, self.streams, self.launch, steps)
+
+
+class PackedRunner:
+    """Lengths-only packed frames: ingot_gpu_parse_packed (tile-sum scan +
+    parse) on arena k % R, a workspace per stream."""
+
+    def __init__(self, torch, lib, ctx, chain, n, arenas, lens, outs, streams):
+        self.torch, self.streams = torch, streams
+        reps, h, c = len(arenas), ctx._h, int(chain)
+        aptrs = [a.data_ptr() for a in arenas]
+        outptrs = [o.data_ptr() for o in outs]
+        lptr = lens.data_ptr()
+        wb = lib.ingot_gpu_packed_workspace_size(n)
+        self.work = [torch.empty(wb, dtype=torch.uint8, device=lens.device) for _ in streams]
+        wptrs = [w.data_ptr() for w in self.work]
+        sps = [s.cuda_stream for s in streams]
+        ns = len(sps)
+        self.launch = lambda k: lib.ingot_gpu_parse_packed(h, aptrs[k % reps], lptr, n, c,
+                                                           outptrs[k % reps], None,
+                                                           wptrs[k % ns], wb, sps[k % ns])
+
+    def run(self, steps):
         return _timed(self.torch, self.streams, self.launch, steps)
 
 
@@ -397,6 +424,9 @@ def main():
         if mode == "modify":
             return ModifyRunner(torch, lib, ctx, chain, n, stride, arenas, off, lens,
                                 streams[:nstreams])
+        if mode == "packed":
+            return PackedRunner(torch, lib, ctx, chain, n, arenas, lens, outs,
+                                streams[:nstreams])
         if mode == "read":
             return ReadRunner(torch, lib, ctx, chain, n, arenas, seg_off, seg_len, pkt_seg,
                               outs, streams[:nstreams])
@@ -405,7 +435,7 @@ def main():
 
     if flows:
         args.no_variants = True
-    if mode in ("modify", "read") and args.record == 8:
+    if mode in ("modify", "read", "packed") and args.record == 8:
         ap.error("8-B records are not offered for this config")
     if chain == Chain.GeneveOverV6Tunnel and args.record == 8:
         ap.error("8-B records are not offered for the tunnel chain (include/ingot_gpu.h)")
@@ -433,6 +463,11 @@ def main():
         # chunk 0 read like a frame of the header span's length; descriptors:
         # pkt_seg (4 B) + chunk 0's (u64 off, u16 len) = 14 B
         rd, wr = algorithmic_bytes(recs_np, recs_np["payload_off"], 0, 14, 16)
+    elif mode == "packed":
+        # descriptors: the u16 length, read by the parse and once more by the
+        # tile-sum pass; tile sums and bases: 12 B per 64 packets
+        rd, wr = algorithmic_bytes(recs_np, lens_np, 0, 2, args.record)
+        rd += 2 * n + 12 * ((n + 63) // 64)
     else:
         rd, wr = algorithmic_bytes(recs_np, lens_np, stride or 0, 0 if stride else 10,
                                    args.record)
@@ -540,6 +575,7 @@ def main():
                 "traffic_detail": traffic,
                 "kernel": ("k_parse_pipe" if ring else "k_parse") + " (ingot_amd/csrc/parse.hip)" + {
                     "modify": ", OUT_MODIFY", "read": ", LAYOUT_SEGMENTED",
+                    "packed": ", LAYOUT_PACKED + k_tile_sums/k_tile_scan",
                     "flows": ", OUT_FLOWS + k_flow_count16/k_flow_reduce16"}.get(mode, ""),
                 "launch_mean_us": round(launch_ms * 1e3, 3),
                 "launch_timing": "single-stream pass, HIP events, region/K",

@@ -588,6 +588,23 @@ int ingot_gpu_flow_hist_ws(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
 size_t ingot_gpu_flow_hist_workspace_size(uint64_t n, uint32_t bins);
 
 /* ---------------------------------------------------------------------------
+ * Frames stored back to back with only a length array (a capture buffer, a
+ * ring without a descriptor table): frame i starts at d_arena + the sum of
+ * d_len[0..i).  The offsets are derived on the device — a base per
+ * 64-packet tile from a scan of tile sums (two small passes over the lengths,
+ * into the caller's workspace d_work of >= ingot_gpu_packed_workspace_size(n)
+ * bytes, 8-B aligned), then a wavefront prefix scan of each tile's lengths
+ * inside the parse — and the batch is parsed as by ingot_gpu_parse.  2 B of
+ * descriptor per packet instead of 10.  d_off_out (optional, n x u64)
+ * receives the offsets.
+ * ------------------------------------------------------------------------- */
+size_t ingot_gpu_packed_workspace_size(uint64_t n);
+int ingot_gpu_parse_packed(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
+                           const uint16_t* d_len, uint64_t n, int chain,
+                           ingot_rec* d_out, uint64_t* d_off_out, void* d_work,
+                           size_t work_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Single-header parse, batched: `HeaderParse::parse(slice)` of one header kind
  * at the start of every slice (ingot-types/src/lib.rs:137-147; the generated
  * bodies, packet/mod.rs:1831-2005) — ValidEthernet::parse, ValidIpv4::parse

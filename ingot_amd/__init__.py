@@ -123,6 +123,24 @@ class Context:
     def get_tuning(self, key: int) -> int:
         return int(self._lib.ingot_gpu_ctx_get_tuning(self._h, int(key)))
 
+    def parse_packed(self, arena, lens, chain: Chain, out=None, off_out=None, workspace=None,
+                     stream=None):
+        """ingot_gpu_parse_packed: frames back to back in `arena`, only their
+        lengths given (uint16); offsets derived on the device (optionally
+        written to `off_out`, int64).  Returns the (n, 16) records."""
+        torch = _torch()
+        n = lens.numel()
+        if out is None:
+            out = torch.empty((n, REC_BYTES), dtype=torch.uint8, device=arena.device)
+        wb = int(self._lib.ingot_gpu_packed_workspace_size(n))
+        if workspace is None:
+            workspace = torch.empty(wb, dtype=torch.uint8, device=arena.device)
+        self._check_dev(arena, lens, out, off_out, workspace)
+        _lib.check(self._lib.ingot_gpu_parse_packed(
+            self._h, _ptr(arena), _ptr(lens), n, int(chain), _ptr(out), _ptr(off_out),
+            _ptr(workspace), workspace.numel(), _stream(stream)), "ingot_gpu_parse_packed")
+        return out
+
     def parse_header(self, arena, off, lens, kind, hint=None, hints=None, stride: int = 0,
                      n: Optional[int] = None, out=None, stream=None):
         """ingot_gpu_parse_header: `ValidX::parse(slice)` of header `kind`

@@ -21,6 +21,12 @@ SIGNATURES = {
     "ingot_gpu_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "ingot_gpu_ctx_destroy": (None, [ctypes.c_void_p]),
     "ingot_gpu_ctx_device": (ctypes.c_int, [ctypes.c_void_p]),
+    "ingot_gpu_packed_workspace_size": (ctypes.c_size_t, [c_u64]),
+    "ingot_gpu_parse_packed": (
+        ctypes.c_int,
+        [ctypes.c_void_p, c_u8p, c_u8p, c_u64, ctypes.c_int, c_u8p, c_u8p, ctypes.c_void_p,
+         ctypes.c_size_t, ctypes.c_void_p],
+    ),
     "ingot_gpu_parse_header": (
         ctypes.c_int,
         [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, ctypes.c_uint32, c_u64, ctypes.c_int, c_u8p,

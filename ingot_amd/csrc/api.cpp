@@ -169,6 +169,26 @@ void ingot_gpu_ctx_destroy(ingot_gpu_ctx* ctx) { delete ctx; }
 
 int ingot_gpu_ctx_device(const ingot_gpu_ctx* ctx) { return ctx ? ctx->device : -1; }
 
+size_t ingot_gpu_packed_workspace_size(uint64_t n) { return ingot_gpu::packed_workspace(n); }
+
+int ingot_gpu_parse_packed(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint16_t* d_len,
+                           uint64_t n, int chain, ingot_rec* d_out, uint64_t* d_off_out,
+                           void* d_work, size_t work_bytes, void* stream) {
+    if (!ctx || !chain_ok(chain)) return INGOT_GPU_EINVAL;
+    if (n == 0) return INGOT_GPU_SUCCESS;
+    if (!d_arena || !d_len || !d_out || !d_work || ((uintptr_t)d_work & 7u)) return INGOT_GPU_EINVAL;
+    if (work_bytes < ingot_gpu::packed_workspace(n)) return INGOT_GPU_ERANGE;
+    if (int e = enter(ctx)) return e;
+    const hipStream_t s = (hipStream_t)stream;
+    if (int e = from_hip(ingot_gpu::launch_tile_bases(d_len, n, d_work, s))) return e;
+    const uint64_t ngroups = ((n + 63) / 64 + ingot_gpu::PACKED_GROUP - 1) / ingot_gpu::PACKED_GROUP;
+    ingot_gpu::ParseArgs a{d_arena, static_cast<const uint64_t*>(d_work), d_len, 0, n, d_out};
+    a.tile_local = reinterpret_cast<const uint32_t*>(static_cast<const uint64_t*>(d_work) + ngroups);
+    a.off_out = d_off_out;
+    return from_hip(ingot_gpu::launch_parse(a, ingot_gpu::LAYOUT_PACKED, chain,
+                                            ingot_gpu::OUT_REC16, tuning_for(ctx, d_arena), s));
+}
+
 int ingot_gpu_parse_header(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
                            const uint16_t* d_len, uint32_t stride, uint64_t n, int kind,
                            const uint32_t* d_hint, uint32_t hint, ingot_hdr* d_out,

@@ -12,7 +12,11 @@ namespace ingot_gpu {
 // STRIDED: frame i at i*stride; INDEXED: (off[i], len[i]); SEGMENTED: packet i
 // is the chunks pkt_seg[i] .. pkt_seg[i+1] of (off, len) = (seg_off, seg_len),
 // walked with parse_read's chunk semantics.
-enum LayoutKind { LAYOUT_STRIDED = 0, LAYOUT_INDEXED = 1, LAYOUT_SEGMENTED = 2 };
+// PACKED: frames back to back with only a length array; `off` holds one u64
+// base per group of tiles and `tile_local` each tile's prefix in its group
+// (packed.hip); the frame offsets come from a wavefront prefix scan of the
+// tile's lengths.
+enum LayoutKind { LAYOUT_STRIDED = 0, LAYOUT_INDEXED = 1, LAYOUT_SEGMENTED = 2, LAYOUT_PACKED = 3 };
 
 // Output mode: 16-B ingot_rec, 8-B ingot_rec8, 256-B ingot_fields, or the
 // flow hash + histogram.
@@ -31,6 +35,8 @@ struct ParseArgs {
     void* out;             // n records of the OutMode's type
     const uint32_t* pkt_seg = nullptr;  // LAYOUT_SEGMENTED: n+1 chunk-index bounds
     uint16_t* chunk = nullptr;          // LAYOUT_SEGMENTED, optional: remainder's chunk
+    uint64_t* off_out = nullptr;        // LAYOUT_PACKED, optional: the computed offsets
+    const uint32_t* tile_local = nullptr;  // LAYOUT_PACKED: tile prefix within its group
     uint32_t policy = 0;                // INGOT_TUNE_CACHE_POLICY bits (launch_parse sets it)
 };
 
@@ -74,6 +80,13 @@ struct HeaderArgs {
     ingot_hdr* out;
 };
 hipError_t launch_header(const HeaderArgs& a, hipStream_t s);
+
+// Lengths-only packed frames (packed.hip): tile base = u64 base of its group
+// of PACKED_GROUP tiles (at the start of `work`, >= packed_workspace(n)
+// bytes) + the tile's u32 prefix within the group (after the group bases).
+constexpr uint32_t PACKED_GROUP = 128;
+size_t packed_workspace(uint64_t n);
+hipError_t launch_tile_bases(const uint16_t* len, uint64_t n, void* work, hipStream_t s);
 
 // Per-context tuning (0 = measured default); see INGOT_TUNE_* in ingot_gpu.h.
 struct Tuning {

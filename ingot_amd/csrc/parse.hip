@@ -977,6 +977,18 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
             off = i * a.stride;
             len = valid ? (a.len ? (uint32_t)a.len[i] : a.stride) : 0u;
             if (len > a.stride) len = a.stride;  // a slot holds at most one frame
+        } else if constexpr (LAYOUT == LAYOUT_PACKED) {
+            // frames back to back: offset = the tile's base + the exclusive
+            // prefix of the tile's lengths (wavefront scan, 6 shuffle steps)
+            len = valid ? (uint32_t)a.len[i] : 0u;
+            uint32_t x = len;
+#pragma unroll
+            for (uint32_t d = 1; d < WAVE; d <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)x, d);
+                if (lane >= d) x += y;
+            }
+            off = a.off[t / PACKED_GROUP] + a.tile_local[t] + (x - len);
+            if (valid && a.off_out) a.off_out[i] = off;
         } else {
             off = valid ? a.off[i] : 0u;
             len = valid ? (uint32_t)a.len[i] : 0u;
@@ -1457,6 +1469,13 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
         if (w == 4) return launch_mode<4, LAYOUT_STRIDED>(a, chain, mode, g, s);
         if (w == 5) return launch_mode<5, LAYOUT_STRIDED>(a, chain, mode, g, s);
         return launch_mode<8, LAYOUT_STRIDED>(a, chain, mode, g, s);
+    }
+    if (layout_kind == LAYOUT_PACKED) {
+        switch (t.window_indexed ? t.window_indexed : tun ? 8 : host ? 5 : 3) {
+        case 3: return launch_mode<3, LAYOUT_PACKED>(a, chain, mode, g, s);
+        case 8: return launch_mode<8, LAYOUT_PACKED>(a, chain, mode, g, s);
+        default: return launch_mode<5, LAYOUT_PACKED>(a, chain, mode, g, s);
+        }
     }
     switch (t.window_indexed ? t.window_indexed : tun ? 8 : host ? 5 : 3) {
     case 100: return launch_mode<0, LAYOUT_INDEXED>(a, chain, mode, g, s);

@@ -48,7 +48,7 @@ def test_config_table():
         Chain[chain]
     # the metric's configuration (BASELINE.json configs[1]) is the default
     assert bench.CONFIGS["c2"][:4] == ("V4UDP64", 1 << 20, 64, "UdpParser")
-    assert set(bench.MODES.values()) <= {"flows", "modify", "read"}
+    assert set(bench.MODES.values()) <= {"flows", "modify", "read", "packed"}
     assert set(bench.STREAMS) == set(bench.CONFIGS)
     assert all(1 <= v <= 4 for v in bench.STREAMS.values())
 

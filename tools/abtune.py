@@ -75,6 +75,8 @@ def main():
             fids = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(reps)]
             r = bench.FlowRunner(torch, lib, ctx, chain, n, arenas, off, lens, hists, fids,
                                  streams[:ns], lambda h: None)
+        elif mode == "packed":
+            r = bench.PackedRunner(torch, lib, ctx, chain, n, arenas, lens, outs, streams[:ns])
         elif mode == "modify":
             r = bench.ModifyRunner(torch, lib, ctx, chain, n, stride, arenas, off, lens,
                                    streams[:ns])
