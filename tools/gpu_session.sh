@@ -1,6 +1,11 @@
+# Evidence refresh: full GPU suite, smoke, bench lines for every config,
+# rocprofv3 kernel stats of the default command.
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-tools/gpu_step.sh 300 pytest_packed python -u -m pytest tests/test_packed.py -x -q -m gpu --timeout 120 --timeout-method thread
-tools/gpu_step.sh 300 ab_c3p python tools/abtune.py --config c3p --rounds 3 --var mode=packed --var mode=parse --out gpurun_out/ab_c3p.json
-tools/gpu_step.sh 200 prof_c3p rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_c3p -o run -- python3 bench.py --config c3p --steps 30 --warmup 2 --no-cpu-baseline --no-variants
+tools/gpu_step.sh 900 pytest_gpu python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread
+tools/gpu_step.sh 200 smoke python -c "import __graft_entry__ as g; g.smoke()"
+tools/gpu_step.sh 300 bench_c2 python bench.py
+for c in c2m c3 c3p c3r c3s c4 c5 c6; do
+tools/gpu_step.sh 300 bench_$c python bench.py --config $c --steps 200 --warmup 10
+done
