@@ -186,3 +186,26 @@ def test_parse_modify_in_host_memory(torch, ctx, stride):
     diff = np.nonzero(got != want)[0]
     assert diff.size == 0, (diff[:10], got[diff[:10]], want[diff[:10]])
     assert (got != arena.cpu().numpy()).any()  # something was rewritten
+
+
+def test_parse_packed_from_host_capture_buffer(torch, ctx):
+    """A capture buffer in host memory (frames back to back, lengths only):
+    ingot_gpu_parse_packed scans the lengths and parses across PCIe; records
+    and derived offsets equal the device-resident parse with offsets."""
+    lib = _lib.load()
+    n = 30_011
+    arena, off, lens = ingot_amd.gen_frames(GenProfile.MIXED, n, seed=19)
+    want = ctx.parse(arena, off, lens, Chain.GenericUlp)
+    torch.cuda.synchronize()
+    h_arena, h_lens = _pinned(torch, arena), _pinned(torch, lens)
+    h_out = torch.zeros((n, 16), dtype=torch.uint8, pin_memory=True)
+    h_off = torch.zeros(n, dtype=torch.int64, pin_memory=True)
+    wb = lib.ingot_gpu_packed_workspace_size(n)
+    work = torch.empty(wb, dtype=torch.uint8, device="cuda")
+    rc = lib.ingot_gpu_parse_packed(ctx._h, ctx.host_map(h_arena), ctx.host_map(h_lens), n,
+                                    int(Chain.GenericUlp), ctx.host_map(h_out),
+                                    ctx.host_map(h_off), work.data_ptr(), wb, None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert h_out.numpy().tobytes() == want.cpu().numpy().tobytes()
+    assert (h_off.numpy() == off.cpu().numpy()).all()
