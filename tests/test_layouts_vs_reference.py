@@ -144,3 +144,40 @@ def test_setter_geometry_matches_reference_declaration():
         assert kinds[hdr] == kind, name
         ref, _ = reference_layout(REF / structs[hdr][0], structs[hdr][1])
         assert ref[field.lower()] == (int(bit), int(width)), (name, ref[field.lower()], bit, width)
+
+
+def _consts(src: str, ty: str):
+    block = re.search(r"impl " + ty + r" \{(.*?)\n\}", src, re.S).group(1)
+    return {k: int(v, 0) for k, v in re.findall(r"pub const (\w+): Self = Self\((\w+)\);", block)}
+
+
+@pytest.mark.skipif(not REF.exists(), reason="reference checkout not present")
+def test_protocol_constants_and_eh_classes_match_reference():
+    """Ethertype / IpProtocol constants (ethernet.rs:12-20, ip.rs:20-38) and
+    IpProtocol::class (ip.rs:40-54) against layouts.h, the kernel's eh_class
+    and the oracle's."""
+    import oracle
+
+    et = _consts((REF / "ethernet.rs").read_text(), "Ethertype")
+    ip = (REF / "ip.rs").read_text()
+    pp = _consts(ip, "IpProtocol")
+    lay = LAYOUTS.read_text()
+    for ours, theirs in (("ET_IPV4", "IPV4"), ("ET_ARP", "ARP"), ("ET_VLAN", "VLAN"),
+                         ("ET_IPV6", "IPV6"), ("ET_QINQ", "QINQ")):
+        assert re.search(rf"{ours} = 0x{et[theirs]:04x}\b", lay), ours
+    for ours, theirs in (("IPP_ICMP", "ICMP"), ("IPP_TCP", "TCP"), ("IPP_UDP", "UDP"),
+                         ("IPP_ICMP_V6", "ICMP_V6")):
+        assert re.search(rf"{ours} = {pp[theirs]}\b", lay), ours
+    cls = re.search(r"pub fn class\(self\).*?match self \{(.*?)\n\s*_ => None", ip, re.S).group(1)
+    frag = {pp[n] for n in re.findall(r"Self::(\w+) => Some\(ExtHdrClass::FragmentHeader\)", cls)}
+    r6564_src = cls.split("FragmentHeader),", 1)[1]
+    r6564 = {pp[n] for n in re.findall(r"Self::(\w+)", r6564_src)}
+    assert frag == {44} and 0 in r6564 and len(r6564) == 8
+    kernel = (LAYOUTS.parent / "parse.hip").read_text()
+    body = re.search(r"uint32_t eh_class\(uint32_t h\) \{(.*?)\n\}", kernel, re.S).group(1)
+    k_frag = {int(x) for x in re.findall(r"h == (\d+)u\) return EH_FRAGMENT", body)}
+    k_6564 = {int(x) for x in re.findall(r"h == (\d+)u", body)} - k_frag
+    assert k_frag == frag and k_6564 == r6564
+    for p in range(256):
+        want = 1 if p in frag else 2 if p in r6564 else 0
+        assert oracle.v6eh_class(p) == want, p
