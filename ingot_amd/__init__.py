@@ -55,7 +55,8 @@ from .abi import (  # noqa: F401  (re-exports)
 __all__ = [
     "Chain", "Context", "GenProfile", "PacketParseError", "ParseError", "UdpParser",
     "GenericUlp", "VlanUlp", "GeneveOverV6Tunnel", "gen_frames", "gen_lengths", "records_to_numpy",
-    "fields_to_numpy", "load_library", "Parsed", "chunk_tables",
+    "fields_to_numpy", "load_library", "Parsed", "chunk_tables", "HeaderKind", "parse_header",
+    "HeaderParseError",
 ]
 
 
@@ -724,6 +725,37 @@ def parse_frames(frames: list, chain: Chain, device: int = 0):
         flds = fields_to_numpy(ctx.fields(arena, off, lens, chain))
     torch.cuda.synchronize(device)
     return records_to_numpy(recs), flds
+
+
+class HeaderParseError(Exception):
+    """A single header's ParseError (HeaderParse::parse returns a bare
+    ParseError, ingot-types/src/lib.rs:137-147)."""
+
+    def __init__(self, inner: ParseError):
+        super().__init__(inner.name)
+        self.inner = inner
+
+
+def parse_header(kind: HeaderKind, data: bytes, hint: Optional[int] = None, device: int = 0):
+    """`ValidX::parse(data)` for header `kind`, or a choice's
+    `parse_choice(data, hint)` (HeaderKind.L3 / L4 / Ulp), on the device:
+    -> (variant HeaderKind, HeaderLen, NextLayer hint or None, remainder
+    bytes), or raises HeaderParseError."""
+    import numpy as np
+
+    torch = _torch()
+    data = bytes(data)
+    dev = f"cuda:{device}"
+    arena = torch.from_numpy(np.frombuffer(data + bytes(16), np.uint8).copy()).to(dev)
+    off = torch.zeros(1, dtype=torch.int64, device=dev)
+    lens = torch.tensor([len(data)], dtype=torch.int32).to(torch.uint16).to(dev)
+    out = _ctx_for(device).parse_header(arena, off, lens, kind, hint=hint).cpu().numpy()
+    status, variant = int(out[0, 0]), int(out[0, 1])
+    used = int(out[0, 2]) | int(out[0, 3]) << 8
+    h = int(out[0, 4:8].view(np.uint32)[0])
+    if status:
+        raise HeaderParseError(ParseError(status))
+    return HeaderKind(variant), used, (None if h == HINT_NONE else h), data[used:]
 
 
 def chunk_tables(packets):

@@ -105,3 +105,36 @@ def test_header_strided_and_scalar_hint(torch, ctx):
                                       0, out.data_ptr(), None) == -1  # no such kind
     assert lib.ingot_gpu_parse_header(ctx._h, arena.data_ptr(), None, None, 0, 4, 0, None,
                                       0, out.data_ptr(), None) == -5  # no offsets, no stride
+
+
+def test_python_mirror_reads_like_the_reference(torch, kats):
+    """ingot's own single-header tests, restated on the Python mirror:
+    base_parse (ingot/src/tests.rs:57-71), v6_repeat_extension_headers
+    (tests.rs:332-368), the choice bench (ingot-examples/benches/choice.rs)."""
+    from ingot_amd import HeaderParseError, parse_header
+
+    hk = {k["name"]: k for k in kats["header_kats"]}
+    ck = {k["name"]: k for k in kats["choice_kats"]}
+    # let (eth, ..) = ValidEthernet::parse(&buf[..]).unwrap(); ipv6 over zeros
+    v, used, hint, rest = parse_header(HeaderKind.Ethernet, bytes.fromhex(hk["base_parse_ethernet"]["bytes"]))
+    assert (v, used, hint, len(rest)) == (HeaderKind.Ethernet, 14, 0, 40)
+    v, used, hint, _ = parse_header(HeaderKind.Ipv6, bytes.fromhex(hk["base_parse_ipv6_tcp"]["bytes"]))
+    assert (used, hint) == (40, 6)
+    # the EH chain: v6.next_layer() == Some(IpProtocol::UDP)
+    v, used, hint, _ = parse_header(HeaderKind.Ipv6,
+                                    bytes.fromhex(hk["v6_repeat_extension_headers"]["bytes"]))
+    assert (used, hint) == (96, 17)
+    # ValidL3::parse_choice(&pkt_body_v4[14..], Some(Ethertype::IPV4)) / LLDP
+    body = bytes.fromhex(ck["choice_l3_success"]["bytes"])
+    v, used, hint, rest = parse_header(HeaderKind.L3, body, hint=0x0800)
+    assert (v, used, hint) == (HeaderKind.Ipv4, 20, 17) and rest == body[20:]
+    with pytest.raises(HeaderParseError) as e:
+        parse_header(HeaderKind.L3, body, hint=0x88CC)
+    assert e.value.inner.name == "Unwanted"
+    with pytest.raises(HeaderParseError) as e:
+        parse_header(HeaderKind.L3, body)
+    assert e.value.inner.name == "NeedsHint"
+    # RepeatedView over 20 B of Udp: TooSmall (tests.rs:377-380)
+    with pytest.raises(HeaderParseError) as e:
+        parse_header(HeaderKind.RepeatedUdp, bytes(20))
+    assert e.value.inner.name == "TooSmall"
