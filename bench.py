@@ -99,6 +99,23 @@ def algorithmic_bytes(recs_np, lens_np, stride, descriptor_bytes, record_bytes):
     return int(r.sum()), record_bytes * len(recs_np)
 
 
+def host_inclusive(config: str):
+    """The host-inclusive rates of this config (frames start and end in host
+    memory), from the committed tools/hostpath.py measurement — reported
+    beside `value`, never as it."""
+    f = sorted(ROOT.glob("profiles/*_hostpath.json"))
+    if not f:
+        return None
+    d = json.loads(f[-1].read_text())
+    if config not in d:
+        return None
+    out = {"memcpy_Mpkt_s": d[config]["host_inclusive_Mpkt_s"],
+           "source": f"{f[-1].relative_to(ROOT)} (tools/hostpath.py, 1 M frames per batch)"}
+    if f"{config}_zc" in d:
+        out["zero_copy_Mpkt_s"] = d[f"{config}_zc"]["host_inclusive_Mpkt_s"]
+    return out
+
+
 def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode="parse",
                  segs=None):
     """Time the oracle on the host cores over the same frames (bounded).
@@ -590,6 +607,7 @@ def main():
             "variants": variants,
             "cpu_baseline": cpu,
             "wall_s_timed_region": round(wall, 4),
+            "host_inclusive": host_inclusive(args.config),
         }
         print(json.dumps(result), flush=True)
     if world > 1:
