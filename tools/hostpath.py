@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--zero-copy", action="store_true")
     ap.add_argument("--win", type=int, default=0, help="staged window (INGOT_TUNE_WINDOW_*)")
+    ap.add_argument("--rec8", action="store_true", help="8-B records (zero-copy mode)")
     args = ap.parse_args()
 
     import torch
@@ -84,11 +85,12 @@ def main():
     def step_zc(k):
         s = streams[k % S].cuda_stream
         if host_desc is not None:
-            rc = lib.ingot_gpu_parse(ctx._h, d_arena[k % R], d_off, d_len, n, int(chain),
-                                     d_recs[k % R], s)
+            fn = lib.ingot_gpu_parse_compact if args.rec8 else lib.ingot_gpu_parse
+            rc = fn(ctx._h, d_arena[k % R], d_off, d_len, n, int(chain), d_recs[k % R], s)
         else:
-            rc = lib.ingot_gpu_parse_strided(ctx._h, d_arena[k % R], stride, d_slot_lens, n,
-                                             int(chain), d_recs[k % R], s)
+            fn = lib.ingot_gpu_parse_strided_compact if args.rec8 else \
+                lib.ingot_gpu_parse_strided
+            rc = fn(ctx._h, d_arena[k % R], stride, d_slot_lens, n, int(chain), d_recs[k % R], s)
         assert rc == 0
 
     def step(k):
@@ -120,7 +122,7 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     h2d = arena.numel() + desc_bytes
-    d2h = n * 16
+    d2h = n * (8 if args.rec8 else 16)
     # raw copy ceilings for context
     t1 = time.perf_counter()
     for k in range(50):
@@ -129,7 +131,7 @@ def main():
     h2d_gbs = 50 * arena.numel() / (time.perf_counter() - t1) / 1e9
     res = {
         "config": args.config, "mode": "zero-copy" if args.zero_copy else "memcpy",
-        "window": args.win or "default",
+        "window": args.win or "default", "record_bytes": 8 if args.rec8 else 16,
         "frames_per_batch": n, "streams": S, "steps": args.steps,
         "host_inclusive_Mpkt_s": round(n * args.steps / dt / 1e6, 1),
         "ms_per_batch": round(dt / args.steps * 1e3, 4),
@@ -141,7 +143,8 @@ def main():
         res["note"] = ("zero-copy: nothing is copied; bytes_h2d/pcie_GBps_effective count what "
                        "the memcpy path would move for the same batch")
     print(json.dumps(res))
-    out = ROOT / "gpurun_out" / f"hostpath_{args.config}{'_zc' if args.zero_copy else ''}.json"
+    tag = ("_zc" if args.zero_copy else "") + ("_rec8" if args.rec8 else "")
+    out = ROOT / "gpurun_out" / f"hostpath_{args.config}{tag}.json"
     out.parent.mkdir(exist_ok=True)
     out.write_text(json.dumps(res, indent=1))
 
