@@ -58,7 +58,7 @@ def test_shard_and_split():
         idist.shard(4, 4, 1)
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 4])
 def test_histogram_allreduce_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
