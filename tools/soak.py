@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Validation tool: determinism soak of the pipelined kernels.  Thousands of
+launches of the ring kernel (C2 slots, 2 streams), the flow kernel
+(persistent grid) and the packed-layout parse, each output compared on the
+device with the first run's over the same arena (which the parity tests pin
+to the oracle) — an intermittent race in LDS-image reuse or the persistent
+grids would show up as a mismatch.  Writes gpurun_out/soak.json.
+
+    python tools/soak.py [--iters 3000]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=3000)
+    args = ap.parse_args()
+
+    import torch
+
+    import ingot_amd
+    from ingot_amd import Chain, GenProfile
+
+    ctx = ingot_amd.Context(0)
+    res, t0 = {}, time.time()
+    s = [torch.cuda.current_stream(), torch.cuda.Stream()]
+
+    # ring kernel: 4 arenas x 1 M x 64-B slots, steps alternating over 2 streams
+    n = 1 << 20
+    arenas = [ingot_amd.gen_frames(GenProfile.ADVERSARIAL if k % 2 else GenProfile.V4UDP64, n,
+                                   seed=k, stride=64)[0] for k in range(4)]
+    want = [ctx.parse_strided(a, 64, n, Chain.UdpParser) for a in arenas]
+    outs = [torch.empty_like(w) for w in want]
+    torch.cuda.synchronize()
+    # mismatch counters on the device, one per stream (no host sync inside the
+    # loop, so the two streams keep overlapping; outs[k] is rewritten 4 steps
+    # later on the same stream, after its comparison)
+    acc = [torch.zeros((), dtype=torch.int64, device="cuda") for _ in s]
+    for it in range(args.iters):
+        k = it % 4
+        st = s[it % 2]
+        ctx.parse_strided(arenas[k], 64, n, Chain.UdpParser, out=outs[k], stream=st)
+        with torch.cuda.stream(st):
+            acc[it % 2] += (outs[k] != want[k]).any().to(torch.int64)
+    torch.cuda.synchronize()
+    bad = int(sum(a.item() for a in acc))
+    res["ring_kernel_c2"] = {"launches": args.iters, "mismatching_launches": bad}
+    del arenas, want, outs
+
+    # flow kernel (persistent grid) on VLAN/v6 traffic
+    m = 1 << 21
+    arena, off, lens = ingot_amd.gen_frames(GenProfile.FLOWS, m, seed=3)
+    h0 = torch.zeros(m, dtype=torch.int32, device="cuda")
+    f0 = ctx.flow_hist(arena, off, lens, Chain.VlanUlp, hashes=h0)
+    torch.cuda.synchronize()
+    bad = 0
+    for it in range(args.iters // 10):
+        h = torch.zeros(m, dtype=torch.int32, device="cuda")
+        f = ctx.flow_hist(arena, off, lens, Chain.VlanUlp, hashes=h)
+        bad += int(not (torch.equal(f, f0) and torch.equal(h, h0)))
+    torch.cuda.synchronize()
+    res["flow_kernel"] = {"launches": args.iters // 10, "mismatching_launches": bad}
+
+    # packed layout (tile scan + in-kernel prefix scan)
+    want = ctx.parse(arena, off, lens, Chain.VlanUlp)
+    bad = 0
+    for it in range(args.iters // 10):
+        got = ctx.parse_packed(arena, lens, Chain.VlanUlp)
+        bad += int(not torch.equal(got, want))
+    torch.cuda.synchronize()
+    res["packed_layout"] = {"launches": args.iters // 10, "mismatching_launches": bad}
+
+    out = {"wall_s": round(time.time() - t0, 1), "checks": res,
+           "all_zero": all(v["mismatching_launches"] == 0 for v in res.values())}
+    print(json.dumps(out))
+    (ROOT / "gpurun_out").mkdir(exist_ok=True)
+    (ROOT / "gpurun_out" / "soak.json").write_text(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
