@@ -396,7 +396,10 @@ int ingot_gpu_ctx_get_tuning(const ingot_gpu_ctx* ctx, int key);
 /*
  * Batched `<Chain>::parse_slice` over frames in a device arena.
  *
- *   d_arena   device pointer to the packet bytes
+ *   d_arena   device pointer to the packet bytes, any alignment (the
+ *             kernels align the absolute addresses they stage; they may read
+ *             up to 15 bytes before d_arena + d_off[i] and after a frame's
+ *             end, never outside that frame's 16-byte blocks)
  *   d_off     per-packet byte offset into d_arena (u64)
  *   d_len     per-packet length in bytes (u16)
  *   n         number of packets

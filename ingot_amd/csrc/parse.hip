@@ -782,18 +782,20 @@ constexpr uint32_t WB_BYTES = 32;  // write-back unit (aligned), see below
 struct EditSink {
     uint8_t* frame;     // frame start in HBM
     uint64_t off;       // frame start, arena offset
-    uint64_t base;      // staging base (off & ~15), arena offset
+    int64_t base;       // staging base (16-B aligned address), arena offset
     uint32_t len;       // frame length
     uint32_t staged;    // staged chunks for this frame (0 = none)
     uint32_t dirty;     // sector first-chunk bits
+    uint32_t mis;       // arena address mod 32 (sectors are aligned addresses)
 };
 
 template <class FR>
 __device__ __forceinline__ void put_byte(const FR& f, EditSink& k, uint32_t i, uint8_t v) {
     f.put_staged(i, v);
-    const uint64_t a = k.off + i;
-    const uint64_t s = a & ~(uint64_t)(WB_BYTES - 1u);
-    if (s >= k.off && s + WB_BYTES <= k.off + k.len && s + WB_BYTES <= k.base + 16u * k.staged) {
+    const int64_t a = (int64_t)(k.off + i);
+    const int64_t s = ((a + k.mis) & ~(int64_t)(WB_BYTES - 1u)) - k.mis;  // aligned sector
+    if (s >= (int64_t)k.off && s + WB_BYTES <= (int64_t)(k.off + k.len) &&
+        s + WB_BYTES <= k.base + 16 * (int64_t)k.staged) {
         k.dirty |= 1u << (uint32_t)((s - k.base) >> 4);
     } else {
         k.frame[i] = v;
@@ -959,6 +961,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
     const uint32_t wave = threadIdx.x / WAVE;
     uint32_t* wimg = s_win + wave * WAVE_DW;
     const uint64_t ntiles = (a.n + WAVE - 1u) / WAVE;
+    const uint32_t mis = (uint32_t)((uintptr_t)a.arena & 31u);  // arena address mod 32
 
     for (uint64_t t = (uint64_t)blockIdx.x * WAVES + wave; t < ntiles;
          t += (uint64_t)gridDim.x * WAVES) {
@@ -993,8 +996,11 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
             off = valid ? a.off[i] : 0u;
             len = valid ? (uint32_t)a.len[i] : 0u;
         }
-        const uint64_t base = off & ~(uint64_t)15;
-        const uint32_t sh = (uint32_t)(off & 15u);
+        // 16-B alignment of the absolute address (the arena itself may be at
+        // any alignment): the staged chunks are aligned loads, `base` may sit
+        // up to 15 B before the arena (same 16-B block: same page).
+        const uint32_t sh = (uint32_t)((off + mis) & 15u);
+        const int64_t base = (int64_t)off - (int64_t)sh;
         const uint32_t take = NCH == 0 ? 0u : (len < WIN - sh ? len : WIN - sh);
         const uint32_t nch = (sh + take + 15u) >> 4;
 
@@ -1007,11 +1013,11 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
             const uint32_t pp = q / NCH1;
             const uint32_t c = (q - pp * NCH1) ^ swz<NCH>(pp);
             const uint32_t np = (uint32_t)__shfl((int)nch, (int)pp);
-            uint64_t bp;
+            int64_t bp;
             if constexpr (LAYOUT == LAYOUT_STRIDED) {
-                bp = (t * WAVE + pp) * a.stride;
+                bp = (int64_t)((t * WAVE + pp) * a.stride);
             } else {
-                bp = (uint64_t)__shfl((long long)base, (int)pp);
+                bp = (int64_t)__shfl((long long)base, (int)pp);
             }
             if (c < np) stage16(a.arena + bp + 16u * c, wimg + k * WAVE * 4u, a.policy & 1u);
         }
@@ -1062,7 +1068,8 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
             // edits' bytes: put8 updates HBM and the staged window)
             walk<CHAIN, false>(fr, r, nullptr, nullptr);
             if (valid && r.status == INGOT_OK) {
-                EditSink sink{const_cast<uint8_t*>(a.arena) + off, off, base, len, NCH ? nch : 0u, 0u};
+                EditSink sink{const_cast<uint8_t*>(a.arena) + off, off, base, len, NCH ? nch : 0u,
+                              0u, mis};
                 for (uint32_t k = 0; k < args.n_edits; ++k) {
                     const Edit e = args.e[k];
                     uint32_t h;

@@ -469,3 +469,44 @@ def test_maximum_size_frames(ctx, torch, chain):
     torch.cuda.synchronize()
     ws = oracle.parse_batch(slots, None, sl, chain, stride=stride, n=n)
     assert rs.cpu().numpy().tobytes() == ws.tobytes()
+
+
+# ---------------------------------------------------------------------------
+# arenas at any alignment (the staging aligns absolute addresses)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("mis", [1, 3, 8, 15, 17])
+def test_misaligned_arena_base(ctx, torch, mis):
+    """The same frames in an arena whose base address is not 16-B aligned:
+    records, getters, parse_packed, parse_read, flows and in-place rewrites
+    equal the aligned arena's (and rewrites touch only the frames' bytes)."""
+    from ingot_amd import EditOp, Field
+
+    n = 20_011
+    arena, off, lens = ingot_amd.gen_frames(GenProfile.ADVERSARIAL, n, seed=mis)
+    big = torch.zeros(arena.numel() + 64, dtype=torch.uint8, device="cuda")
+    big[mis:mis + arena.numel()] = arena
+    view = big[mis:mis + arena.numel()]
+    assert view.data_ptr() % 16 == mis % 16
+    for chain in Chain:
+        assert torch.equal(ctx.parse(view, off, lens, chain), ctx.parse(arena, off, lens, chain))
+        assert torch.equal(dev_fields(ctx, view, off, lens, chain),
+                           dev_fields(ctx, arena, off, lens, chain))
+    assert torch.equal(ctx.parse_packed(view, lens, Chain.GenericUlp),
+                       ctx.parse(arena, off, lens, Chain.GenericUlp))
+    f1 = ctx.flow_hist(view, off, lens, Chain.VlanUlp)
+    f2 = ctx.flow_hist(arena, off, lens, Chain.VlanUlp)
+    assert torch.equal(f1, f2)
+    # chunk lists: every frame one chunk
+    pkt_seg = torch.arange(0, n + 1, dtype=torch.int32, device="cuda")
+    r1, c1 = ctx.parse_read(view, off, lens.view(torch.int16), pkt_seg, Chain.GenericUlp)
+    r2, c2 = ctx.parse_read(arena, off, lens.view(torch.int16), pkt_seg, Chain.GenericUlp)
+    assert torch.equal(r1, r2) and torch.equal(c1, c2)
+    # in-place rewrite: same bytes afterwards, padding around the view intact
+    edits = [(2, Field.UDP_DESTINATION, EditOp.SUB, 1), (1, Field.V4_HOP_LIMIT, EditOp.SUB, 1),
+             (2, Field.TCP_FLAGS, EditOp.XOR, 0x10)]
+    a2 = arena.clone()
+    ctx.parse_modify(view, off, lens, Chain.GenericUlp, edits)
+    ctx.parse_modify(a2, off, lens, Chain.GenericUlp, edits)
+    torch.cuda.synchronize()
+    assert torch.equal(view, a2)
+    assert int(big[:mis].abs().sum()) == 0 and int(big[mis + arena.numel():].sum()) == 0
