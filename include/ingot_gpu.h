@@ -401,7 +401,10 @@ int ingot_gpu_ctx_get_tuning(const ingot_gpu_ctx* ctx, int key);
  *             up to 15 bytes before d_arena + d_off[i] and after a frame's
  *             end, never outside that frame's 16-byte blocks)
  *   d_off     per-packet byte offset into d_arena (u64)
- *   d_len     per-packet length in bytes (u16)
+ *   d_len     per-packet length in bytes (u16); the caller guarantees every
+ *             [d_off[i], d_off[i] + d_len[i]) lies inside its allocation
+ *             (ingot's borrowed-slice contract: the kernels read no byte of
+ *             a frame past d_len[i] except within its last 16-byte block)
  *   n         number of packets
  *   chain     enum ingot_chain
  *   d_out     n records (device memory, 16 B each)
