@@ -840,6 +840,9 @@ __device__ __forceinline__ void apply_edit(const FR& f, EditSink& sink, uint32_t
 // blocks per CU instead of 5, worth more than the conflicts cost.  Built once
 // per block (the flows grid is persistent).
 constexpr uint32_t FLOW_POS = FLOW_INPUT_BITS / 4;
+#ifndef INGOT_FLOW_SKIP
+#define INGOT_FLOW_SKIP 12
+#endif
 #ifndef INGOT_FLOW_COPIES
 #define INGOT_FLOW_COPIES 1
 #endif
@@ -962,6 +965,9 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
     uint32_t* wimg = s_win + wave * WAVE_DW;
     const uint64_t ntiles = (a.n + WAVE - 1u) / WAVE;
     const uint32_t mis = (uint32_t)((uintptr_t)a.arena & 31u);  // arena address mod 32
+    constexpr uint32_t SKIP =
+        MODE == OUT_FLOWS && LAYOUT == LAYOUT_INDEXED && !TUN ? INGOT_FLOW_SKIP : 0u;
+    static_assert(SKIP <= 12u, "the walk reads the ethertype at frame byte 12");
 
     for (uint64_t t = (uint64_t)blockIdx.x * WAVES + wave; t < ntiles;
          t += (uint64_t)gridDim.x * WAVES) {
@@ -999,10 +1005,25 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
         // 16-B alignment of the absolute address (the arena itself may be at
         // any alignment): the staged chunks are aligned loads, `base` may sit
         // up to 15 B before the arena (same 16-B block: same page).
-        const uint32_t sh = (uint32_t)((off + mis) & 15u);
-        const int64_t base = (int64_t)off - (int64_t)sh;
-        const uint32_t take = NCH == 0 ? 0u : (len < WIN - sh ? len : WIN - sh);
-        const uint32_t nch = (sh + take + 15u) >> 4;
+        // Flows (indexed frames): the window starts at the 16-B chunk holding
+        // frame byte SKIP (12, the ethertype), not at the frame start — the
+        // MAC addresses are never read there, and NCH chunks then reach past
+        // the IPv6 addresses and ports.  Frame bytes [SKIP - sh, SKIP - sh +
+        // WIN) are staged; the walk reads nothing below SKIP, so `avail` (the
+        // window's end) is the only bound Frame checks, and fr.sh = sh - SKIP
+        // (mod 2^32) maps frame byte i >= SKIP to image byte i + sh - SKIP.
+        const uint32_t sh = (uint32_t)((off + SKIP + mis) & 15u);
+        const int64_t base = (int64_t)off + (int64_t)SKIP - (int64_t)sh;
+        uint32_t take, nch;
+        if constexpr (SKIP == 0) {
+            take = NCH == 0 ? 0u : (len < WIN - sh ? len : WIN - sh);
+            nch = (sh + take + 15u) >> 4;
+        } else {
+            const uint32_t wend = SKIP + WIN - sh;  // frame byte after the window
+            take = len < wend ? len : wend;
+            const int32_t staged = (int32_t)take - ((int32_t)SKIP - (int32_t)sh);
+            nch = staged > 0 ? ((uint32_t)staged + 15u) >> 4 : 0u;
+        }
 
         // Stage: instruction k, lane L fills LDS slot q = 64k + L, i.e.
         // packet p = q / NCH, swizzled chunk c.  (LDS-DMA: lane-linear image.)
@@ -1028,7 +1049,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
         FR fr;
         fr.win = (const lds_u32*)wimg;
         fr.p = lane;
-        fr.sh = sh;
+        fr.sh = sh - SKIP;
         fr.avail = take;
         fr.len = len;
         fr.g = a.arena + off;
@@ -1538,12 +1559,14 @@ hipError_t launch_modify(const ModifyArgs& args, int layout_kind, int chain, con
 }
 
 // Flow mode needs the addresses (IPv6: 32 bytes past byte 22) and ports, so
-// its default window is 5 chunks; the same tuning knobs override it.
+// its default window is 5 chunks from the chunk holding byte 12 (SKIP in
+// k_parse: 392 -> 384 us per C5 flow_hist vs 5 chunks from the frame start;
+// 4 chunks from byte 12: 387); the same tuning knobs override the size.
 hipError_t launch_flows(const FlowArgs& a, int layout_kind, int chain, const Tuning& t,
                         hipStream_t s) {
     if (a.p.n == 0) return hipSuccess;
     // Each block builds the table once, so the grid is persistent: exactly the
-    // blocks the device holds at once (5 per CU at the default window: LDS),
+    // blocks the device holds at once (6 per CU at the default window: LDS),
     // each wave walking tiles.  Measured on C5 (parse+hash+histogram, us per
     // step): one tile per wave 546, 4 blocks per CU 434, 5 per CU 402, 6 / 8
     // per CU (a second partial round) 511 / 443.  A double-buffered variant
