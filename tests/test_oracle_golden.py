@@ -4,6 +4,9 @@ The reference (Rust) cannot be compiled or run in this image, so the parity
 oracle is a C restatement; these tests check it against every golden vector
 transcribed from ingot's tests and benches (tests/golden/kats.json).
 """
+import json
+from pathlib import Path
+
 import numpy as np
 import pytest
 
@@ -18,10 +21,12 @@ def test_golden_file_has_vectors(kats):
     assert kats["bitfield_kats"]
 
 
-@pytest.mark.parametrize("idx", range(40))
+_N_CHAIN_KATS = len(json.loads(
+    (Path(__file__).resolve().parent / "golden" / "kats.json").read_text())["chain_kats"])
+
+
+@pytest.mark.parametrize("idx", range(_N_CHAIN_KATS))
 def test_chain_kat(kats, idx):
-    if idx >= len(kats["chain_kats"]):
-        pytest.skip("fewer vectors")
     kat = kats["chain_kats"][idx]
     if Chain[kat["chain"]] == Chain.GeneveOverV6Tunnel:
         fld = oracle.parse_geneve(bytes.fromhex(kat["frame"]))
