@@ -74,15 +74,28 @@ CONFIGS = {
     "c3p": ("MIXED", 1 << 24, None, "GenericUlp",
             "C3 frames back to back with only a length array (capture-buffer layout): "
             "offsets scanned on the device, 16,777,216 per GPU, GenericUlp"),
+    "c2r": ("V4UDP64", 1 << 20, 64, "UdpParser",
+            "C2 frames as the reference's parse-read-v4 chunk chain (ingot-examples/benches/"
+            "packet.rs:130-134, 152-156): one chunk per header, 14 / 20 / 8 B + payload, "
+            "parse_read over chunk lists, 1,048,576 per GPU, UdpParser"),
 }
 # configs that time something other than the batched parse_slice records
-MODES = {"c5": "flows", "c2m": "modify", "c3r": "read", "c3p": "packed"}
+MODES = {"c5": "flows", "c2m": "modify", "c3r": "read", "c3p": "packed", "c2r": "read"}
+# parse_read chunking: "split2" = header span | payload; "per_header" = one
+# chunk per parsed header, then the payload (the reference bench's shape)
+READ_CHUNKS = {"c3r": "split2", "c2r": "per_header"}
+# Strong scaling (--scaling strong): the whole job's frames, split over the
+# ranks (BASELINE.json configs[3]: 64 M frames over 8 GPUs); other configs
+# split their single-GPU batch.
+STRONG_TOTAL = {"c4": 1 << 26, "c5": 1 << 26}
+# Arena copies rotated across steps are capped at this many bytes per GPU.
+ROTATE_CAP_BYTES = 64 << 30
 # Streams the steps alternate over, measured per config (tools/abtune.py,
 # DESIGN.md §5): short launches overlap their ramp-up/drain on 2 (C2 12.3 vs
 # 15.2 us, C2m 20.5 vs 25.0) or 3 (C3s 112.5 vs 115.1); long gather-bound
 # launches gain nothing (C3 606 / 618, C4 324 / 324, C6 392 / 393 us on 1 / 2).
 STREAMS = {"c2": 2, "c2m": 2, "c3": 1, "c3p": 1, "c3r": 2, "c3s": 3, "c4": 1, "c5": 2,
-           "c6": 1}
+           "c6": 1, "c2r": 2}
 FLOW_BINS = 1 << 16
 
 
@@ -118,9 +131,13 @@ def host_inclusive(config: str):
 
 def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode="parse",
                  segs=None):
-    """Time the oracle on the host cores over the same frames (bounded).
-    mode "read": parse_read over `segs` = (seg_off, seg_len, pkt_seg);
-    "modify": parse + the same setter in place on the sample."""
+    """Time the oracle (the C restatement of ingot's parse) on the host's
+    cores over the same frames, bounded: all os.cpu_count() threads (the
+    figure reported) and 1 thread.  Each worker repeats its contiguous share
+    of the sample `passes` times per call, so thread start-up (one pthread
+    per CPU per call) is amortised; a share is then cache-resident after the
+    first pass — generous to the CPU.  mode "read": parse_read over `segs` =
+    (seg_off, seg_len, pkt_seg); "modify": parse + the same setter in place."""
     import oracle
     from ingot_amd import EditOp, Field
 
@@ -133,7 +150,7 @@ def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode
         lib = oracle.load()
         arch = "x86-64-v3"
 
-    def one_pass(t):
+    def one_call(t):
         if mode == "read":
             oracle.parse_read_batch(arena_np, *segs, chain, lib=lib, nthreads=t)
         elif mode == "modify":
@@ -144,28 +161,41 @@ def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode
             oracle.parse_batch(arena_np, off_np, lens_np, chain, stride=stride, n=n,
                                nthreads=t, lib=lib)
 
-    threads = max(1, min(16, os.cpu_count() or 1))
+    host = os.cpu_count() or 1
     res = {}
-    for t in sorted({1, threads}):
-        one_pass(t)
-        reps, t0 = 0, time.perf_counter()
+    for t, budget in ((1, budget_s / 2), (host, budget_s)):
+        lib.oracle_set_passes(1)
+        one_call(t)  # warm (page faults, thread stacks)
+        t0 = time.perf_counter()
+        one_call(t)
+        once = max(time.perf_counter() - t0, 1e-6)
+        passes = max(1, min(10000, int(budget / 4 / once)))
+        lib.oracle_set_passes(passes)
+        calls, t0 = 0, time.perf_counter()
         while True:
-            one_pass(t)
-            reps += 1
+            one_call(t)
+            calls += 1
             el = time.perf_counter() - t0
-            if el > (budget_s if t > 1 else budget_s / 2):
+            if el > budget:
                 break
-        res[t] = (reps * n / el / 1e6, reps, el)
-    mp, reps, el = res[threads]
+        res[t] = (calls * passes * n / el / 1e6, calls * passes, el)
+    lib.oracle_set_passes(1)
+    mp, reps, el = res[host]
     what = {"parse": "parse_slice", "read": "parse_read", "modify": "parse + set_destination"}
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = host
     return {
-        "value": round(mp, 3), "unit": "Mpkt/s", "cores": threads, "kind": "port",
+        "value": round(mp, 3), "unit": "Mpkt/s", "cores": host, "kind": "port",
         "sample": f"{reps} passes x {n} frames of the benchmark batch (same bytes), "
-                  f"{el:.2f} s wall on {threads} threads; C restatement of ingot "
+                  f"{el:.2f} s wall on {host} threads (every host CPU; each thread repeats "
+                  f"its share, cache-resident after the first pass); C restatement of ingot "
                   f"{what.get(mode, mode)} (oracle/), -march={arch}",
         "single_core_value": round(res[1][0], 3),
         "cpu_model": _cpu_model(),
-        "host_cpus": os.cpu_count(),
+        "host_cpus": host,
+        "affinity_cpus": affinity,
     }
 
 
@@ -204,9 +234,9 @@ class Runner:
             self.launch = lambda k: fn(h, aptrs[k % reps], optr, lptr, n, c,
                                        outptrs[k % reps], sps[k % ns])
 
-    def run(self, steps):
-        """Time `steps` launches: fork all streams from streams[0], join back."""
-        return _timed(self.torch, self.streams, self.launch, steps)
+    def run(self, steps, gate=None):
+        """Time `steps` launches (see _timed)."""
+        return _timed(self.torch, self.streams, self.launch, steps, gate=gate)
 
 
 class PackedRunner:
@@ -228,8 +258,8 @@ class PackedRunner:
                                                            outptrs[k % reps], None,
                                                            wptrs[k % ns], wb, sps[k % ns])
 
-    def run(self, steps):
-        return _timed(self.torch, self.streams, self.launch, steps)
+    def run(self, steps, gate=None):
+        return _timed(self.torch, self.streams, self.launch, steps, gate=gate)
 
 
 class ModifyRunner:
@@ -253,8 +283,8 @@ class ModifyRunner:
                                                            stride or 0, n, c, eptr, 1, None,
                                                            sps[k % ns])
 
-    def run(self, steps):
-        return _timed(self.torch, self.streams, self.launch, steps)
+    def run(self, steps, gate=None):
+        return _timed(self.torch, self.streams, self.launch, steps, gate=gate)
 
 
 class ReadRunner:
@@ -272,8 +302,8 @@ class ReadRunner:
         self.launch = lambda k: lib.ingot_gpu_parse_read(h, aptrs[k % reps], so, sl, ps, n, c,
                                                          outptrs[k % reps], None, sps[k % ns])
 
-    def run(self, steps):
-        return _timed(self.torch, self.streams, self.launch, steps)
+    def run(self, steps, gate=None):
+        return _timed(self.torch, self.streams, self.launch, steps, gate=gate)
 
 
 class FlowRunner:
@@ -325,34 +355,239 @@ class FlowRunner:
 
         self.launch, self.finish = launch, finish
 
-    def run(self, steps):
-        return _timed(self.torch, self.streams, self.launch, steps, self.finish)
+    def run(self, steps, gate=None):
+        return _timed(self.torch, self.streams, self.launch, steps, self.finish, gate=gate)
 
 
-def _timed(torch, streams, launch, steps, finish=None):
-    """Run `steps` launches between two HIP events on streams[0]; the other
-    streams fork from the start event and join before the end event (as does
-    `finish`'s outstanding work)."""
+class Gate:
+    """Holds the first launches of a timed region behind a doorbell
+    (ingot_gpu_doorbell_wait on every stream), the way a ring consumer
+    enqueues its next batches before they arrive: the region then starts when
+    the GPU starts the first step, not when the host has finished submitting
+    it (ctypes + hipLaunchKernel + event records cost tens of us of host time
+    while the start event has already been stamped).  Every launch still runs
+    inside the region.  Only the first HOLD launches wait (a bounded number of
+    queued packets); a watchdog thread rings the doorbell after WATCHDOG_S
+    whatever happens, so a stream can never be left waiting."""
+
+    HOLD = 64
+    WATCHDOG_S = 20.0
+
+    def __init__(self, ingot_amd, ctx):
+        import threading
+
+        self.db = ingot_amd.Doorbell(ctx)
+        self.seq = 0
+        self._threading = threading
+
+    def arm(self, streams):
+        self.seq += 1
+        for s in streams:
+            self.db.wait(self.seq, s)
+        seq, db = self.seq, self.db
+        self._timer = self._threading.Timer(self.WATCHDOG_S, lambda: db.ring(seq))
+        self._timer.daemon = True
+        self._timer.start()
+
+    def open(self):
+        self.db.ring(self.seq)
+        self._timer.cancel()
+
+
+def _timed(torch, streams, launch, steps, finish=None, gate=None):
+    """Run `steps` launches; returns (ms, wall s).  Ungated: between a start
+    event on streams[0] (the other streams fork from it) and an end event
+    after every stream has joined back.  Gated: every stream waits on the
+    doorbell, then stamps its own start event; the region runs from the
+    earliest start to the end event."""
     s0 = streams[0]
-    e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     w0 = time.perf_counter()
-    e0.record(s0)
-    for s in streams[1:]:
-        s.wait_event(e0)
-    for k in range(steps):
-        rc = launch(k)
-        if rc:
-            raise RuntimeError(f"launch failed: {rc}")
-    if finish is not None:
-        finish()
-    for s in streams[1:]:
-        ev = torch.cuda.Event()
-        ev.record(s)
-        s0.wait_event(ev)
-    e1.record(s0)
+    if gate is not None:
+        gate.arm(streams)
+    starts = []
+    try:
+        if gate is not None:
+            for s in streams:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record(s)
+                starts.append(e)
+        else:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record(s0)
+            starts.append(e0)
+            for s in streams[1:]:
+                s.wait_event(e0)
+        for k in range(steps):
+            rc = launch(k)
+            if rc:
+                raise RuntimeError(f"launch failed: {rc}")
+            if gate is not None and k + 1 == Gate.HOLD:
+                gate.open()
+        if finish is not None:
+            finish()
+        for s in streams[1:]:
+            ev = torch.cuda.Event()
+            ev.record(s)
+            s0.wait_event(ev)
+        e1.record(s0)
+    finally:
+        if gate is not None:
+            gate.open()
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1), time.perf_counter() - w0
+    return max(e.elapsed_time(e1) for e in starts), time.perf_counter() - w0
+
+
+def kernel_sources_sha() -> str:
+    """Digest of every source the library's kernels are built from: a PMC
+    profile in profiles/ is attached to a bench line only when it was taken
+    on these exact sources (tools/pmc_traffic.py records the same digest)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    files = sorted((ROOT / "ingot_amd" / "csrc").glob("*")) + sorted((ROOT / "include").glob("*.h"))
+    for f in files:
+        if f.suffix in (".hip", ".h", ".cpp"):
+            h.update(f.name.encode())
+            h.update(f.read_bytes())
+    return h.hexdigest()[:16]
+
+
+def kernel_family(mode: str, ring: bool) -> str:
+    """The dominant kernel this config launches (parse.hip's dispatch)."""
+    if mode == "modify":
+        return "k_modify_pipe" if ring else "k_parse"
+    return "k_parse_pipe" if ring else "k_parse"
+
+
+def pmc_for(config: str, family: str, sha: str):
+    """The newest profiles/*_pmc_<config>.json taken on these kernel sources
+    whose profiled kernel is `family`; None (with the reason) otherwise."""
+    for f in sorted(ROOT.glob(f"profiles/*_pmc_{config}.json"), reverse=True):
+        t = json.loads(f.read_text())
+        k = t.get("kernel") or (t.get("kernels") or [""])[0]
+        if t.get("sources_sha") != sha:
+            continue
+        if f"::{family}<" not in k and not k.startswith(f"{family}<"):
+            continue
+        return t, f
+    return None, None
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list) -> int:
+    """`--gpus N` without a launcher: start N child processes of this script,
+    one per GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* as torchrun sets
+    them), before anything in this process touches a GPU.  Rank 0's JSON
+    line goes to the shared stdout.  If a rank fails, the others (exact PIDs
+    started here) are terminated; returns the first failing exit code."""
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + argv,
+                                      env=env))
+    rc, live = 0, list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r if r > 0 else 128 - r
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def frames_for_rank(config: str, scaling: str, rank: int, world: int):
+    """(first, n, total): this rank's contiguous share of the job's frames."""
+    from ingot_amd import dist as idist
+
+    n = CONFIGS[config][1]
+    if scaling == "strong":
+        total = STRONG_TOTAL.get(config, n)
+        first, cnt = idist.split(total, rank, world)
+        return first, cnt, total
+    first, cnt = idist.shard(rank, world, n)
+    return first, cnt, n * world
+
+
+def read_chunks(torch, off, stride, lens, recs_np, kind, dev):
+    """parse_read chunk tables for the read configs (all chunks inside the
+    packet's own bytes of the arena, mblk-style): "split2" = [header span |
+    payload], "per_header" = one chunk per parsed header, then the payload
+    (cuts at l3_off, l4_off, payload_off: no header straddles a cut, so the
+    records equal parse_slice's).  Returns (seg_off u64, seg_len u16,
+    pkt_seg u32 as int32, chunks covering the header span per packet)."""
+    n = len(recs_np)
+    L = lens.to(torch.int64)
+    poff = torch.from_numpy(recs_np["payload_off"].astype(np.int64)).to(dev)
+    if kind == "split2":
+        cuts = poff[:, None]
+    else:
+        cuts = torch.stack([torch.from_numpy(recs_np[k].astype(np.int64)).to(dev)
+                            for k in ("l3_off", "l4_off", "payload_off")], 1)
+    # keep a cut when it is past every earlier cut and inside the frame
+    prev = torch.zeros(n, dtype=torch.int64, device=dev)
+    keep = []
+    for k in range(cuts.shape[1]):
+        c = cuts[:, k]
+        m = (c > prev) & (c < L)
+        keep.append(m)
+        prev = torch.where(m, c, prev)
+    keep = torch.stack(keep, 1)
+    bounds = torch.cat([torch.zeros(n, 1, dtype=torch.int64, device=dev), cuts, L[:, None]], 1)
+    valid = torch.cat([torch.ones(n, 1, dtype=torch.bool, device=dev), keep], 1)
+    nchunks = valid.sum(1)
+    starts = bounds[:, :-1][valid]                        # row-major: packet by packet
+    # each chunk ends at the next kept boundary (or the frame end)
+    nxt = torch.full_like(bounds[:, :-1], -1)
+    run = L.clone()
+    for k in range(valid.shape[1] - 1, -1, -1):
+        nxt[:, k] = run
+        run = torch.where(valid[:, k], bounds[:, k], run)
+    ends = nxt[valid]
+    base = off if off is not None else torch.arange(n, dtype=torch.int64, device=dev) * stride
+    seg_off = (base.repeat_interleave(nchunks) + starts).contiguous()
+    seg_len = (ends - starts).to(torch.int32).to(torch.uint16).contiguous()
+    pkt_seg = torch.zeros(n + 1, dtype=torch.int32, device=dev)
+    pkt_seg[1:] = nchunks.cumsum(0).to(torch.int32)
+    # chunks covering [0, payload_off): every kept chunk that starts below it
+    head = ((bounds[:, :-1] < poff[:, None]) & valid).sum(1)
+    return seg_off, seg_len, pkt_seg, head
+
+
+def plan(args, world, rank):
+    """--plan: the distributed plumbing without a GPU (gloo): every rank
+    computes its share, rank 0 gathers them and prints one JSON line."""
+    import torch.distributed as dist
+
+    first, n, total = frames_for_rank(args.config, args.scaling, rank, world)
+    shards = [(first, n)]
+    if world > 1:
+        dist.init_process_group("gloo")
+        shards = [None] * world
+        dist.all_gather_object(shards, (first, n))
+    if rank == 0:
+        print(json.dumps({"plan": True, "n_gpus": world, "scaling": args.scaling,
+                          "config": args.config, "total_frames": total,
+                          "shards": [list(s) for s in shards]}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def main():
@@ -361,11 +596,18 @@ def main():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
+                    help="weak: every rank parses a full batch; strong: the job's frames "
+                         "(STRONG_TOTAL, e.g. 64 M for c4) are split over the ranks")
     ap.add_argument("--streams", type=int, default=0,
                     help="streams the steps alternate over (0 = the config's measured best)")
     ap.add_argument("--record", type=int, default=16, choices=(16, 8))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true")
+    ap.add_argument("--no-gate", action="store_true",
+                    help="time from host submission (no doorbell-held first launches)")
+    ap.add_argument("--plan", action="store_true",
+                    help="print the ranks' shares and exit without touching a GPU")
     ap.add_argument("--cpu-budget", type=float, default=1.5)
     ap.add_argument("--rotate-mib", type=int, default=512,
                     help="minimum bytes of distinct arenas rotated across steps")
@@ -374,6 +616,26 @@ def main():
     args = ap.parse_args()
     if args.streams <= 0:
         args.streams = STREAMS.get(args.config, 2)
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+
+    # --- one process per GPU: under a launcher (WORLD_SIZE set) its world
+    # must be --gpus; without one, start the ranks here (nothing has touched
+    # a GPU yet in this process) ---
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+        world, rank, local = 1, 0, 0
+    else:
+        world = int(os.environ["WORLD_SIZE"])
+        rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if world != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+            sys.exit(2)
+    if args.plan:
+        plan(args, world, rank)
+        return
 
     import torch
     import torch.distributed as dist
@@ -383,9 +645,6 @@ def main():
 
     from ingot_amd import dist as idist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # one GPU per rank; a --dist-backend gloo rehearsal may fold ranks onto
     # fewer GPUs (e.g. the 1-GPU test box)
     local = local % max(1, torch.cuda.device_count())
@@ -398,41 +657,49 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
-    prof_name, n, stride, chain_name, desc = CONFIGS[args.config]
+    prof_name, _, stride, chain_name, desc = CONFIGS[args.config]
     profile, chain = GenProfile[prof_name], Chain[chain_name]
     ctx = ingot_amd.Context(local)
     lib = ingot_amd.load_library()
+    mode = MODES.get(args.config, "parse")
+    flows = mode == "flows"
 
-    # --- data: this rank's shard (pure in (seed, index)) + R copies ---
-    first, n = idist.shard(rank, world, n)
+    # --- data: this rank's share (pure in (seed, index)) + R copies ---
+    first, n, n_total = frames_for_rank(args.config, args.scaling, rank, world)
     arena, off, lens = ingot_amd.gen_frames(profile, n, first=first, stride=stride,
                                             device=local)
+    if flows:
+        args.no_variants = True
     # >= 512 MiB of distinct arenas (the 256 MiB MALL cannot serve a step from
-    # the previous one), and >= 4 copies so that launches in flight on up to 4
-    # streams never read the same bytes (no cross-step cache sharing)
-    reps = max(4, -(-(args.rotate_mib << 20) // arena.numel()))
+    # the previous one), and a copy per stream in flight (launches running
+    # together never read the same bytes) — up to ROTATE_CAP_BYTES; above it
+    # (a 50 GB strong-scaling arena is far past every cache) one copy, and
+    # only single-stream variants
+    need = max(1, -(-(args.rotate_mib << 20) // arena.numel()))
+    reps = max(need, args.streams, 1 if args.no_variants else 4)
+    multi_stream_variants = True
+    if arena.numel() * reps > ROTATE_CAP_BYTES:
+        reps = max(need, args.streams)
+        multi_stream_variants = False
     arenas = [arena] + [arena.clone() for _ in range(reps - 1)]
     outs = [torch.empty((n, 16), dtype=torch.uint8, device=dev) for _ in range(reps)]
     torch.cuda.synchronize(dev)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
                                                   for _ in range(max(3, args.streams - 1))]
 
-    mode = MODES.get(args.config, "parse")
-    flows = mode == "flows"
     if flows:
         hists = [torch.zeros(FLOW_BINS, dtype=torch.int32, device=dev) for _ in range(reps)]
         flow_ids = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(reps)]
+    recs0 = None
     if mode == "read":
-        # mblk-style packets: chunk 0 = the header span (payload_off of a
-        # parse_slice pass), chunk 1 = the payload; both in the same arena
-        poff = ingot_amd.records_to_numpy(ctx.parse(arena, off, lens, chain))["payload_off"]
-        poff = torch.from_numpy(poff.astype(np.int64)).to(dev)
-        len64 = lens.to(torch.int64)
-        seg_off = torch.stack([off, off + poff], 1).reshape(-1).contiguous()
-        seg_len = torch.stack([poff, len64 - poff], 1).reshape(-1).to(torch.int32) \
-            .to(torch.uint16).contiguous()
-        pkt_seg = torch.arange(0, 2 * n + 1, 2, dtype=torch.int32, device=dev)
-        del poff, len64
+        # mblk-style packets over the same frames (chunks inside each frame)
+        recs0 = ingot_amd.records_to_numpy(
+            ctx.parse_strided(arena, stride, n, chain) if stride is not None else
+            ctx.parse(arena, off, lens, chain))
+        rlens = lens if lens is not None else torch.full((n,), stride, dtype=torch.int32,
+                                                         device=dev).to(torch.uint16)
+        seg_off, seg_len, pkt_seg, head_chunks = read_chunks(
+            torch, off, stride, rlens.to(torch.int32), recs0, READ_CHUNKS[args.config], dev)
 
     def runner(nstreams, record):
         if flows:
@@ -450,25 +717,41 @@ def main():
         return Runner(torch, lib, ctx, chain, n, stride, arenas, off, lens, outs,
                       streams[:nstreams], record)
 
-    if flows:
-        args.no_variants = True
     if mode in ("modify", "read", "packed") and args.record == 8:
         ap.error("8-B records are not offered for this config")
     if chain == Chain.GeneveOverV6Tunnel and args.record == 8:
         ap.error("8-B records are not offered for the tunnel chain (include/ingot_gpu.h)")
+    # the doorbell gate needs every launch of the region to be asynchronous:
+    # the gloo rehearsal's histogram reduce copies through the host
+    gate = None
+    gate_note = "off (--no-gate)"
+    if not args.no_gate and not (flows and world > 1 and args.dist_backend == "gloo"):
+        try:
+            gate = Gate(ingot_amd, ctx)
+            gate_note = (f"first {Gate.HOLD} launches held behind a doorbell "
+                         "(ingot_gpu_doorbell_wait); region from the first step's start")
+        except RuntimeError as e:
+            gate_note = f"unavailable ({e}); region from host submission"
     main_run = runner(args.streams, args.record)
-    main_run.run(args.warmup)
+    main_run.run(args.warmup, gate)
 
     # --- timed region: K steps, barrier + sync on both sides ---
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    ms_region, wall = main_run.run(args.steps)
+    ms_region, wall = main_run.run(args.steps, gate)
+    torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t_sec = idist.max_over_ranks(ms_region / 1e3, device=dev)
-    value = n * args.steps * world / t_sec / 1e6
+    # every rank's frames: weak = n per rank; strong = the job's total
+    frames_all = n_total
+    value = frames_all * args.steps / t_sec / 1e6
     ms_step = t_sec * 1e3 / args.steps
+    ungated = None
+    if gate is not None:  # the same region timed from host submission, for reference
+        ms_u, _ = main_run.run(args.steps)
+        ungated = round(idist.max_over_ranks(ms_u / 1e3, device=dev) * 1e3 / args.steps, 5)
 
     # --- algorithmic bytes from this batch's records (16-B form) ---
     recs = ctx.parse_strided(arenas[0], stride, n, chain, lens=lens) \
@@ -477,9 +760,10 @@ def main():
     recs_np = ingot_amd.records_to_numpy(recs)
     lens_np = lens.cpu().numpy() if lens is not None else None
     if mode == "read":
-        # chunk 0 read like a frame of the header span's length; descriptors:
-        # pkt_seg (4 B) + chunk 0's (u64 off, u16 len) = 14 B
-        rd, wr = algorithmic_bytes(recs_np, recs_np["payload_off"], 0, 14, 16)
+        # the header chunks read like a frame of the header span's length;
+        # descriptors: pkt_seg (4 B) + (u64 off, u16 len) per header chunk
+        hc = head_chunks.cpu().numpy().astype(np.int64)
+        rd, wr = algorithmic_bytes(recs_np, recs_np["payload_off"], 0, 4 + 10 * hc, 16)
     elif mode == "packed":
         # descriptors: the u16 length, read by the parse and once more by the
         # tile-sum pass; tile sums and bases: 12 B per 64 packets
@@ -494,7 +778,7 @@ def main():
     if mode == "modify":  # no records; the 2 rewritten bytes per packet
         wr = 2 * n
     bytes_launch = rd + wr
-    pipelined_gbs = bytes_launch / (ms_region / args.steps / 1e3) / 1e9
+    pipelined_gbs = bytes_launch / (ms_step / 1e3) / 1e9
     # Roofline of the kernel itself: a single-stream pass (launches back to
     # back, so region/K = one launch incl. the dependent-launch boundary; this
     # is what rocprofv3's per-dispatch mean measures).  In the pipelined
@@ -502,22 +786,24 @@ def main():
     iso = runner(1, args.record)
     iso.run(min(args.warmup, 50))
     iso_steps = min(args.steps, 1000)
-    ms_iso, _ = iso.run(iso_steps)
+    ms_iso, _ = iso.run(iso_steps, gate)
     launch_ms = ms_iso / iso_steps
     achieved = bytes_launch / (launch_ms / 1e3) / 1e9
     ok_frac = float((recs_np["status"] == 0).mean())
-    # the multi-tile ring kernel serves slot rings without a length array
-    # (launch_parse in parse.hip); everything else is the one-tile k_parse
-    ring = (mode == "parse" and stride is not None and stride >= 64 and lens is None
-            and chain != Chain.GeneveOverV6Tunnel)
+    # the multi-tile ring kernels serve slot rings without a length array
+    # (launch_parse / launch_modify in parse.hip); everything else is k_parse
+    ring = (mode in ("parse", "modify") and stride is not None and stride >= 64
+            and lens is None and chain != Chain.GeneveOverV6Tunnel)
+    family = kernel_family(mode, ring)
+    sha = kernel_sources_sha()
     traffic = None
-    pmc = sorted(ROOT.glob(f"profiles/*_pmc_{args.config}.json"))
-    if pmc and args.record == 16:
-        t = json.loads(pmc[-1].read_text())
+    t, pf = pmc_for(args.config, family, sha) if args.record == 16 else (None, None)
+    if t is not None:
         traffic = {"bytes_per_launch": t["traffic_bytes_per_launch"],
                    "ratio_to_algorithmic": round(t["traffic_bytes_per_launch"] / bytes_launch, 4),
-                   "source": f"{pmc[-1].relative_to(ROOT)} (rocprofv3 --pmc FETCH_SIZE x2 + "
-                             "WRITE_SIZE, separate passes)"}
+                   "source": f"{pf.relative_to(ROOT)} (rocprofv3 --pmc FETCH_SIZE x2 + "
+                             "WRITE_SIZE, separate passes, same kernel sources)",
+                   "kernel": t.get("kernel")}
 
     # --- variants (outside the timed region; same data) ---
     variants = {}
@@ -526,11 +812,13 @@ def main():
         for ns, rb in ((1, 16), (2, 8), (1, 8), (4, 16)):
             if (ns, rb) == (args.streams, args.record):
                 continue
+            if ns > 1 and not multi_stream_variants:
+                continue
             if rb == 8 and (chain == Chain.GeneveOverV6Tunnel or mode != "parse"):
                 continue
             r = runner(ns, rb)
             r.run(min(args.warmup, 50))
-            ms, _ = r.run(vsteps)
+            ms, _ = r.run(vsteps, gate)
             bpl = rd + (rb * n if mode != "modify" else wr)
             variants[f"streams{ns}_rec{rb}"] = {
                 "value": round(n * vsteps / (ms / 1e3) / 1e6, 2),
@@ -551,11 +839,16 @@ def main():
             l_np = lens_np[:m] if lens_np is not None else None
             segs = None
             if mode == "read":
-                segs = (seg_off[:2 * m].cpu().numpy().view(np.uint64),
-                        seg_len[:2 * m].to(torch.int32).cpu().numpy().astype(np.uint16),
-                        pkt_seg[:m + 1].cpu().numpy().view(np.uint32))
+                ps = pkt_seg[:m + 1].cpu().numpy().view(np.uint32)
+                ns_ = int(ps[-1])
+                segs = (seg_off[:ns_].cpu().numpy().view(np.uint64),
+                        seg_len[:ns_].to(torch.int32).cpu().numpy().astype(np.uint16), ps)
             cpu = cpu_baseline(a_np, o_np, l_np, stride or 0, m, chain, args.cpu_budget,
                                mode="parse" if flows else mode, segs=segs)
+        kname = {"modify": ", parse + setters",
+                 "read": ", LAYOUT_SEGMENTED (parse_read)",
+                 "packed": ", LAYOUT_PACKED + k_tile_sums/k_group_scan",
+                 "flows": ", OUT_FLOWS + k_flow_count16/k_flow_reduce16"}.get(mode, "")
         result = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -565,22 +858,25 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 5),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (device-generated, seed 20250808)",
             "config": {
                 "workload": desc,
                 "frames_per_gpu": n,
+                "frames_total": n_total,
                 "chain": chain_name,
                 "layout": f"strided {stride} B" if stride else "packed, u64 offsets + u16 lengths",
                 "record_bytes": args.record,
                 "streams": args.streams,
                 "arena_copies_rotated": reps,
-                "parallelism": (f"shard per GPU x{world}; RCCL all-reduce (sum) of the "
-                                f"{FLOW_BINS} x u32 flow histogram every step" if flows else
-                                f"shard per GPU x{world} (no data-path collective)"),
+                "parallelism": (f"{args.scaling} scaling, contiguous share per GPU x{world}" +
+                                (f"; RCCL all-reduce (sum) of the {FLOW_BINS} x u32 flow "
+                                 "histogram every step" if flows else
+                                 " (no data-path collective)")),
                 "ok_fraction": round(ok_frac, 6),
+                "timing": gate_note,
             },
             "roofline": {
                 "bound": "hbm",
@@ -590,20 +886,21 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic["bytes_per_launch"] if traffic else None,
                 "traffic_detail": traffic,
-                "kernel": ("k_parse_pipe" if ring else "k_parse") + " (ingot_amd/csrc/parse.hip)" + {
-                    "modify": ", OUT_MODIFY", "read": ", LAYOUT_SEGMENTED",
-                    "packed": ", LAYOUT_PACKED + k_tile_sums/k_tile_scan",
-                    "flows": ", OUT_FLOWS + k_flow_count16/k_flow_reduce16"}.get(mode, ""),
+                "kernel": (traffic or {}).get("kernel") or
+                          f"{family} (ingot_amd/csrc/parse.hip){kname}",
+                "kernel_sources_sha": sha,
                 "launch_mean_us": round(launch_ms * 1e3, 3),
                 "launch_timing": "single-stream pass, HIP events, region/K",
                 "pipelined_GBps": round(pipelined_gbs, 1),
                 "pipelined_frac": round(pipelined_gbs / HBM_PEAK_GBS, 4),
+                "pipelined_read_frac": round(rd / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                 "algorithmic_bytes_per_launch": bytes_launch,
                 "read_bytes_per_launch": rd,
                 "write_bytes_per_launch": wr,
                 "read_frac": round(rd / (launch_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                 "frac_of_measured_copy_ceiling": round(achieved / HBM_MEASURED_GBS, 4),
             },
+            "ms_per_step_ungated": ungated,
             "variants": variants,
             "cpu_baseline": cpu,
             "wall_s_timed_region": round(wall, 4),

@@ -358,6 +358,29 @@ int ingot_gpu_host_map(ingot_gpu_ctx* ctx, void* host, size_t bytes, void** d_pt
 int ingot_gpu_host_unmap(ingot_gpu_ctx* ctx, void* host);
 
 /*
+ * Doorbells.  A ring consumer that knows its next batches in advance (a NIC
+ * or loopback ring: slot k of the ring is batch k) can enqueue their parse
+ * launches before the frames arrive, each behind a doorbell wait; the
+ * producer publishes batch k by writing k (or more) into the doorbell from
+ * the host, and the GPU starts the queued launch with no host round trip
+ * (no launch latency on the critical path).  The doorbell is one 32-bit word
+ * of pinned host memory polled by the GPU's command processor
+ * (hipStreamWaitValue32, compare >=).  *host_word may be written directly by
+ * the producer (e.g. another thread) or through ingot_gpu_doorbell_ring.
+ *   ingot_gpu_doorbell_wait: everything enqueued on `stream` after this call
+ *     runs only once *doorbell >= value.  The caller must make sure the
+ *     doorbell is eventually rung: a stream left waiting never drains.
+ *   ingot_gpu_doorbell_destroy: only after every wait on it has been passed.
+ * ENODEV when the device cannot wait on memory values.
+ */
+typedef struct ingot_gpu_doorbell ingot_gpu_doorbell;
+int ingot_gpu_doorbell_create(ingot_gpu_ctx* ctx, ingot_gpu_doorbell** out,
+                              volatile uint32_t** host_word);
+int ingot_gpu_doorbell_wait(ingot_gpu_doorbell* db, uint32_t value, void* stream);
+int ingot_gpu_doorbell_ring(ingot_gpu_doorbell* db, uint32_t value);
+void ingot_gpu_doorbell_destroy(ingot_gpu_doorbell* db);
+
+/*
  * Tuning knobs (results never depend on them).  Defaults are the measured
  * best on MI355X; value 0 restores the default.
  *   INGOT_TUNE_WINDOW_INDEXED  16-B chunks staged in LDS per packed frame:

@@ -74,11 +74,20 @@ def _ptr(t) -> Optional[int]:
     return None if t is None else t.data_ptr()
 
 
-def _stream(stream) -> Optional[int]:
+def _stream(stream, device: Optional[int] = None) -> Optional[int]:
+    """hipStream_t of `stream`; None = torch's current stream on `device`."""
     torch = _torch()
     if stream is None:
-        stream = torch.cuda.current_stream()
+        stream = torch.cuda.current_stream(device)
     return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+
+
+# dtype names accepted for each C type of the ABI (16- and 32-bit tables may
+# arrive as the signed view of the same bits)
+_U8 = ("uint8",)
+_U64 = ("int64", "uint64")
+_U16 = ("uint16", "int16")
+_U32 = ("int32", "uint32")
 
 
 class PacketParseError(Exception):
@@ -136,10 +145,16 @@ class Context:
         wb = int(self._lib.ingot_gpu_packed_workspace_size(n))
         if workspace is None:
             workspace = torch.empty(wb, dtype=torch.uint8, device=arena.device)
-        self._check_dev(arena, lens, out, off_out, workspace)
+        self._arg("arena", arena, _U8)
+        self._arg("lens", lens, _U16, n)
+        self._arg("out", out, _U8, n * REC_BYTES)
+        self._arg("off_out", off_out, _U64, n, optional=True)
+        self._arg("workspace", workspace, _U8, wb)
+        self._on_device(arena=arena, lens=lens, out=out, off_out=off_out, workspace=workspace)
         _lib.check(self._lib.ingot_gpu_parse_packed(
             self._h, _ptr(arena), _ptr(lens), n, int(chain), _ptr(out), _ptr(off_out),
-            _ptr(workspace), workspace.numel(), _stream(stream)), "ingot_gpu_parse_packed")
+            _ptr(workspace), workspace.numel(), _stream(stream, self.device)),
+            "ingot_gpu_parse_packed")
         return out
 
     def parse_header(self, arena, off, lens, kind, hint=None, hints=None, stride: int = 0,
@@ -153,11 +168,14 @@ class Context:
             n = off.numel()
         if out is None:
             out = torch.empty((n, HDR_DTYPE.itemsize), dtype=torch.uint8, device=arena.device)
-        self._check_dev(arena, off, lens, hints, out)
+        self._frames(arena, off, lens, stride, n, align16=False)
+        self._arg("hints", hints, _U32, n, optional=True)
+        self._arg("out", out, _U8, n * HDR_DTYPE.itemsize)
         h = HINT_NONE if hint is None else int(hint)
+        self._on_device(arena=arena, off=off, lens=lens, hints=hints, out=out)
         _lib.check(self._lib.ingot_gpu_parse_header(self._h, _ptr(arena), _ptr(off), _ptr(lens),
                                                     int(stride), n, int(kind), _ptr(hints), h,
-                                                    _ptr(out), _stream(stream)),
+                                                    _ptr(out), _stream(stream, self.device)),
                    "ingot_gpu_parse_header")
         return out
 
@@ -179,10 +197,45 @@ class Context:
         ptr = host.data_ptr() if hasattr(host, "data_ptr") else host.ctypes.data
         _lib.check(self._lib.ingot_gpu_host_unmap(self._h, ptr), "ingot_gpu_host_unmap")
 
-    def _check_dev(self, *tensors) -> None:
-        for t in tensors:
+    def _arg(self, name: str, t, dtypes, numel: Optional[int] = None,
+             optional: bool = False) -> None:
+        """Validate one buffer before its raw pointer crosses the C ABI: the
+        kernels trust dtype (element size), contiguity and extent, so a
+        mismatch here would be an out-of-bounds access on the device."""
+        if t is None:
+            if optional:
+                return
+            raise ValueError(f"{name} is required")
+        if not hasattr(t, "data_ptr") or not hasattr(t, "dtype"):
+            raise TypeError(f"{name} must be a tensor")
+        dt = str(t.dtype).replace("torch.", "")
+        if dt not in dtypes:
+            raise ValueError(f"{name} must be {' or '.join(dtypes)}, not {dt}")
+        if not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+        if numel is not None and t.numel() < numel:
+            raise ValueError(f"{name} holds {t.numel()} elements, needs at least {numel}")
+
+    def _on_device(self, **tensors) -> None:
+        """After the shape checks: every buffer lives on the context's device."""
+        for name, t in tensors.items():
             if t is not None and (not t.is_cuda or t.device.index != self.device):
-                raise ValueError("tensors must live on the context's device")
+                raise ValueError(f"{name} must live on cuda:{self.device}")
+
+    def _frames(self, arena, off, lens, stride: int, n: int, align16: bool = True) -> None:
+        """The frame descriptors of an indexed (off/lens) or slot (stride)
+        arena: dtypes, counts and, for slots, that n slots fit the arena."""
+        self._arg("arena", arena, _U8)
+        if off is not None:
+            self._arg("off", off, _U64, n)
+            self._arg("lens", lens, _U16, n)
+        else:
+            if stride <= 0 or (align16 and stride % 16):
+                raise ValueError("stride must be a positive multiple of 16"
+                                 if align16 else "stride must be positive")
+            if n * stride > arena.numel():
+                raise ValueError(f"{n} slots of {stride} B exceed the {arena.numel()}-B arena")
+            self._arg("lens", lens, _U16, n, optional=True)
 
     def parse(self, arena, off, lens, chain: Chain, out=None, stream=None):
         """Batched `<chain>::parse_slice` over frames (off[i], lens[i]) of arena.
@@ -196,9 +249,11 @@ class Context:
             raise ValueError("off and lens must have the same length")
         if out is None:
             out = torch.empty((n, REC_BYTES), dtype=torch.uint8, device=arena.device)
-        self._check_dev(arena, off, lens, out)
+        self._frames(arena, off, lens, 0, n)
+        self._arg("out", out, _U8, n * REC_BYTES)
+        self._on_device(arena=arena, off=off, lens=lens, out=out)
         _lib.check(self._lib.ingot_gpu_parse(self._h, _ptr(arena), _ptr(off), _ptr(lens), n,
-                                             int(chain), _ptr(out), _stream(stream)),
+                                             int(chain), _ptr(out), _stream(stream, self.device)),
                    "ingot_gpu_parse")
         return out
 
@@ -207,10 +262,12 @@ class Context:
         torch = _torch()
         if out is None:
             out = torch.empty((n, REC_BYTES), dtype=torch.uint8, device=arena.device)
-        self._check_dev(arena, lens, out)
+        self._frames(arena, None, lens, stride, n)
+        self._arg("out", out, _U8, n * REC_BYTES)
+        self._on_device(arena=arena, lens=lens, out=out)
         _lib.check(self._lib.ingot_gpu_parse_strided(self._h, _ptr(arena), int(stride),
                                                      _ptr(lens), n, int(chain), _ptr(out),
-                                                     _stream(stream)),
+                                                     _stream(stream, self.device)),
                    "ingot_gpu_parse_strided")
         return out
 
@@ -220,9 +277,12 @@ class Context:
         n = off.numel()
         if out is None:
             out = torch.empty((n, REC8_BYTES), dtype=torch.uint8, device=arena.device)
-        self._check_dev(arena, off, lens, out)
+        self._frames(arena, off, lens, 0, n)
+        self._arg("out", out, _U8, n * REC8_BYTES)
+        self._on_device(arena=arena, off=off, lens=lens, out=out)
         _lib.check(self._lib.ingot_gpu_parse_compact(self._h, _ptr(arena), _ptr(off), _ptr(lens),
-                                                     n, int(chain), _ptr(out), _stream(stream)),
+                                                     n, int(chain), _ptr(out),
+                                                     _stream(stream, self.device)),
                    "ingot_gpu_parse_compact")
         return out
 
@@ -231,10 +291,12 @@ class Context:
         torch = _torch()
         if out is None:
             out = torch.empty((n, REC8_BYTES), dtype=torch.uint8, device=arena.device)
-        self._check_dev(arena, lens, out)
+        self._frames(arena, None, lens, stride, n)
+        self._arg("out", out, _U8, n * REC8_BYTES)
+        self._on_device(arena=arena, lens=lens, out=out)
         _lib.check(self._lib.ingot_gpu_parse_strided_compact(
             self._h, _ptr(arena), int(stride), _ptr(lens), n, int(chain), _ptr(out),
-            _stream(stream)), "ingot_gpu_parse_strided_compact")
+            _stream(stream, self.device)), "ingot_gpu_parse_strided_compact")
         return out
 
     def fields(self, arena, off, lens, chain: Chain, stride: int = 0, n: Optional[int] = None,
@@ -245,10 +307,12 @@ class Context:
             n = off.numel()
         if out is None:
             out = torch.empty((n, FIELDS_BYTES), dtype=torch.uint8, device=arena.device)
-        self._check_dev(arena, off, lens, out)
+        self._frames(arena, off, lens, stride, n)
+        self._arg("out", out, _U8, n * FIELDS_BYTES)
+        self._on_device(arena=arena, off=off, lens=lens, out=out)
         _lib.check(self._lib.ingot_gpu_fields(self._h, _ptr(arena), _ptr(off), _ptr(lens),
                                               int(stride), n, int(chain), _ptr(out),
-                                              _stream(stream)),
+                                              _stream(stream, self.device)),
                    "ingot_gpu_fields")
         return out
 
@@ -262,9 +326,12 @@ class Context:
         if out is None:
             out = torch.empty((n, GENEVE_FIELDS_DTYPE.itemsize), dtype=torch.uint8,
                               device=arena.device)
-        self._check_dev(arena, off, lens, out)
+        self._frames(arena, off, lens, stride, n)
+        self._arg("out", out, _U8, n * GENEVE_FIELDS_DTYPE.itemsize)
+        self._on_device(arena=arena, off=off, lens=lens, out=out)
         _lib.check(self._lib.ingot_gpu_geneve_fields(self._h, _ptr(arena), _ptr(off), _ptr(lens),
-                                                     int(stride), n, _ptr(out), _stream(stream)),
+                                                     int(stride), n, _ptr(out),
+                                                     _stream(stream, self.device)),
                    "ingot_gpu_geneve_fields")
         return out
 
@@ -284,17 +351,22 @@ class Context:
             out = torch.empty((n, width), dtype=torch.uint8, device=arena.device)
         if chunk is None:
             chunk = torch.empty(n, dtype=torch.int16, device=arena.device)
-        self._check_dev(arena, seg_off, seg_len, pkt_seg, out, chunk)
+        self._arg("arena", arena, _U8)
+        self._arg("pkt_seg", pkt_seg, _U32, n + 1)
+        self._arg("seg_off", seg_off, _U64)
+        self._arg("seg_len", seg_len, _U16, seg_off.numel())
+        self._arg("out", out, _U8, n * width)
+        self._arg("chunk", chunk, _U16, n)
+        self._on_device(arena=arena, seg_off=seg_off, seg_len=seg_len, pkt_seg=pkt_seg, out=out,
+                        chunk=chunk)
+        st = _stream(stream, self.device)
         args = (self._h, _ptr(arena), _ptr(seg_off), _ptr(seg_len), _ptr(pkt_seg), n)
         if fields is None:
-            rc = self._lib.ingot_gpu_parse_read(*args, int(chain), _ptr(out), _ptr(chunk),
-                                                _stream(stream))
+            rc = self._lib.ingot_gpu_parse_read(*args, int(chain), _ptr(out), _ptr(chunk), st)
         elif fields == "fields":
-            rc = self._lib.ingot_gpu_fields_read(*args, int(chain), _ptr(out), _ptr(chunk),
-                                                 _stream(stream))
+            rc = self._lib.ingot_gpu_fields_read(*args, int(chain), _ptr(out), _ptr(chunk), st)
         else:
-            rc = self._lib.ingot_gpu_geneve_fields_read(*args, _ptr(out), _ptr(chunk),
-                                                        _stream(stream))
+            rc = self._lib.ingot_gpu_geneve_fields_read(*args, _ptr(out), _ptr(chunk), st)
         _lib.check(rc, "ingot_gpu_parse_read")
         return out, chunk
 
@@ -306,11 +378,13 @@ class Context:
         (an (n, 16) uint8 tensor) is given, else None."""
         if n is None:
             n = off.numel()
-        self._check_dev(arena, off, lens, out)
+        self._frames(arena, off, lens, stride, n)
+        self._arg("out", out, _U8, n * REC_BYTES, optional=True)
         e = edits_array(edits)
+        self._on_device(arena=arena, off=off, lens=lens, out=out)
         _lib.check(self._lib.ingot_gpu_parse_modify(
             self._h, _ptr(arena), _ptr(off), _ptr(lens), int(stride), n, int(chain),
-            e.ctypes.data_as(ctypes.c_void_p), len(e), _ptr(out), _stream(stream)),
+            e.ctypes.data_as(ctypes.c_void_p), len(e), _ptr(out), _stream(stream, self.device)),
             "ingot_gpu_parse_modify")
         return out
 
@@ -331,15 +405,22 @@ class Context:
             bins = hist.numel() if hist is not None else 65536
         if flow is None:
             flow = torch.empty(n, dtype=torch.int32, device=arena.device)
-        self._check_dev(arena, off, lens, hist, hashes, flow)
+        self._frames(arena, off, lens, stride, n)
+        self._arg("flow", flow, _U32, n)
+        self._arg("hashes", hashes, _U32, n, optional=True)
+        self._arg("hist", hist, _U32, bins, optional=True)
+        if key is not None and len(bytes(key)) != 40:
+            raise ValueError("key must be 40 bytes (the RSS key length)")
         kbuf = None if key is None else ctypes.create_string_buffer(bytes(key), 40)
         wbytes = 0 if workspace is None else workspace.numel() * workspace.element_size()
         if workspace is not None:
-            self._check_dev(workspace)
+            self._arg("workspace", workspace, _U8)
+        self._on_device(arena=arena, off=off, lens=lens, flow=flow, hashes=hashes, hist=hist, workspace=workspace)
         _lib.check(self._lib.ingot_gpu_flow_hist_ws(
             self._h, _ptr(arena), _ptr(off), _ptr(lens), int(stride), n, int(chain),
             ctypes.cast(kbuf, ctypes.c_void_p) if kbuf is not None else None, int(bins),
-            _ptr(flow), _ptr(hashes), _ptr(hist), _ptr(workspace), wbytes, _stream(stream)),
+            _ptr(flow), _ptr(hashes), _ptr(hist), _ptr(workspace), wbytes,
+            _stream(stream, self.device)),
             "ingot_gpu_flow_hist_ws")
         return flow
 
@@ -353,6 +434,34 @@ class Context:
         if not b:
             return None
         return _torch().empty(b, dtype=_torch().uint8, device=f"cuda:{self.device}")
+
+
+class Doorbell:
+    """ingot_gpu_doorbell: launches enqueued after `wait(value, stream)` run
+    once the doorbell word reaches `value` (rung from the host by `ring`)."""
+
+    def __init__(self, ctx: Context):
+        self._lib = _lib.load()
+        h, word = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.check(self._lib.ingot_gpu_doorbell_create(ctx._h, ctypes.byref(h),
+                                                       ctypes.byref(word)),
+                   "ingot_gpu_doorbell_create")
+        self._h = h
+        self.device = ctx.device
+
+    def wait(self, value: int, stream=None) -> None:
+        _lib.check(self._lib.ingot_gpu_doorbell_wait(self._h, int(value),
+                                                     _stream(stream, self.device)),
+                   "ingot_gpu_doorbell_wait")
+
+    def ring(self, value: int) -> None:
+        _lib.check(self._lib.ingot_gpu_doorbell_ring(self._h, int(value)),
+                   "ingot_gpu_doorbell_ring")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.ingot_gpu_doorbell_destroy(self._h)
+            self._h = None
 
 
 def records_to_numpy(t):
@@ -385,7 +494,7 @@ def gen_lengths(profile: GenProfile, n: int, seed: int = GEN_SEED, first: int = 
     torch = _torch()
     lens = torch.empty(n, dtype=torch.uint16, device=f"cuda:{device}")
     _lib.check(_lib.load().ingot_pktgen_lengths(int(profile), seed, first, n, _ptr(lens),
-                                                _stream(stream)), "ingot_pktgen_lengths")
+                                                _stream(stream, device)), "ingot_pktgen_lengths")
     return lens
 
 
@@ -410,7 +519,8 @@ def gen_frames(profile: GenProfile, n: int, seed: int = GEN_SEED, first: int = 0
         nbytes = n * stride + slack
         arena = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         _lib.check(lib.ingot_pktgen_fill(int(profile), seed, first, n, None, int(stride),
-                                         _ptr(lens), _ptr(arena), nbytes, _stream(stream)),
+                                         _ptr(lens), _ptr(arena), nbytes,
+                                         _stream(stream, device)),
                    "ingot_pktgen_fill")
         return arena, None, lens
     lens = gen_lengths(profile, n, seed, first, device, stream)
@@ -420,7 +530,8 @@ def gen_frames(profile: GenProfile, n: int, seed: int = GEN_SEED, first: int = 0
     nbytes = total + slack
     arena = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     _lib.check(lib.ingot_pktgen_fill(int(profile), seed, first, n, _ptr(off), 0, _ptr(lens),
-                                     _ptr(arena), nbytes, _stream(stream)), "ingot_pktgen_fill")
+                                     _ptr(arena), nbytes, _stream(stream, device)),
+               "ingot_pktgen_fill")
     return arena, off, lens
 
 

@@ -35,6 +35,12 @@ SIGNATURES = {
     "ingot_gpu_host_map": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                           ctypes.POINTER(ctypes.c_void_p)]),
     "ingot_gpu_host_unmap": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "ingot_gpu_doorbell_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
+                                                 ctypes.POINTER(ctypes.c_void_p)]),
+    "ingot_gpu_doorbell_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32,
+                                               ctypes.c_void_p]),
+    "ingot_gpu_doorbell_ring": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
+    "ingot_gpu_doorbell_destroy": (None, [ctypes.c_void_p]),
     "ingot_gpu_ctx_set_tuning": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "ingot_gpu_ctx_get_tuning": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ingot_gpu_parse": (

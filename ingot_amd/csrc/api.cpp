@@ -248,6 +248,57 @@ int ingot_gpu_host_unmap(ingot_gpu_ctx* ctx, void* host) {
     return INGOT_GPU_SUCCESS;
 }
 
+// Doorbell: one pinned, coherent host word the command processor polls
+// (hipStreamWaitValue32).  Host stores to coherent memory are seen by the
+// device without a flush.
+struct ingot_gpu_doorbell {
+    int device;
+    uint32_t* word;
+};
+
+int ingot_gpu_doorbell_create(ingot_gpu_ctx* ctx, ingot_gpu_doorbell** out,
+                              volatile uint32_t** host_word) {
+    if (!ctx || !out) return INGOT_GPU_EINVAL;
+    *out = nullptr;
+    if (host_word) *host_word = nullptr;
+    if (int e = enter(ctx)) return e;
+    int can = 0;
+    if (hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, ctx->device) !=
+            hipSuccess ||
+        !can)
+        return INGOT_GPU_ENODEV;
+    void* p = nullptr;
+    if (hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+        return INGOT_GPU_EHIP;
+    ingot_gpu_doorbell* d = new (std::nothrow) ingot_gpu_doorbell{ctx->device, (uint32_t*)p};
+    if (!d) {
+        (void)hipHostFree(p);
+        return INGOT_GPU_ENOMEM;
+    }
+    __atomic_store_n(d->word, 0u, __ATOMIC_SEQ_CST);
+    *out = d;
+    if (host_word) *host_word = d->word;
+    return INGOT_GPU_SUCCESS;
+}
+
+int ingot_gpu_doorbell_wait(ingot_gpu_doorbell* db, uint32_t value, void* stream) {
+    if (!db) return INGOT_GPU_EINVAL;
+    return from_hip(hipStreamWaitValue32((hipStream_t)stream, db->word, value,
+                                         hipStreamWaitValueGte, 0xffffffffu));
+}
+
+int ingot_gpu_doorbell_ring(ingot_gpu_doorbell* db, uint32_t value) {
+    if (!db) return INGOT_GPU_EINVAL;
+    __atomic_store_n(db->word, value, __ATOMIC_SEQ_CST);
+    return INGOT_GPU_SUCCESS;
+}
+
+void ingot_gpu_doorbell_destroy(ingot_gpu_doorbell* db) {
+    if (!db) return;
+    (void)hipHostFree(db->word);
+    delete db;
+}
+
 int ingot_gpu_ctx_set_tuning(ingot_gpu_ctx* ctx, int key, int value) {
     if (!ctx || !ingot_gpu::tuning_valid(key, value)) return INGOT_GPU_EINVAL;
     switch (key) {

@@ -29,7 +29,8 @@
 // No MFMA: this is integer field extraction bounded by HBM bandwidth.
 #include <hip/hip_runtime.h>
 
-#include <atomic>
+#include <mutex>
+#include <vector>
 
 #include <type_traits>
 
@@ -1349,17 +1350,27 @@ hipError_t launch_pipe(const ParseArgs& a, int chain, uint32_t grid, hipStream_t
 }
 
 // Blocks of `kernel` one CU holds at once (its LDS / VGPR footprint), queried
-// once per kernel instance.
+// once per (kernel instance, device).  Keyed by the kernel's address: every
+// k_parse<..., ARGS> instance has the same function type, and their LDS
+// footprints differ with the window (about 9 blocks per CU at 3 chunks, 4 at 8).
 template <class K>
 uint32_t resident_per_cu(K kernel) {
-    static std::atomic<int> occ{0};
-    int v = occ.load(std::memory_order_relaxed);
-    if (!v) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kernel, BLOCK, 0) != hipSuccess ||
-            v < 1)
-            v = 1;
-        occ.store(v, std::memory_order_relaxed);
-    }
+    struct Entry {
+        const void* k;
+        int dev, blocks;
+    };
+    static std::mutex mu;
+    static std::vector<Entry> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const void* key = reinterpret_cast<const void*>(kernel);
+    std::lock_guard<std::mutex> g(mu);
+    for (const Entry& e : cache)
+        if (e.k == key && e.dev == dev) return (uint32_t)e.blocks;
+    int v = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kernel, BLOCK, 0) != hipSuccess || v < 1)
+        v = 1;
+    cache.push_back(Entry{key, dev, v});
     return (uint32_t)v;
 }
 

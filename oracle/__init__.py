@@ -65,6 +65,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     lib.oracle_parse_read_batch.argtypes = [vp, vp, vp, vp, ctypes.c_uint64, ctypes.c_int, vp,
                                             vp, vp, vp, ctypes.c_int]
     lib.oracle_parse_read_batch.restype = ctypes.c_int
+    lib.oracle_set_passes.argtypes = [ctypes.c_int]
+    lib.oracle_set_passes.restype = None
     if path is None:
         _lib = lib
     return lib

@@ -923,9 +923,16 @@ typedef struct {
     uint64_t lo, hi;
 } range_job_t;
 
+/* Passes each worker makes over its range per batch call (default 1).  A
+ * throughput measurement only: >1 amortises thread start-up over more work
+ * (bench.py's all-core CPU baseline); results are those of one pass. */
+static int g_passes = 1;
+
+void oracle_set_passes(int passes) { g_passes = passes < 1 ? 1 : passes; }
+
 static void* run_range(void* arg) {
     range_job_t* j = (range_job_t*)arg;
-    j->fn(j->ctx, j->lo, j->hi);
+    for (int k = 0; k < g_passes; ++k) j->fn(j->ctx, j->lo, j->hi);
     return 0;
 }
 

@@ -54,6 +54,10 @@ int oracle_parse_batch(const uint8_t* arena, const uint64_t* off,
                        int chain, ingot_rec* rec, ingot_fields* fields,
                        int nthreads);
 
+/* Throughput measurement only: every batch worker repeats its range `passes`
+ * times per call (thread start-up amortised over more work). */
+void oracle_set_passes(int passes);
+
 /* Generic big-endian bitfield getter (ingot-macros/src/packet/bitfield.rs
  * BE get paths): the n_bits (<= 64) starting at bit first_bit, MSB first. */
 uint64_t oracle_be_bits(const uint8_t* hdr, uint32_t first_bit, uint32_t n_bits);

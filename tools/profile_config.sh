@@ -12,6 +12,6 @@ mkdir -p gpurun_out
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$cfg -o run -- \
     python3 $R/bench.py --config $cfg --streams 1 --steps 100 --warmup 10 --no-cpu-baseline \
-    --no-variants > $R/gpurun_out/prof_$cfg.log 2>&1
+    --no-variants --no-gate > $R/gpurun_out/prof_$cfg.log 2>&1
 find $R/gpurun_out/prof_$cfg -name "*kernel_stats.csv" -exec cp {} $R/gpurun_out/${tag}_${cfg}_streams1_kernel_stats.csv \;
 head -5 $R/gpurun_out/${tag}_${cfg}_streams1_kernel_stats.csv
