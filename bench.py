@@ -395,29 +395,30 @@ class Gate:
 
 
 def _timed(torch, streams, launch, steps, finish=None, gate=None):
-    """Run `steps` launches; returns (ms, wall s).  Ungated: between a start
-    event on streams[0] (the other streams fork from it) and an end event
-    after every stream has joined back.  Gated: every stream waits on the
-    doorbell, then stamps its own start event; the region runs from the
-    earliest start to the end event."""
+    """Run `steps` launches; returns (ms, wall s).  Every stream stamps a
+    start event before its first launch and an end event after its last one;
+    the region is the earliest start to the latest end (all on the device
+    clock).  Ungated, the other streams fork from streams[0]'s start event;
+    gated, every stream waits on the doorbell instead.  No stream joins
+    another at the end: a cross-stream event wait costs ~7 us of device time
+    that would land inside the region (tools/region_probe.py)."""
     s0 = streams[0]
-    e1 = torch.cuda.Event(enable_timing=True)
     w0 = time.perf_counter()
     if gate is not None:
         gate.arm(streams)
-    starts = []
+    starts, ends = [], []
     try:
-        if gate is not None:
-            for s in streams:
-                e = torch.cuda.Event(enable_timing=True)
-                e.record(s)
-                starts.append(e)
-        else:
+        if gate is None:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record(s0)
             starts.append(e0)
             for s in streams[1:]:
                 s.wait_event(e0)
+        else:
+            for s in streams:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record(s)
+                starts.append(e)
         for k in range(steps):
             rc = launch(k)
             if rc:
@@ -426,16 +427,16 @@ def _timed(torch, streams, launch, steps, finish=None, gate=None):
                 gate.open()
         if finish is not None:
             finish()
-        for s in streams[1:]:
-            ev = torch.cuda.Event()
-            ev.record(s)
-            s0.wait_event(ev)
-        e1.record(s0)
+        for s in streams:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(s)
+            ends.append(e)
     finally:
         if gate is not None:
             gate.open()
     torch.cuda.synchronize()
-    return max(e.elapsed_time(e1) for e in starts), time.perf_counter() - w0
+    ms = max(a.elapsed_time(b) for a in starts for b in ends)
+    return ms, time.perf_counter() - w0
 
 
 def kernel_sources_sha() -> str:

@@ -7,6 +7,9 @@ construction", a value the reference's frame literally carries, e.g. the
 bench frames that it only `unwrap()`s).  "derived" vectors wrap a reference
 header-level vector in the minimal chain prefix/suffix needed to run it
 through a chain parser; their expected values follow from the same asserts.
+The edge vectors (edge_frames) are built here to pin semantics the generated
+code defines but no reference test exercises; each cites the generated-code
+line its expectation follows from.
 
 The reference is Rust and cannot run here (no cargo/rustc), so these
 fixtures are what pins the CPU oracle (tests/test_oracle_golden.py) and,
@@ -277,6 +280,108 @@ def chain_frames():
         chain="GenericUlp", frame=hexs(f), derived="emitted bytes restated from the layout",
         expect=dict(ok=False, error="Unwanted", label="inner_ulp", l3="ipv6", l4_proto=59,
                     n_v6ext=1)))
+    return out
+
+
+def edge_frames():
+    """Edge semantics the generated code defines but no reference test pins
+    (VERDICT r01 weak item 1).  Each vector cites the generated-code line its
+    expectation follows from; frames are built here, not taken from a test."""
+    out = []
+    udp = u16(0x1234) + u16(0x5678) + u16(12) + u16(0)
+
+    def v4(ihl, proto, total=0):
+        h = [0] * 20
+        h[0] = 0x40 | ihl
+        h[2:4] = u16(total)
+        h[8] = 64
+        h[9] = proto
+        h[12:16] = [10, 0, 0, 1]
+        h[16:20] = [10, 0, 0, 2]
+        return h
+
+    # IPv4 ihl 1..4: options = (ihl*4).saturating_sub(20) = 0 (ip.rs:91), so
+    # the header is the 20-B fixed part whatever ihl says; parse goes on.
+    for ihl in (1, 2, 3, 4):
+        f = eth(BROADCAST, MAC_ABCDEF, 0x0800) + v4(ihl, 17) + udp + [0xEE] * 4
+        out.append(dict(
+            name=f"ipv4_ihl_{ihl}_saturates", source="ingot/src/ip.rs:91",
+            chain="UdpParser", frame=hexs(f), derived="saturating_sub var_len, ihl < 5",
+            expect=dict(ok=True, l3="ipv4", l4="udp", remainder=4,
+                        fields=dict(v4_ihl=ihl, v4_version=4, l4_source=0x1234,
+                                    l4_destination=0x5678))))
+    # TCP data_offset 1..4: options = (data_offset*4).saturating_sub(20) = 0
+    # (tcp.rs:28).
+    for doff in (1, 2, 3, 4):
+        t = u16(443) + u16(51000) + [0, 0, 0, 7] + [0, 0, 0, 9] + [doff << 4, 0x18] + u16(512)
+        t += u16(0) + u16(0)
+        f = eth(BROADCAST, MAC_ABCDEF, 0x0800) + v4(5, 6) + t + [0xEE] * 3
+        out.append(dict(
+            name=f"tcp_data_offset_{doff}_saturates", source="ingot/src/tcp.rs:28",
+            chain="GenericUlp", frame=hexs(f), derived="saturating_sub var_len, data_offset < 5",
+            expect=dict(ok=True, l3="ipv4", l4="tcp", remainder=3,
+                        fields=dict(tcp_data_offset=doff, l4_source=443, l4_destination=51000,
+                                    tcp_sequence=7, tcp_acknowledgement=9, tcp_flags=0x18))))
+
+    def v6(nh):
+        h = [0] * 40
+        h[0] = 0x60
+        h[6] = nh
+        h[7] = 64
+        h[23] = 1
+        h[39] = 2
+        return h
+
+    # An EH chain that ends exactly at the end of the buffer with an EH-class
+    # next_header: RepeatedView's loop stops at bytes_read == original_len
+    # (util.rs:206), the last hint (43, Routing) goes to the Ulp choice, which
+    # has no such variant: Unwanted at inner_ulp, before any bounds check
+    # (choice.rs:231-246).
+    f = eth(BROADCAST, MAC_ABCDEF, 0x86DD) + v6(0) + [43, 0] + [0] * 6
+    out.append(dict(
+        name="eh_chain_ends_at_buffer_end", source="ingot-types/src/util.rs:206-216",
+        chain="GenericUlp", frame=hexs(f), derived="HBH whose next_header is Routing, then EOF",
+        expect=dict(ok=False, error="Unwanted", label="inner_ulp", l3="ipv6", l4_proto=43,
+                    n_v6ext=1)))
+    # A Fragment EH cut short: the loop enters (bytes remain), the 8-B
+    # Fragment header is TooSmall, and a non-Unwanted error propagates out of
+    # RepeatedView (util.rs:214): TooSmall for the IPv6 layer.
+    f = eth(BROADCAST, MAC_ABCDEF, 0x86DD) + v6(44) + [17, 0, 0, 0, 0]
+    out.append(dict(
+        name="truncated_fragment_eh", source="ingot-types/src/util.rs:214",
+        chain="UdpParser", frame=hexs(f), derived="next_header 44 with 5 of its 8 bytes",
+        expect=dict(ok=False, error="TooSmall", label="l3", l3="ipv6")))
+    # ... and with no byte after the IPv6 header the loop never runs: the
+    # Fragment hint reaches the L4 choice, which rejects it.
+    f = eth(BROADCAST, MAC_ABCDEF, 0x86DD) + v6(44)
+    out.append(dict(
+        name="fragment_hint_with_no_bytes", source="ingot-types/src/util.rs:206",
+        chain="UdpParser", frame=hexs(f), derived="next_header 44 at the end of the buffer",
+        expect=dict(ok=False, error="Unwanted", label="l4", l3="ipv6", l4_proto=44,
+                    n_v6ext=0)))
+    # GenericUlp on an ARP frame of exactly 14 B: the exit_on_arp control
+    # accepts after inner_eth (packets.rs:45-51; parse.rs:144-156, 221-254):
+    # Ok, remainder empty.
+    f = eth(BROADCAST, MAC_ABCDEF, 0x0806)
+    out.append(dict(
+        name="generic_ulp_arp_exactly_14", source="ingot-macros/src/parse.rs:144-156,221-254",
+        chain="GenericUlp", frame=hexs(f), derived="ARP Ethernet header, no body",
+        expect=dict(ok=True, accepted=True, l3="none", l4="none", remainder=0)))
+    # UdpParser's L4 choice (choices.rs:25-29) has no ICMP variant: Unwanted
+    # at l4 before any bounds check, even with no L4 bytes at all ...
+    f = eth(BROADCAST, MAC_ABCDEF, 0x0800) + v4(5, 1)
+    out.append(dict(
+        name="udp_parser_icmp_is_unwanted", source="ingot-examples/src/choices.rs:25-29",
+        chain="UdpParser", frame=hexs(f), derived="IPv4 protocol 1, nothing after",
+        expect=dict(ok=False, error="Unwanted", label="l4", l3="ipv4", l4_proto=1)))
+    # ... while a truncated TCP header is selected by the choice, fails its
+    # own parse (TooSmall) before the from= conversion is reached
+    # (parse.rs:196-200).
+    f = eth(BROADCAST, MAC_ABCDEF, 0x0800) + v4(5, 6) + [0] * 10
+    out.append(dict(
+        name="udp_parser_truncated_tcp_is_too_small", source="ingot-macros/src/parse.rs:196-200",
+        chain="UdpParser", frame=hexs(f), derived="IPv4 protocol 6, 10 of TCP's 20 bytes",
+        expect=dict(ok=False, error="TooSmall", label="l4", l3="ipv4", l4="tcp")))
     return out
 
 
@@ -651,7 +756,7 @@ def main() -> None:
     doc = dict(
         reference="oxidecomputer/ingot @ 2025-08-08",
         generator="tests/golden/make_golden.py",
-        chain_kats=chain_frames() + geneve_frames(),
+        chain_kats=chain_frames() + edge_frames() + geneve_frames(),
         header_kats=header_kats(),
         choice_kats=choice_kats(),
         read_kats=read_kats(),
