@@ -405,6 +405,10 @@ void ingot_gpu_doorbell_destroy(ingot_gpu_doorbell* db);
  *   INGOT_TUNE_WRITEBACK       ingot_gpu_parse_modify on slot rings: bytes
  *                              written back per edited unit, 16, 32 or 64
  *                              (0 = measured default)
+ *   INGOT_TUNE_FLOW_TABLE      ingot_gpu_flow_hist's Toeplitz lookup table:
+ *                              0 / 16 = 16-bit entries when bins <= 65,536
+ *                              and no full hash is requested (default), 32 =
+ *                              always 32-bit entries (same flow bins)
  */
 #define INGOT_TUNE_WINDOW_INDEXED 1
 #define INGOT_TUNE_WINDOW_STRIDED 2
@@ -413,6 +417,7 @@ void ingot_gpu_doorbell_destroy(ingot_gpu_doorbell* db);
 #define INGOT_TUNE_CACHE_POLICY 5
 #define INGOT_TUNE_PIPE_DEPTH 6
 #define INGOT_TUNE_WRITEBACK 7
+#define INGOT_TUNE_FLOW_TABLE 8
 int ingot_gpu_ctx_set_tuning(ingot_gpu_ctx* ctx, int key, int value);
 int ingot_gpu_ctx_get_tuning(const ingot_gpu_ctx* ctx, int key);
 

@@ -77,6 +77,7 @@ TUNE_PIPELINE = 4
 TUNE_CACHE_POLICY = 5
 TUNE_PIPE_DEPTH = 6
 TUNE_WRITEBACK = 7
+TUNE_FLOW_TABLE = 8
 
 
 class IngotRec(ctypes.Structure):

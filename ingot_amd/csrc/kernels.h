@@ -19,8 +19,16 @@ namespace ingot_gpu {
 enum LayoutKind { LAYOUT_STRIDED = 0, LAYOUT_INDEXED = 1, LAYOUT_SEGMENTED = 2, LAYOUT_PACKED = 3 };
 
 // Output mode: 16-B ingot_rec, 8-B ingot_rec8, 256-B ingot_fields, or the
-// flow hash + histogram.
-enum OutMode { OUT_REC16 = 0, OUT_REC8 = 1, OUT_FIELDS = 2, OUT_FLOWS = 3, OUT_MODIFY = 4 };
+// flow hash + histogram (OUT_FLOWS16: only the hash's low 16 bits, enough for
+// <= 65,536 bins when the full hash is not requested — half the LDS table).
+enum OutMode {
+    OUT_REC16 = 0,
+    OUT_REC8 = 1,
+    OUT_FIELDS = 2,
+    OUT_FLOWS = 3,
+    OUT_MODIFY = 4,
+    OUT_FLOWS16 = 5
+};
 
 // Toeplitz key windows: w[b] = the 32 key bits starting at input bit b, for
 // every bit of the longest input (IPv6 src|dst|ports = 36 bytes).
@@ -97,6 +105,7 @@ struct Tuning {
     int pipe_depth = 0;    // ring kernel: tiles in flight per wave (0 = 2)
     int writeback = 0;     // ring rewrite kernel: write-back unit (0 = measured default)
     int cache_policy = 0;  // bit 0: nt staging loads; bit 1: nt record stores
+    int flow_table = 0;    // flows: 0 = auto (16-bit table when it suffices), 32 = 32-bit
     uint32_t cus = 256;  // compute units of the context's device (grid shaping)
     bool host_arena = false;  // per call: the arena is host memory (ingot_gpu_host_map)
 };

@@ -860,6 +860,28 @@ __device__ __forceinline__ void build_flow_table(uint32_t* tab, const uint32_t* 
     }
 }
 
+// The 16-bit table (OUT_FLOWS16): entry (p, v) = the low 16 bits of the
+// 32-bit entry, two per dword (entry e at half-word e).  The low 16 bits of a
+// Toeplitz hash are the XOR of the low 16 bits of its key windows, so the
+// flow bin (hash & bin_mask, bins <= 65,536) is unchanged; 2,304 B instead
+// of 4,608 per block.
+constexpr uint32_t FLOW_TAB16 = FLOW_POS * 16 / 2;  // dwords
+
+__device__ __forceinline__ void build_flow_table16(uint32_t* tab, const uint32_t* W) {
+    for (uint32_t d = threadIdx.x; d < FLOW_TAB16; d += BLOCK) {
+        uint32_t two = 0;
+#pragma unroll
+        for (uint32_t h = 0; h < 2; ++h) {
+            const uint32_t e = 2u * d + h, p = e / 16u, v = e & 15u;
+            uint32_t acc = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) acc ^= ((v >> (3u - k)) & 1u) ? W[4u * p + k] : 0u;
+            two |= (acc & 0xffffu) << (16u * h);
+        }
+        tab[d] = two;
+    }
+}
+
 // Flow classification (ingot_gpu_flow_hist): hash of src|dst|ports.
 // Appending zero ports leaves a Toeplitz hash unchanged, so ICMP/other L4 use
 // the same word positions with a zero port word — and an IPv4 input
@@ -937,12 +959,37 @@ __device__ __forceinline__ uint32_t toeplitz9(const FlowWords& x, const uint32_t
     return h;
 }
 
-template <class FR>
+// The low 16 bits of the Toeplitz hash of the 9 words from the 16-bit table:
+// lookup (position q, nibble v) is the half-word at byte 32 q + 2 v (the
+// table is 32-B aligned: one shift + one v_and_or per lookup, the position
+// in the ds_read_u16 offset).
+__device__ __forceinline__ uint32_t toeplitz9_16(const FlowWords& x, const uint32_t* tab) {
+    typedef __attribute__((address_space(3))) const uint16_t lds_u16;
+    uint32_t base = (uint32_t)(size_t)(const lds_u32*)tab;
+    asm volatile("" : "+v"(base));
+    uint32_t h = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 9; ++k) {
+        uint32_t t[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t s = 28u - 4u * j;
+            const uint32_t v8 = s >= 1u ? (x.w[k] >> (s - 1u)) : (x.w[k] << 1u);
+            lds_u16* e = (lds_u16*)(size_t)((v8 & (15u << 1)) | base);
+            t[j] = e[(8u * k + j) * 16u];
+        }
+        h = xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), xor3(t[6], t[7], h));
+    }
+    return h;
+}
+
+template <bool H16, class FR>
 __device__ __forceinline__ bool flow_hash(const FR& f, const Rec& r, const uint32_t* tab,
                                           uint32_t& h) {
     FlowWords x;
     const bool ok = flow_words(f, r, x);
-    h = ok ? toeplitz9(x, tab) : 0u;
+    if constexpr (H16) h = ok ? toeplitz9_16(x, tab) : 0u;
+    else h = ok ? toeplitz9(x, tab) : 0u;
     return ok;
 }
 
@@ -955,9 +1002,13 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
     // +16 dwords: the second dword of a pair read may run past the last image.
     // NCH = 0: no staging, every read goes to L2/HBM.
     __shared__ __attribute__((aligned(16))) uint32_t s_win[WAVES * WAVE_DW + 16];
-    __shared__ __attribute__((aligned(64 * FLOW_COPIES))) uint32_t s_tab[MODE == OUT_FLOWS ? FLOW_TAB : 1];
-    if constexpr (MODE == OUT_FLOWS) {
-        build_flow_table(s_tab, args.w);
+    constexpr bool FLOWS = MODE == OUT_FLOWS || MODE == OUT_FLOWS16;
+    constexpr bool H16 = MODE == OUT_FLOWS16;
+    __shared__ __attribute__((aligned(64 * FLOW_COPIES)))
+    uint32_t s_tab[FLOWS ? (H16 ? FLOW_TAB16 : FLOW_TAB) : 1];
+    if constexpr (FLOWS) {
+        if constexpr (H16) build_flow_table16(s_tab, args.w);
+        else build_flow_table(s_tab, args.w);
         __syncthreads();
     }
 
@@ -967,7 +1018,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
     const uint64_t ntiles = (a.n + WAVE - 1u) / WAVE;
     const uint32_t mis = (uint32_t)((uintptr_t)a.arena & 31u);  // arena address mod 32
     constexpr uint32_t SKIP =
-        MODE == OUT_FLOWS && LAYOUT == LAYOUT_INDEXED && !TUN ? INGOT_FLOW_SKIP : 0u;
+        FLOWS && LAYOUT == LAYOUT_INDEXED && !TUN ? INGOT_FLOW_SKIP : 0u;
     static_assert(SKIP <= 12u, "the walk reads the ethertype at frame byte 12");
 
     for (uint64_t t = (uint64_t)blockIdx.x * WAVES + wave; t < ntiles;
@@ -1109,10 +1160,10 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
             if (valid && a.out) static_cast<uint4*>(a.out)[i] = pack(r);
             // the window writes must land before the next tile's LDS-DMA
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        } else if constexpr (MODE == OUT_FLOWS) {
+        } else if constexpr (FLOWS) {
             walk<CHAIN, false>(fr, r, nullptr, nullptr);
             uint32_t h;
-            const bool counted = valid && flow_hash(fr, r, s_tab, h);
+            const bool counted = valid && flow_hash<H16>(fr, r, s_tab, h);
             if (valid) {
                 args.flow[i] = counted ? (h & args.bin_mask) : INGOT_FLOW_NONE;
                 if (args.hash) args.hash[i] = h;
@@ -1573,32 +1624,42 @@ hipError_t launch_modify(const ModifyArgs& args, int layout_kind, int chain, con
 // its default window is 5 chunks from the chunk holding byte 12 (SKIP in
 // k_parse: 392 -> 384 us per C5 flow_hist vs 5 chunks from the frame start;
 // 4 chunks from byte 12: 387); the same tuning knobs override the size.
+template <int MODE>
+hipError_t launch_flows_mode(const FlowArgs& a, int layout_kind, int chain, const Tuning& t,
+                             hipStream_t s) {
+    const uint32_t g = grid_for(a.p.n, t.max_blocks);
+    const uint32_t pc = t.max_blocks ? 0u : t.cus;
+    if (layout_kind == LAYOUT_STRIDED) {
+        switch (t.window_strided ? t.window_strided : (a.p.stride <= 64u ? 4 : 5)) {
+        case 3: return launch_chain<3, LAYOUT_STRIDED, MODE>(a, chain, g, s, pc);
+        case 4: return launch_chain<4, LAYOUT_STRIDED, MODE>(a, chain, g, s, pc);
+        case 8: return launch_chain<8, LAYOUT_STRIDED, MODE>(a, chain, g, s, pc);
+        default: return launch_chain<5, LAYOUT_STRIDED, MODE>(a, chain, g, s, pc);
+        }
+    }
+    switch (t.window_indexed ? t.window_indexed : 5) {
+    case 3: return launch_chain<3, LAYOUT_INDEXED, MODE>(a, chain, g, s, pc);
+    case 4: return launch_chain<4, LAYOUT_INDEXED, MODE>(a, chain, g, s, pc);
+    case 6: return launch_chain<6, LAYOUT_INDEXED, MODE>(a, chain, g, s, pc);
+    default: return launch_chain<5, LAYOUT_INDEXED, MODE>(a, chain, g, s, pc);
+    }
+}
+
 hipError_t launch_flows(const FlowArgs& a, int layout_kind, int chain, const Tuning& t,
                         hipStream_t s) {
     if (a.p.n == 0) return hipSuccess;
     // Each block builds the table once, so the grid is persistent: exactly the
-    // blocks the device holds at once (6 per CU at the default window: LDS),
+    // blocks the device holds at once (resident_per_cu, per kernel instance),
     // each wave walking tiles.  Measured on C5 (parse+hash+histogram, us per
     // step): one tile per wave 546, 4 blocks per CU 434, 5 per CU 402, 6 / 8
     // per CU (a second partial round) 511 / 443.  A double-buffered variant
     // (next tile staged while hashing, 3 blocks per CU for its two images)
     // measured 526 vs 454 at the time.
-    const uint32_t g = grid_for(a.p.n, t.max_blocks);
-    const uint32_t pc = t.max_blocks ? 0u : t.cus;
-    if (layout_kind == LAYOUT_STRIDED) {
-        switch (t.window_strided ? t.window_strided : (a.p.stride <= 64u ? 4 : 5)) {
-        case 3: return launch_chain<3, LAYOUT_STRIDED, OUT_FLOWS>(a, chain, g, s, pc);
-        case 4: return launch_chain<4, LAYOUT_STRIDED, OUT_FLOWS>(a, chain, g, s, pc);
-        case 8: return launch_chain<8, LAYOUT_STRIDED, OUT_FLOWS>(a, chain, g, s, pc);
-        default: return launch_chain<5, LAYOUT_STRIDED, OUT_FLOWS>(a, chain, g, s, pc);
-        }
-    }
-    switch (t.window_indexed ? t.window_indexed : 5) {
-    case 3: return launch_chain<3, LAYOUT_INDEXED, OUT_FLOWS>(a, chain, g, s, pc);
-    case 4: return launch_chain<4, LAYOUT_INDEXED, OUT_FLOWS>(a, chain, g, s, pc);
-    case 6: return launch_chain<6, LAYOUT_INDEXED, OUT_FLOWS>(a, chain, g, s, pc);
-    default: return launch_chain<5, LAYOUT_INDEXED, OUT_FLOWS>(a, chain, g, s, pc);
-    }
+    // Bins <= 65,536 and no full hash requested: the 16-bit table
+    // (OUT_FLOWS16) suffices — the flow bins are identical.
+    const bool h16 = t.flow_table != 32 && a.bin_mask <= 0xffffu && !a.hash;
+    return h16 ? launch_flows_mode<OUT_FLOWS16>(a, layout_kind, chain, t, s)
+               : launch_flows_mode<OUT_FLOWS>(a, layout_kind, chain, t, s);
 }
 
 bool tuning_valid(int key, int value) {
@@ -1618,6 +1679,8 @@ bool tuning_valid(int key, int value) {
         return value == 0 || (value >= 2 && value <= 4);
     case INGOT_TUNE_WRITEBACK:
         return value == 0 || value == 16 || value == 32 || value == 64;
+    case INGOT_TUNE_FLOW_TABLE:
+        return value == 0 || value == 16 || value == 32;
     default:
         return false;
     }

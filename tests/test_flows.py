@@ -156,6 +156,49 @@ def test_flow_kernels_every_setting(tune, profile, chain, stride):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("table", [0, 32])
+@pytest.mark.parametrize("tune", [{}, {"win": 3}, {"win": 4}, {"win": 8}, {"blocks": 5}])
+@pytest.mark.parametrize("bins", [1 << 16, 1024])
+@pytest.mark.parametrize("profile,chain,stride", [
+    ("FLOWS", "VlanUlp", None), ("ADVERSARIAL", "GenericUlp", None),
+    ("GENEVE_ADVERSARIAL", "GeneveOverV6Tunnel", None), ("VLAN_V6EH", "VlanUlp", 256),
+])
+def test_flow_bins_without_hashes(table, tune, bins, profile, chain, stride):
+    """No full hash requested and bins <= 65,536: the kernel uses the 16-bit
+    lookup table (OUT_FLOWS16) unless INGOT_TUNE_FLOW_TABLE = 32 forces the
+    32-bit one.  Flow ids and the histogram equal the oracle's either way."""
+    import torch
+
+    import ingot_amd
+    from ingot_amd import GenProfile
+    from ingot_amd.abi import (TUNE_FLOW_TABLE, TUNE_MAX_BLOCKS, TUNE_WINDOW_INDEXED,
+                               TUNE_WINDOW_STRIDED)
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    n = 100_003
+    ctx = ingot_amd.Context(0)
+    ctx.set_tuning(TUNE_FLOW_TABLE, table)
+    if "win" in tune:
+        ctx.set_tuning(TUNE_WINDOW_STRIDED if stride else TUNE_WINDOW_INDEXED, tune["win"])
+    if "blocks" in tune:
+        ctx.set_tuning(TUNE_MAX_BLOCKS, tune["blocks"])
+    arena, off, lens = ingot_amd.gen_frames(GenProfile[profile], n, seed=17, stride=stride)
+    hist = torch.zeros(bins, dtype=torch.int32, device="cuda")
+    flow = ctx.flow_hist(arena, off, lens, Chain[chain], hist=hist, stride=stride or 0, n=n,
+                         workspace=ctx.flow_hist_workspace(n, bins))
+    torch.cuda.synchronize()
+    host = lambda t: None if t is None else t.cpu().numpy()  # noqa: E731
+    w_hist, _ = oracle.flow_hist(host(arena), host(off), host(lens), Chain[chain],
+                                 stride=stride or 0, n=n, bins=bins)
+    w_flow = oracle.flow_hist.last_flows
+    g = flow.cpu().numpy().view(np.uint32)
+    bad = np.nonzero(g != w_flow)[0]
+    assert bad.size == 0, (bad[:5], g[bad[:5]], w_flow[bad[:5]])
+    assert (hist.cpu().numpy().view(np.uint32) == w_hist).all()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("ws", [False, True])
 @pytest.mark.parametrize("bins", [1, 2, 4096, 1 << 16, 1 << 17, 1 << 20])
 def test_flow_hist_bin_regimes(bins, ws):
