@@ -609,6 +609,9 @@ def main():
                     help="time from host submission (no doorbell-held first launches)")
     ap.add_argument("--plan", action="store_true",
                     help="print the ranks' shares and exit without touching a GPU")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="INGOT_TUNE_* knob for this run, e.g. slow_path=1 (A/B and "
+                         "profiling of variants; results never depend on it)")
     ap.add_argument("--cpu-budget", type=float, default=1.5)
     ap.add_argument("--rotate-mib", type=int, default=512,
                     help="minimum bytes of distinct arenas rotated across steps")
@@ -661,6 +664,11 @@ def main():
     prof_name, _, stride, chain_name, desc = CONFIGS[args.config]
     profile, chain = GenProfile[prof_name], Chain[chain_name]
     ctx = ingot_amd.Context(local)
+    from ingot_amd import abi
+
+    for kv in args.tune:
+        k, v = kv.split("=")
+        ctx.set_tuning(getattr(abi, f"TUNE_{k.upper()}"), int(v))
     lib = ingot_amd.load_library()
     mode = MODES.get(args.config, "parse")
     flows = mode == "flows"
@@ -798,7 +806,8 @@ def main():
     family = kernel_family(mode, ring)
     sha = kernel_sources_sha()
     traffic = None
-    t, pf = pmc_for(args.config, family, sha) if args.record == 16 else (None, None)
+    t, pf = (pmc_for(args.config, family, sha) if args.record == 16 and not args.tune
+             else (None, None))
     if t is not None:
         traffic = {"bytes_per_launch": t["traffic_bytes_per_launch"],
                    "ratio_to_algorithmic": round(t["traffic_bytes_per_launch"] / bytes_launch, 4),

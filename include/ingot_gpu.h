@@ -409,6 +409,12 @@ void ingot_gpu_doorbell_destroy(ingot_gpu_doorbell* db);
  *                              0 / 16 = 16-bit entries when bins <= 65,536
  *                              and no full hash is requested (default), 32 =
  *                              always 32-bit entries (same flow bins)
+ *   INGOT_TUNE_SLOW_PATH       bytes past the staged window (indexed frames,
+ *                              16-B records, default windows): 0 = read per
+ *                              lane from L2/HBM (default), 1 = ballot the
+ *                              lanes whose chain outruns the window, re-stage
+ *                              a window twice as large for just those frames
+ *                              (compacted) and walk them again
  */
 #define INGOT_TUNE_WINDOW_INDEXED 1
 #define INGOT_TUNE_WINDOW_STRIDED 2
@@ -418,6 +424,7 @@ void ingot_gpu_doorbell_destroy(ingot_gpu_doorbell* db);
 #define INGOT_TUNE_PIPE_DEPTH 6
 #define INGOT_TUNE_WRITEBACK 7
 #define INGOT_TUNE_FLOW_TABLE 8
+#define INGOT_TUNE_SLOW_PATH 9
 int ingot_gpu_ctx_set_tuning(ingot_gpu_ctx* ctx, int key, int value);
 int ingot_gpu_ctx_get_tuning(const ingot_gpu_ctx* ctx, int key);
 

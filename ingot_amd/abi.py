@@ -78,6 +78,7 @@ TUNE_CACHE_POLICY = 5
 TUNE_PIPE_DEPTH = 6
 TUNE_WRITEBACK = 7
 TUNE_FLOW_TABLE = 8
+TUNE_SLOW_PATH = 9
 
 
 class IngotRec(ctypes.Structure):

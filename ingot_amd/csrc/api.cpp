@@ -309,6 +309,7 @@ int ingot_gpu_ctx_set_tuning(ingot_gpu_ctx* ctx, int key, int value) {
     case INGOT_TUNE_PIPE_DEPTH: ctx->tuning.pipe_depth = value; break;
     case INGOT_TUNE_WRITEBACK: ctx->tuning.writeback = value; break;
     case INGOT_TUNE_FLOW_TABLE: ctx->tuning.flow_table = value; break;
+    case INGOT_TUNE_SLOW_PATH: ctx->tuning.slow_path = value; break;
     default: ctx->tuning.max_blocks = (uint32_t)value; break;
     }
     return INGOT_GPU_SUCCESS;
@@ -325,6 +326,7 @@ int ingot_gpu_ctx_get_tuning(const ingot_gpu_ctx* ctx, int key) {
     case INGOT_TUNE_PIPE_DEPTH: return ctx->tuning.pipe_depth;
     case INGOT_TUNE_WRITEBACK: return ctx->tuning.writeback;
     case INGOT_TUNE_FLOW_TABLE: return ctx->tuning.flow_table;
+    case INGOT_TUNE_SLOW_PATH: return ctx->tuning.slow_path;
     default: return INGOT_GPU_EINVAL;
     }
 }

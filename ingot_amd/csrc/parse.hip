@@ -98,15 +98,20 @@ __device__ __forceinline__ uint32_t slot_of(uint32_t p, uint32_t c) {
 }
 
 // One lane's view of its frame: LDS window for the first bytes, HBM beyond.
-template <uint32_t NCH>
+// PROBE (the compacted slow path, INGOT_TUNE_SLOW_PATH = 1): a read past the
+// window loads nothing — it sets `miss` and yields 0, and the walk's loops
+// stop; the lane is walked again over a larger, re-staged window.
+template <uint32_t NCH, bool PROBE = false>
 struct Frame {
     static constexpr bool kRead = false;
+    static constexpr bool kProbe = PROBE;
     const lds_u32* win;  // this wave's LDS image
     uint32_t p;          // packet index within the wave (== lane)
     uint32_t sh;         // frame start inside its first staged chunk (0..15)
     uint32_t avail;      // frame bytes [0, avail) are staged in LDS
     uint32_t len;        // frame length
     const uint8_t* g;    // frame start in HBM
+    mutable uint32_t miss = 0;  // PROBE: a read fell past the window
 
     __device__ __forceinline__ uint32_t dw(uint32_t b) const {
         return win[slot_of<NCH>(p, b >> 4) * 4u + ((b >> 2) & 3u)];
@@ -123,6 +128,9 @@ struct Frame {
             const uint32_t d1 = ((b & 3u) + n > 4u) ? dw(a + 4u) : 0u;
             const uint32_t x = __builtin_amdgcn_alignbyte(d1, d0, b & 3u);  // bytes b.. little-endian
             v = __builtin_bswap32(x) >> (32u - 8u * n);
+        } else if constexpr (PROBE) {
+            miss = 1u;
+            v = 0u;
         } else {
             v = beyond(i, n);
         }
@@ -305,6 +313,9 @@ template <bool FIELDS, class FR>
 __device__ __forceinline__ bool v6_ext_chain(const FR& f, uint32_t len, uint32_t& q, uint32_t& h,
                                              uint32_t& n_eh, ingot_v6eh* eh) {
     while (q < len) {
+        if constexpr (FR::kProbe) {
+            if (f.miss) break;  // walked again over a larger window
+        }
         const uint32_t c = eh_class(h);
         if (c == EH_NONE) break;  // Err(Unwanted) => break
         uint32_t used, nh, x = 0;
@@ -496,6 +507,9 @@ __device__ __forceinline__ void walk(FR& f, Rec& r, ingot_fields* F, ingot_tunne
         uint32_t read = 0, n_opt = 0, crit = 0;
         bool opt_bad = false;
         while (read < span) {
+            if constexpr (FR::kProbe) {
+                if (f.miss) break;
+            }
             const uint32_t o = p + geneve::LEN + read, rem = span - read;
             if (rem < geneve_opt::LEN) { opt_bad = true; break; }
             const uint32_t ow = f.be(o, 4);
@@ -993,7 +1007,72 @@ __device__ __forceinline__ bool flow_hash(const FR& f, const Rec& r, const uint3
     return ok;
 }
 
-template <uint32_t NCH, int LAYOUT, int CHAIN, int MODE, class ARGS>
+// Index of the j-th set bit of m (j < popcount(m)): binary search on
+// popcounts, 6 steps.
+__device__ __forceinline__ uint32_t nth_set_bit(uint64_t m, uint32_t j) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t w = 32; w; w >>= 1) {
+        const uint64_t lo = (1ull << w) - 1ull;
+        const uint32_t c = (uint32_t)__popcll(m & lo);
+        if (j >= c) {
+            j -= c;
+            m >>= w;
+            pos += w;
+        } else {
+            m &= lo;
+        }
+    }
+    return pos;
+}
+
+// The compacted slow path (INGOT_TUNE_SLOW_PATH = 1; A/B against per-lane
+// byte loads).  After a PROBE walk over the NCH-chunk window,
+// the lanes whose chain ran past it are balloted and ranked (prefix count of
+// the ballot); in batches of B = 64 NCH / NCH2 lanes the wave re-stages the
+// first NCH2 = 2 NCH chunks of just those frames into its LDS image,
+// compacted (rank-major, lane-linear per LDS-DMA instruction: every
+// instruction fills 64 slots of the batch), and walks those lanes again over
+// the larger window; bytes past it are read per lane from L2/HBM.  This is
+// the GPU form of the reference's unbounded EH loop (util.rs:206-216) and
+// long IPv4/TCP options (ip.rs:91, tcp.rs:28).
+template <uint32_t NCH, int CHAIN>
+__device__ __forceinline__ void slow_rewalk(const Frame<NCH, true>& fr, Rec& r, bool valid,
+                                            uint32_t* wimg, uint32_t lane, const uint8_t* arena,
+                                            int64_t base, uint32_t sh, uint32_t len) {
+    constexpr uint32_t NCH2 = 2u * NCH;
+    constexpr uint32_t B = WAVE * NCH / NCH2;
+    const bool miss = valid && fr.miss;
+    const uint64_t m = __ballot(miss);
+    if (!m) return;
+    const uint32_t K = (uint32_t)__popcll(m);
+    const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    const uint32_t take2 = len < 16u * NCH2 - sh ? len : 16u * NCH2 - sh;
+    const uint32_t nch2 = (sh + take2 + 15u) >> 4;
+    for (uint32_t b0 = 0; b0 < K; b0 += B) {
+        // every lane's reads of the image have returned (their values were
+        // consumed by the walk) before LDS-DMA overwrites it
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (uint32_t k = 0; k < NCH; ++k) {
+            const uint32_t q = k * WAVE + lane;
+            const uint32_t cp = q / NCH2, c = q - cp * NCH2;
+            const uint32_t j = b0 + cp;
+            const uint32_t src = nth_set_bit(m, j < K ? j : K - 1u);
+            const uint32_t np = (uint32_t)__shfl((int)nch2, (int)src);
+            const int64_t bp = (int64_t)__shfl((long long)base, (int)src);
+            if (j < K && c < np) stage16(arena + bp + 16u * c, wimg + k * WAVE * 4u, false);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (miss && rank >= b0 && rank < b0 + B) {
+            Frame<NCH2> f2{(const lds_u32*)wimg, rank - b0, sh, take2, len, fr.g};
+            walk<CHAIN, false>(f2, r, nullptr, nullptr);
+        }
+    }
+}
+
+template <uint32_t NCH, int LAYOUT, int CHAIN, int MODE, class ARGS, int SLOW = 0>
 __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
     const ParseArgs& a = base_args(args);
     constexpr bool TUN = CHAIN == INGOT_CHAIN_GENEVE_OVER_V6;
@@ -1096,8 +1175,10 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
+        static_assert(!SLOW || (LAYOUT == LAYOUT_INDEXED && MODE == OUT_REC16),
+                      "the compacted slow path is built for indexed 16-B records");
         using FR = typename std::conditional<LAYOUT == LAYOUT_SEGMENTED, SegFrame<NCH>,
-                                             Frame<NCH>>::type;
+                                             Frame<NCH, SLOW != 0>>::type;
         FR fr;
         fr.win = (const lds_u32*)wimg;
         fr.p = lane;
@@ -1170,6 +1251,8 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
             }
         } else {
             walk<CHAIN, false>(fr, r, nullptr, nullptr);
+            if constexpr (SLOW)
+                slow_rewalk<NCH, CHAIN>(fr, r, valid, wimg, lane, a.arena, base, sh, len);
             if (valid) store_rec(static_cast<uint4*>(a.out) + i, pack(r), a.policy & 2u);
         }
         if constexpr (LAYOUT == LAYOUT_SEGMENTED) {
@@ -1427,7 +1510,7 @@ uint32_t resident_per_cu(K kernel) {
 
 // persist_cus != 0: a persistent grid, capped at the blocks the device holds
 // at once (cus x resident_per_cu), so no CU runs a second partial round.
-template <uint32_t NCH, int LAYOUT, int MODE, class ARGS>
+template <uint32_t NCH, int LAYOUT, int MODE, class ARGS, int SLOW = 0>
 hipError_t launch_chain(const ARGS& a, int chain, uint32_t grid, hipStream_t s,
                         uint32_t persist_cus = 0) {
     auto go = [&](auto kernel) {
@@ -1440,19 +1523,19 @@ hipError_t launch_chain(const ARGS& a, int chain, uint32_t grid, hipStream_t s,
     };
     switch (chain) {
     case INGOT_CHAIN_UDP_PARSER:
-        go(k_parse<NCH, LAYOUT, INGOT_CHAIN_UDP_PARSER, MODE, ARGS>);
+        go(k_parse<NCH, LAYOUT, INGOT_CHAIN_UDP_PARSER, MODE, ARGS, SLOW>);
         break;
     case INGOT_CHAIN_GENERIC_ULP:
-        go(k_parse<NCH, LAYOUT, INGOT_CHAIN_GENERIC_ULP, MODE, ARGS>);
+        go(k_parse<NCH, LAYOUT, INGOT_CHAIN_GENERIC_ULP, MODE, ARGS, SLOW>);
         break;
     case INGOT_CHAIN_VLAN_ULP:
-        go(k_parse<NCH, LAYOUT, INGOT_CHAIN_VLAN_ULP, MODE, ARGS>);
+        go(k_parse<NCH, LAYOUT, INGOT_CHAIN_VLAN_ULP, MODE, ARGS, SLOW>);
         break;
     default:
         if constexpr (MODE == OUT_REC8) {
             return hipErrorInvalidValue;  // not offered for the tunnel (api.cpp)
         } else {
-            go(k_parse<NCH, LAYOUT, INGOT_CHAIN_GENEVE_OVER_V6, MODE, ARGS>);
+            go(k_parse<NCH, LAYOUT, INGOT_CHAIN_GENEVE_OVER_V6, MODE, ARGS, SLOW>);
         }
         break;
     }
@@ -1567,6 +1650,11 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
         default: return launch_mode<5, LAYOUT_PACKED>(a, chain, mode, g, s);
         }
     }
+    // The compacted slow path (INGOT_TUNE_SLOW_PATH = 1, 16-B records,
+    // device arenas): default windows only.
+    if (t.slow_path == 1 && mode == OUT_REC16 && !host && !t.window_indexed)
+        return tun ? launch_chain<8, LAYOUT_INDEXED, OUT_REC16, ParseArgs, 1>(a, chain, g, s)
+                   : launch_chain<3, LAYOUT_INDEXED, OUT_REC16, ParseArgs, 1>(a, chain, g, s);
     switch (t.window_indexed ? t.window_indexed : tun ? 8 : host ? 5 : 3) {
     case 100: return launch_mode<0, LAYOUT_INDEXED>(a, chain, mode, g, s);
     case 2: return launch_mode<2, LAYOUT_INDEXED>(a, chain, mode, g, s);
@@ -1681,6 +1769,8 @@ bool tuning_valid(int key, int value) {
         return value == 0 || value == 16 || value == 32 || value == 64;
     case INGOT_TUNE_FLOW_TABLE:
         return value == 0 || value == 16 || value == 32;
+    case INGOT_TUNE_SLOW_PATH:
+        return value == 0 || value == 1;
     default:
         return false;
     }

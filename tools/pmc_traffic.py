@@ -26,12 +26,13 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 
 
-def run_pass(counter: str, config: str, outdir: Path, steps: int) -> list[float]:
+def run_pass(counter: str, config: str, outdir: Path, steps: int, extra=()) -> list[float]:
     d = outdir / counter.lower()
     d.mkdir(parents=True, exist_ok=True)
     cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", str(d), "-o", "run",
            "--", sys.executable, str(ROOT / "bench.py"), "--config", config, "--steps", str(steps),
-           "--warmup", "2", "--streams", "1", "--no-cpu-baseline", "--no-variants", "--no-gate"]
+           "--warmup", "2", "--streams", "1", "--no-cpu-baseline", "--no-variants", "--no-gate",
+           *extra]
     env = dict(os.environ, TMPDIR="/tmp")
     r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=180)
     (d / "rocprof.log").write_text(r.stdout + "\n" + r.stderr)
@@ -70,10 +71,15 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--tag", default="r02")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--tune", action="append", default=[],
+                    help="bench.py --tune KEY=VALUE for a variant; its file is named "
+                         "<tag>_pmc_<config>@<key>=<value>.json (never attached to a bench line)")
     args = ap.parse_args()
-    out = ROOT / "gpurun_out" / f"pmc_{args.config}"
-    fetch = run_pass("FETCH_SIZE", args.config, out, args.steps)
-    write = run_pass("WRITE_SIZE", args.config, out, args.steps)
+    extra = [x for kv in args.tune for x in ("--tune", kv)]
+    suffix = "".join(f"@{kv}" for kv in args.tune)
+    out = ROOT / "gpurun_out" / f"pmc_{args.config}{suffix}"
+    fetch = run_pass("FETCH_SIZE", args.config, out, args.steps, extra)
+    write = run_pass("WRITE_SIZE", args.config, out, args.steps, extra)
     # the first dispatches include the generator's and the algorithmic-bytes
     # pass: keep the timed ones (all k_parse dispatches are the same launch)
     f_kib = sorted(fetch)[len(fetch) // 2]
@@ -95,7 +101,8 @@ def main():
         "traffic_bytes_per_launch": f_kib * 1024 * 2 + w_kib * 1024,
         "correction": "FETCH_SIZE x2 on gfx950 (MI355X_MICROARCH.md:298)",
     }
-    prof = ROOT / "profiles" / f"{args.tag}_pmc_{args.config}.json"
+    res["tune"] = args.tune
+    prof = ROOT / "profiles" / f"{args.tag}_pmc_{args.config}{suffix}.json"
     prof.write_text(json.dumps(res, indent=1) + "\n")
     (ROOT / "gpurun_out" / prof.name).write_text(json.dumps(res, indent=1) + "\n")
     print(json.dumps(res))
