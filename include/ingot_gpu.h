@@ -415,6 +415,14 @@ void ingot_gpu_doorbell_destroy(ingot_gpu_doorbell* db);
  *                              lanes whose chain outruns the window, re-stage
  *                              a window twice as large for just those frames
  *                              (compacted) and walk them again
+ *   INGOT_TUNE_READ_PLAN       ingot_gpu_parse_read (16-B records): 16-B
+ *                              pieces staged in LDS for each of a packet's
+ *                              first four chunks (a packet's last chunk, the
+ *                              payload, is never staged): 0 / 1 =
+ *                              {4,0,0,0} (default), 2 = {2,2,2,0}, 3 =
+ *                              {4,2,2,0}, 4 = {4,1,1,0}; 9 = no descriptor
+ *                              prefetch: chunk 0 staged, later chunks'
+ *                              descriptors and bytes read on demand
  */
 #define INGOT_TUNE_WINDOW_INDEXED 1
 #define INGOT_TUNE_WINDOW_STRIDED 2
@@ -425,6 +433,7 @@ void ingot_gpu_doorbell_destroy(ingot_gpu_doorbell* db);
 #define INGOT_TUNE_WRITEBACK 7
 #define INGOT_TUNE_FLOW_TABLE 8
 #define INGOT_TUNE_SLOW_PATH 9
+#define INGOT_TUNE_READ_PLAN 10
 int ingot_gpu_ctx_set_tuning(ingot_gpu_ctx* ctx, int key, int value);
 int ingot_gpu_ctx_get_tuning(const ingot_gpu_ctx* ctx, int key);
 

@@ -79,6 +79,7 @@ TUNE_PIPE_DEPTH = 6
 TUNE_WRITEBACK = 7
 TUNE_FLOW_TABLE = 8
 TUNE_SLOW_PATH = 9
+TUNE_READ_PLAN = 10
 
 
 class IngotRec(ctypes.Structure):

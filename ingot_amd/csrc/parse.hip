@@ -254,6 +254,82 @@ struct SegFrame : Frame<NCH> {
     }
 };
 
+// parse_read with the header chunks staged (k_parse_read): the first four
+// chunks' descriptors are loaded up front; chunk 0 gets CS0 16-B slots per
+// packet (packet-major, like a frame's window: a packet's pieces sit side by
+// side, so the wave's requests for one frame coalesce) and each later chunk
+// e < 4 that is not the packet's last one gets CS_e pieces in planes (plane
+// π holds that piece of all 64 packets: one LDS-DMA instruction per piece
+// for the whole wave).  A packet's last chunk is taken to hold the payload
+// (an mblk chain's tail) and is read on demand like chunks past the fourth.
+// Offsets are logical as in SegFrame; `len` is the current chunk's end.
+template <int CS0, int CS1, int CS2, int CS3>
+struct SegFrameP {
+    static constexpr bool kRead = true;
+    static constexpr bool kProbe = false;
+    const lds_u32* win;  // this wave's image: 64 x CS0 slots, then the planes
+    uint32_t p;          // lane
+    uint32_t L, len;     // current chunk: logical [L, len)
+    uint32_t plane, sh, avail;  // its first plane (chunks >= 1), start in it, staged bytes
+    const uint8_t* g;    // g[i] = logical byte i of the current chunk
+    const uint8_t* arena;
+    const uint64_t* seg_off;
+    const uint16_t* seg_len;
+    uint32_t s0, k, nseg;
+    uint64_t o0, o1, o2, o3;  // the first four chunks' offsets and lengths
+    uint32_t l0, l1, l2, l3;
+
+    static constexpr uint32_t cs(uint32_t e) {
+        return e == 0 ? CS0 : e == 1 ? CS1 : e == 2 ? CS2 : e == 3 ? CS3 : 0;
+    }
+    static constexpr uint32_t pb(uint32_t e) {  // first plane of chunk e >= 1
+        return e == 1 ? 0 : e == 2 ? CS1 : CS1 + CS2;
+    }
+    // staged chunk-relative byte b of the current chunk: a dword of the image
+    __device__ __forceinline__ uint32_t dw(uint32_t b) const {
+        const uint32_t c = b >> 4;
+        const uint32_t slot = k == 0 ? slot_of<CS0>(p, c) : WAVE * (CS0 + plane + c) + p;
+        return win[slot * 4u + ((b >> 2) & 3u)];
+    }
+    __device__ __forceinline__ uint32_t be(uint32_t i, uint32_t n) const {
+        const uint32_t x0 = i - L;
+        if (x0 + n <= avail) {
+            const uint32_t b = sh + x0;
+            const uint32_t a = b & ~3u;
+            const uint32_t d0 = dw(a);
+            const uint32_t d1 = ((b & 3u) + n > 4u) ? dw(a + 4u) : 0u;
+            return __builtin_bswap32(__builtin_amdgcn_alignbyte(d1, d0, b & 3u)) >> (32u - 8u * n);
+        }
+        uint32_t v = 0;
+        for (uint32_t j = 0; j < n; ++j) v = (v << 8) | g[i + j];
+        return v;
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t hdr, Field f) const {
+        return (be(hdr + f.byte0(), f.nbytes()) >> f.rshift()) & f.mask();
+    }
+    __device__ __forceinline__ bool more() const { return k + 1 < nseg; }
+    // chunk e's staged pieces: chunk 0 always; later ones unless last
+    __device__ __forceinline__ static uint32_t staged(uint32_t e, uint32_t nseg) {
+        return e == 0 ? CS0 : (e + 1 < nseg ? cs(e) : 0u);
+    }
+    __device__ __forceinline__ void enter(uint64_t o, uint32_t l, uint32_t pl, uint32_t c) {
+        g = arena + o - L;
+        const uint32_t e = L + l;
+        len = e > 65535u ? 65535u : e;  // record offsets are u16
+        plane = pl;
+        sh = (uint32_t)((uintptr_t)(arena + o) & 15u);
+        avail = c ? (l < 16u * c - sh ? l : 16u * c - sh) : 0u;
+    }
+    __device__ __forceinline__ void advance() {
+        ++k;
+        L = len;
+        if (k == 1) enter(o1, l1, pb(1), staged(1, nseg));
+        else if (k == 2) enter(o2, l2, pb(2), staged(2, nseg));
+        else if (k == 3) enter(o3, l3, pb(3), staged(3, nseg));
+        else enter(seg_off[s0 + k], seg_len[s0 + k], 0u, 0u);
+    }
+};
+
 struct Rec {
     uint32_t status, err_layer, l3_kind, l4_kind, n_vlan, n_v6ext, l4_proto, flags;
     uint32_t l3_off, l4_off, payload_off, ethertype;
@@ -1263,6 +1339,131 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
     }
 }
 
+// parse_read over chunk lists with the header chunks staged (SegFrameP): per
+// tile, the packets' chunk bounds and the first four chunks' descriptors are
+// loaded together (independent loads), chunk 0 is staged packet-major like a
+// frame window, the later non-final chunks plane by plane, then the walk —
+// no dependent descriptor or byte load for headers inside staged pieces.
+// One 64-packet tile per wave.
+template <int CS0, int CS1, int CS2, int CS3, int CHAIN, int MODE>
+__global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
+    using FR = SegFrameP<CS0, CS1, CS2, CS3>;
+    constexpr uint32_t P = CS0 + CS1 + CS2 + CS3;
+    constexpr uint32_t WAVE_DW = WAVE * P * 4u;
+    constexpr bool TUN = CHAIN == INGOT_CHAIN_GENEVE_OVER_V6;
+    __shared__ __attribute__((aligned(16))) uint32_t s_win[WAVES * WAVE_DW + 16];
+    const uint32_t lane = threadIdx.x & (WAVE - 1u);
+    const uint32_t wave = threadIdx.x / WAVE;
+    uint32_t* wimg = s_win + wave * WAVE_DW;
+    const uint64_t ntiles = (a.n + WAVE - 1u) / WAVE;
+    for (uint64_t t = (uint64_t)blockIdx.x * WAVES + wave; t < ntiles;
+         t += (uint64_t)gridDim.x * WAVES) {
+        const uint64_t i = t * WAVE + lane;
+        const bool valid = i < a.n;
+        const uint32_t s0 = valid ? a.pkt_seg[i] : 0u;
+        const uint32_t nseg = valid ? a.pkt_seg[i + 1] - s0 : 0u;
+        FR fr;
+        fr.o0 = nseg > 0 ? a.off[s0] : 0u;
+        fr.o1 = nseg > 1 ? a.off[s0 + 1] : 0u;
+        fr.o2 = nseg > 2 ? a.off[s0 + 2] : 0u;
+        fr.o3 = nseg > 3 ? a.off[s0 + 3] : 0u;
+        fr.l0 = nseg > 0 ? a.len[s0] : 0u;
+        fr.l1 = nseg > 1 ? a.len[s0 + 1] : 0u;
+        fr.l2 = nseg > 2 ? a.len[s0 + 2] : 0u;
+        fr.l3 = nseg > 3 ? a.len[s0 + 3] : 0u;
+        // chunk 0, packet-major: instruction k, lane L fills slot 64k + L =
+        // packet q / CS0, piece (q mod CS0) ^ swz (16-B aligned absolute
+        // addresses; pieces only below the chunk's end)
+        const uint32_t sh0 = (uint32_t)((uintptr_t)(a.arena + fr.o0) & 15u);
+        const uint32_t n0 = nseg ? (sh0 + (fr.l0 < 16u * CS0 - sh0 ? fr.l0 : 16u * CS0 - sh0) +
+                                    15u) >> 4
+                                 : 0u;
+        const int64_t base0 = (int64_t)fr.o0 - (int64_t)sh0;
+#pragma unroll
+        for (uint32_t k = 0; k < (uint32_t)CS0; ++k) {
+            const uint32_t q = k * WAVE + lane;
+            const uint32_t pp = q / CS0;
+            const uint32_t c = (q - pp * CS0) ^ swz<CS0>(pp);
+            const uint32_t np = (uint32_t)__shfl((int)n0, (int)pp);
+            const int64_t bp = (int64_t)__shfl((long long)base0, (int)pp);
+            if (c < np) stage16(a.arena + bp + 16u * c, wimg + k * WAVE * 4u, false);
+        }
+        // chunks 1..3 unless last: piece j of chunk e into plane CS0 + pb(e) + j
+        auto stage_chunk = [&](uint32_t e, uint64_t o, uint32_t l) {
+            const uint32_t sh = (uint32_t)((uintptr_t)(a.arena + o) & 15u);
+            const uint32_t c = FR::staged(e, nseg);
+            for (uint32_t j = 0; j < FR::cs(e); ++j)
+                if (j < c && 16u * j < sh + l)
+                    stage16(a.arena + o - sh + 16u * j,
+                            wimg + (CS0 + FR::pb(e) + j) * WAVE * 4u, false);
+        };
+        if constexpr (CS1 > 0) stage_chunk(1, fr.o1, fr.l1);
+        if constexpr (CS2 > 0) stage_chunk(2, fr.o2, fr.l2);
+        if constexpr (CS3 > 0) stage_chunk(3, fr.o3, fr.l3);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+        fr.win = (const lds_u32*)wimg;
+        fr.p = lane;
+        fr.arena = a.arena;
+        fr.seg_off = a.off;
+        fr.seg_len = a.len;
+        fr.s0 = s0;
+        fr.k = 0;
+        fr.nseg = nseg;
+        fr.L = 0;
+        fr.enter(fr.o0, fr.l0, 0u, nseg ? CS0 : 0u);
+        Rec r;
+        if constexpr (MODE == OUT_FIELDS) {
+            using OutT = typename std::conditional<TUN, ingot_geneve_fields, ingot_fields>::type;
+            OutT* G = static_cast<OutT*>(a.out) + (valid ? i : 0);
+            if (valid) {
+                uint4* z = reinterpret_cast<uint4*>(G);
+#pragma unroll
+                for (int k = 0; k < (int)(sizeof(OutT) / 16); ++k) z[k] = make_uint4(0, 0, 0, 0);
+                ingot_fields* F;
+                ingot_tunnel_fields* T = nullptr;
+                if constexpr (TUN) {
+                    F = &G->inner;
+                    T = &G->outer;
+                } else {
+                    F = G;
+                }
+                walk<CHAIN, true>(fr, r, F, T);
+                reinterpret_cast<uint4*>(F)[0] = pack(r);
+            }
+        } else {
+            walk<CHAIN, false>(fr, r, nullptr, nullptr);
+            if (valid) store_rec(static_cast<uint4*>(a.out) + i, pack(r), a.policy & 2u);
+        }
+        if (valid && a.chunk) a.chunk[i] = (uint16_t)fr.k;
+        // the next tile's LDS-DMA overwrites this image: every lane's reads
+        // above have returned (their values were consumed by the stores)
+    }
+}
+
+template <int CS0, int CS1, int CS2, int CS3, int MODE>
+hipError_t launch_read(const ParseArgs& a, int chain, uint32_t grid, hipStream_t s) {
+    switch (chain) {
+    case INGOT_CHAIN_UDP_PARSER:
+        hipLaunchKernelGGL((k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_UDP_PARSER, MODE>),
+                           dim3(grid), dim3(BLOCK), 0, s, a);
+        break;
+    case INGOT_CHAIN_GENERIC_ULP:
+        hipLaunchKernelGGL((k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENERIC_ULP, MODE>),
+                           dim3(grid), dim3(BLOCK), 0, s, a);
+        break;
+    case INGOT_CHAIN_VLAN_ULP:
+        hipLaunchKernelGGL((k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_VLAN_ULP, MODE>),
+                           dim3(grid), dim3(BLOCK), 0, s, a);
+        break;
+    default:
+        hipLaunchKernelGGL((k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENEVE_OVER_V6, MODE>),
+                           dim3(grid), dim3(BLOCK), 0, s, a);
+        break;
+    }
+    return hipGetLastError();
+}
+
 // Pipelined variant for fixed slots with no length array (C2-style rings):
 // each wave walks several tiles and keeps the next DEPTH-1 tiles' LDS-DMA in
 // flight while it parses the current one (DEPTH LDS images per wave, used
@@ -1586,9 +1787,26 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
     // parse_read over chunk lists: chunk 0 staged in a 4-chunk (64-B) window
     // (first mblk-style chunks are short header blocks), the rest from L2/HBM.
     if (layout_kind == LAYOUT_SEGMENTED) {
-        if (mode == OUT_FIELDS) return launch_chain<4, LAYOUT_SEGMENTED, OUT_FIELDS>(a, chain, g, s);
-        if (mode == OUT_REC16) return launch_chain<4, LAYOUT_SEGMENTED, OUT_REC16>(a, chain, g, s);
-        return hipErrorInvalidValue;
+        if (mode != OUT_FIELDS && mode != OUT_REC16) return hipErrorInvalidValue;
+        // INGOT_TUNE_READ_PLAN: 16-B pieces staged per chunk of the first four.
+        // Measured (tools/abtune.py, us per launch): the
+        // reference's one-header-per-chunk shape (c2r, 1 M) 33.3 on demand
+        // (9) / 25.1 {4,0,0,0} / 24.2 {2,2,2,0} / 27.0 {4,2,2,0}; header +
+        // payload chunks (c3r, 16.7 M) 651 / 667 / 681 / 769 — extra planes
+        // cost occupancy on the gather-bound shape.  Default {4,0,0,0}: the
+        // descriptor prefetch (no dependent descriptor loads) at the legacy
+        // kernel's LDS footprint.
+        if (t.read_plan == 9) {
+            return mode == OUT_FIELDS ? launch_chain<4, LAYOUT_SEGMENTED, OUT_FIELDS>(a, chain, g, s)
+                                      : launch_chain<4, LAYOUT_SEGMENTED, OUT_REC16>(a, chain, g, s);
+        }
+        if (mode == OUT_FIELDS) return launch_read<4, 0, 0, 0, OUT_FIELDS>(a, chain, g, s);
+        switch (t.read_plan) {
+        case 2: return launch_read<2, 2, 2, 0, OUT_REC16>(a, chain, g, s);
+        case 3: return launch_read<4, 2, 2, 0, OUT_REC16>(a, chain, g, s);
+        case 4: return launch_read<4, 1, 1, 0, OUT_REC16>(a, chain, g, s);
+        default: return launch_read<4, 0, 0, 0, OUT_REC16>(a, chain, g, s);
+        }
     }
     // Staged window (16-B chunks per frame); defaults measured on MI355X with
     // interleaved A/B in one process (tools/abtune.py):
@@ -1771,6 +1989,8 @@ bool tuning_valid(int key, int value) {
         return value == 0 || value == 16 || value == 32;
     case INGOT_TUNE_SLOW_PATH:
         return value == 0 || value == 1;
+    case INGOT_TUNE_READ_PLAN:
+        return (value >= 0 && value <= 4) || value == 9;
     default:
         return false;
     }

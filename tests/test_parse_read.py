@@ -147,3 +147,63 @@ def test_read_single_chunk_matches_parse(ctx, torch):
     torch.cuda.synchronize()
     assert torch.equal(recs, want)
     assert int(chunk.abs().max()) == 0
+
+
+def split_many(frames, seed):
+    """Cut every frame into 1-8 chunks (many short ones: every header in its
+    own chunk, chunks past the fourth, empty chunks)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for f in frames:
+        k = int(rng.integers(0, 8))
+        cuts = sorted(min(int(rng.choice(EDGES)) if rng.random() < 0.7
+                          else int(rng.integers(0, len(f) + 1)), len(f)) for _ in range(k))
+        bounds = [0] + cuts + [len(f)]
+        out.append([f[a:b] for a, b in zip(bounds, bounds[1:])])
+    return out
+
+
+@pytest.mark.parametrize("plan", [0, 2, 3, 4, 9])
+def test_every_read_plan_is_bit_exact(torch, plan):
+    """INGOT_TUNE_READ_PLAN: how many 16-B pieces of each of the first four
+    chunks are staged in LDS never changes a record, a field block or the
+    remainder's chunk index (1-8 chunks per packet, every chain)."""
+    from ingot_amd.abi import TUNE_READ_PLAN
+
+    c = ingot_amd.Context(0)
+    c.set_tuning(TUNE_READ_PLAN, plan)
+    for chain in Chain:
+        prof = GenProfile.GENEVE_ADVERSARIAL if chain == TUN else GenProfile.ADVERSARIAL
+        frames = frames_of(prof, 15_000, seed=81 + int(chain))
+        frames += frames_of(GenProfile.GENEVE if chain == TUN else GenProfile.VLAN_V6EH, 10_000,
+                            seed=91)
+        packets = split_many(frames, seed=plan * 7 + int(chain))
+        kind = "geneve" if chain == TUN else "fields"
+        out, recs, chunk, segs = run_device(c, torch, packets, chain, kind)
+        w_rec, w_fld, w_chunk = oracle.parse_read_batch(*segs, chain, fields=kind)
+        n = len(packets)
+        bad = np.nonzero((recs.reshape(n, 16) != w_rec.view(np.uint8).reshape(n, 16)).any(1))[0]
+        assert bad.size == 0, (chain, bad[:5], [len(x) for x in packets[bad[0]]])
+        width = w_fld.dtype.itemsize
+        fb = np.nonzero((out.reshape(n, width) != w_fld.view(np.uint8).reshape(n, width))
+                        .any(1))[0]
+        assert fb.size == 0, (chain, fb[:5])
+        assert np.array_equal(chunk, w_chunk)
+
+
+def test_reference_bench_shape(ctx, torch):
+    """The reference's parse-read-v4 shape (ingot-examples/benches/packet.rs:
+    130-134): one chunk per header, 14 / 20 / 8 B, then the payload, over the
+    C2 frames; records equal the oracle's, the walk ends in the exhausted
+    UDP chunk (index 2) and the payload chunk is left unread."""
+    n = 20_000
+    arena, _, _ = ingot_amd.gen_frames(GenProfile.V4UDP64, n, stride=64)
+    a = arena.cpu().numpy()
+    packets = [[a[64 * i:64 * i + 14].tobytes(), a[64 * i + 14:64 * i + 34].tobytes(),
+                a[64 * i + 34:64 * i + 42].tobytes(), a[64 * i + 42:64 * i + 64].tobytes()]
+               for i in range(n)]
+    _, recs, chunk, segs = run_device(ctx, torch, packets, Chain.UdpParser, "fields")
+    w_rec, _, w_chunk = oracle.parse_read_batch(*segs, Chain.UdpParser)
+    assert recs.tobytes() == w_rec.tobytes()
+    assert np.array_equal(chunk, w_chunk) and (w_chunk == 2).all()
+    assert (w_rec["status"] == 0).all()

@@ -7,7 +7,7 @@ cross-process/device variance that looks like a kernel property).
     python tools/abtune.py --config c2 --var streams=1 --var streams=2 --var rec=8
 
 A variant is a comma list of key=value: win_i, win_s, blocks, pipe, depth, pol,
-wb, ftab, slow, streams, rec, mode (parse|flows|modify: the runner; default the config's).
+wb, ftab, slow, plan, streams, rec, mode (parse|flows|modify: the runner; default the config's).
 """
 from __future__ import annotations
 
@@ -37,7 +37,8 @@ def main():
     from ingot_amd import Chain, GenProfile
     from ingot_amd.abi import (TUNE_CACHE_POLICY, TUNE_MAX_BLOCKS, TUNE_PIPE_DEPTH,
                                TUNE_PIPELINE, TUNE_WINDOW_INDEXED, TUNE_WINDOW_STRIDED,
-                               TUNE_WRITEBACK, TUNE_FLOW_TABLE, TUNE_SLOW_PATH)
+                               TUNE_WRITEBACK, TUNE_FLOW_TABLE, TUNE_SLOW_PATH,
+                               TUNE_READ_PLAN)
 
     prof, n, stride, chain_name, _ = bench.CONFIGS[args.config]
     chain = Chain[chain_name]
@@ -48,6 +49,16 @@ def main():
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(3)]
     lib = ingot_amd.load_library()
     steps = args.steps or max(20, int(2e5 / max(1, n / 1e4)))
+    segs = None
+    if bench.MODES.get(args.config) == "read":
+        c0 = ingot_amd.Context(0)
+        recs0 = ingot_amd.records_to_numpy(
+            c0.parse_strided(arena, stride, n, chain) if stride is not None else
+            c0.parse(arena, off, lens, chain))
+        rl = (lens if lens is not None else
+              torch.full((n,), stride, dtype=torch.int32, device="cuda").to(torch.uint16))
+        segs = bench.read_chunks(torch, off, stride, rl.to(torch.int32), recs0,
+                                 bench.READ_CHUNKS[args.config], "cuda")[:3]
     variants = args.var or ["win_i=5"]
     runners = {}
     for v in variants:
@@ -71,6 +82,8 @@ def main():
             ctx.set_tuning(TUNE_FLOW_TABLE, int(kv["ftab"]))
         if "slow" in kv:
             ctx.set_tuning(TUNE_SLOW_PATH, int(kv["slow"]))
+        if "plan" in kv:
+            ctx.set_tuning(TUNE_READ_PLAN, int(kv["plan"]))
         ns, rb = int(kv.get("streams", 1)), int(kv.get("rec", 16))
         mode = kv.get("mode", bench.MODES.get(args.config, "parse"))
         if mode == "flows":
@@ -79,6 +92,8 @@ def main():
             fids = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(reps)]
             r = bench.FlowRunner(torch, lib, ctx, chain, n, arenas, off, lens, hists, fids,
                                  streams[:ns], lambda h: None)
+        elif mode == "read":
+            r = bench.ReadRunner(torch, lib, ctx, chain, n, arenas, *segs, outs, streams[:ns])
         elif mode == "packed":
             r = bench.PackedRunner(torch, lib, ctx, chain, n, arenas, lens, outs, streams[:ns])
         elif mode == "modify":
