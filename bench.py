@@ -112,20 +112,24 @@ def algorithmic_bytes(recs_np, lens_np, stride, descriptor_bytes, record_bytes):
     return int(r.sum()), record_bytes * len(recs_np)
 
 
-def host_inclusive(config: str):
-    """The host-inclusive rates of this config (frames start and end in host
-    memory), from the committed tools/hostpath.py measurement — reported
-    beside `value`, never as it."""
-    f = sorted(ROOT.glob("profiles/*_hostpath.json"))
-    if not f:
-        return None
-    d = json.loads(f[-1].read_text())
-    if config not in d:
-        return None
-    out = {"memcpy_Mpkt_s": d[config]["host_inclusive_Mpkt_s"],
-           "source": f"{f[-1].relative_to(ROOT)} (tools/hostpath.py, 1 M frames per batch)"}
-    if f"{config}_zc" in d:
-        out["zero_copy_Mpkt_s"] = d[f"{config}_zc"]["host_inclusive_Mpkt_s"]
+def host_inclusive_live(torch, ingot_amd, ctx, arena, off, lens, stride, chain, n, steps=30):
+    """The path as it starts and ends in host memory, measured in this run
+    on the first min(n, 1 M) frames of the batch (tools/hostpath.py:measure):
+    a pinned host ring -> hipMemcpyAsync H2D -> parse -> records D2H, and the
+    zero-copy form (ring and records mapped for the device, the kernels read
+    only the header bytes across PCIe).  Reported beside `value`, never as it."""
+    sys.path.insert(0, str(ROOT / "tools"))
+    import hostpath
+
+    m = min(n, 1 << 20)
+    out = {"frames_per_batch": m, "streams": 3}
+    for zc in (False, True):
+        r = hostpath.measure(torch, ingot_amd, ctx, arena, off, lens, stride, chain, m,
+                             streams=3, steps=steps, zero_copy=zc)
+        key = "zero_copy" if zc else "memcpy"
+        out[f"{key}_Mpkt_s"] = r["host_inclusive_Mpkt_s"]
+        out[f"{key}_ms_per_batch"] = r["ms_per_batch"]
+    out["source"] = "measured in this run (tools/hostpath.py: measure)"
     return out
 
 
@@ -605,6 +609,8 @@ def main():
     ap.add_argument("--record", type=int, default=16, choices=(16, 8))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true",
+                    help="skip the live host-inclusive (PCIe) measurement")
     ap.add_argument("--no-gate", action="store_true",
                     help="time from host submission (no doorbell-held first launches)")
     ap.add_argument("--plan", action="store_true",
@@ -836,6 +842,12 @@ def main():
                 "hbm_GBps": round(bpl / (ms / vsteps / 1e3) / 1e9, 1),
             }
 
+    host_path = None
+    if (world == 1 and mode == "parse" and args.record == 16 and not args.no_host_path
+            and not args.tune):
+        host_path = host_inclusive_live(torch, ingot_amd, ctx, arenas[0], off, lens, stride,
+                                        chain, n)
+
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -914,7 +926,7 @@ def main():
             "variants": variants,
             "cpu_baseline": cpu,
             "wall_s_timed_region": round(wall, 4),
-            "host_inclusive": host_inclusive(args.config),
+            "host_inclusive": host_path,
         }
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -32,6 +32,7 @@ def run_pass(counter: str, config: str, outdir: Path, steps: int, extra=()) -> l
     cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", str(d), "-o", "run",
            "--", sys.executable, str(ROOT / "bench.py"), "--config", config, "--steps", str(steps),
            "--warmup", "2", "--streams", "1", "--no-cpu-baseline", "--no-variants", "--no-gate",
+           "--no-host-path",
            *extra]
     env = dict(os.environ, TMPDIR="/tmp")
     r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=180)

@@ -20,7 +20,7 @@ for cfg in $cfgs; do
     cp gpurun_out/${tag}_pmc_$cfg.json profiles/ 2>/dev/null
     (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
         -d $R/gpurun_out/prof_$cfg -o run -- python3 $R/bench.py --config $cfg --streams 1 \
-        --steps 100 --warmup 10 --no-cpu-baseline --no-variants --no-gate \
+        --steps 100 --warmup 10 --no-cpu-baseline --no-variants --no-gate --no-host-path \
         > $R/gpurun_out/prof_$cfg.log 2>&1) || exit $?
     f=$(find $R/gpurun_out/prof_$cfg -name "*kernel_stats.csv" | head -1)
     cp "$f" $R/gpurun_out/${tag}_${cfg}_streams1_kernel_stats.csv
