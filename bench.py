@@ -935,6 +935,8 @@ def main():
                 "write_bytes_per_launch": wr,
                 "read_frac": round(rd / (launch_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                 "frac_of_measured_copy_ceiling": round(achieved / HBM_MEASURED_GBS, 4),
+                "read_frac_of_measured_copy_ceiling": round(
+                    rd / (launch_ms / 1e3) / 1e9 / HBM_MEASURED_GBS, 4),
             },
             "ms_per_step_ungated": ungated,
             "variants": variants,

@@ -4,7 +4,9 @@ the sizes the pytest suite uses.  For every chain: records and every getter
 over N adversarial frames (every truncation / ihl / data_offset / EH / Geneve
 defect path), in the packed layout and in 256-B slots; flow ids and hashes
 for the VLAN chain.  Prints one JSON line with the mismatch counts (all must
-be 0) and writes it to gpurun_out/bigfuzz.json.
+be 0) and writes it to gpurun_out/bigfuzz.json.  Round 2 adds the compacted
+slow path, parse_read over random 4-chunk splits with every staging plan, and
+flow bins from the 16-bit table.
 
     python tools/bigfuzz.py [--frames 4000000] [--seed 1234]
 """
@@ -71,8 +73,54 @@ def main():
             print(chain.name, layout, res[f"{chain.name}/{layout}"], flush=True)
             del arena, off, lens, recs, flds
             torch.cuda.empty_cache()
+    # round 2 kernels: the compacted slow path, parse_read over random chunk
+    # splits with every staging plan, flow bins from the 16-bit table
+    from ingot_amd.abi import TUNE_READ_PLAN, TUNE_SLOW_PATH
+
+    for chain in Chain:
+        prof = (GenProfile.GENEVE_ADVERSARIAL if chain == Chain.GeneveOverV6Tunnel
+                else GenProfile.ADVERSARIAL)
+        arena, off, lens = ingot_amd.gen_frames(prof, n, seed=args.seed + 10 + int(chain))
+        a, o, ln = arena.cpu().numpy(), off.cpu().numpy(), lens.cpu().numpy()
+        w_rec = oracle.parse_batch(a, o, ln, chain, nthreads=16)
+        c1 = ingot_amd.Context(0)
+        c1.set_tuning(TUNE_SLOW_PATH, 1)
+        g = c1.parse(arena, off, lens, chain)
+        torch.cuda.synchronize()
+        bad = int((g.cpu().numpy().reshape(n, -1) != w_rec.view(np.uint8).reshape(n, -1))
+                  .any(axis=1).sum())
+        res[f"{chain.name}/slow_path"] = {"record_mismatches": bad}
+        print(chain.name, "slow_path", res[f"{chain.name}/slow_path"], flush=True)
+        # 4 chunks per packet at 3 sorted random cuts (empty chunks included)
+        rng = np.random.default_rng(args.seed + int(chain))
+        cuts = np.sort(rng.integers(0, ln.astype(np.int64)[:, None] + 1, size=(n, 3)), axis=1)
+        bounds = np.concatenate([np.zeros((n, 1), np.int64), cuts,
+                                 ln.astype(np.int64)[:, None]], axis=1)
+        seg_off = (o.astype(np.int64)[:, None] + bounds[:, :4]).reshape(-1)
+        seg_len = (bounds[:, 1:] - bounds[:, :4]).reshape(-1).astype(np.uint16)
+        pkt_seg = (np.arange(n + 1, dtype=np.int64) * 4).astype(np.uint32)
+        w_r, _, w_ch = oracle.parse_read_batch(a, seg_off.view(np.uint64), seg_len, pkt_seg,
+                                                chain, nthreads=16)
+        d_so = torch.from_numpy(seg_off).cuda()
+        d_sl = torch.from_numpy(seg_len.view(np.int16)).cuda()
+        d_ps = torch.from_numpy(pkt_seg.view(np.int32)).cuda()
+        for plan in (0, 2, 3, 9):
+            c2 = ingot_amd.Context(0)
+            c2.set_tuning(TUNE_READ_PLAN, plan)
+            r, ch = c2.parse_read(arena, d_so, d_sl, d_ps, chain)
+            torch.cuda.synchronize()
+            bad = int((r.cpu().numpy().reshape(n, -1) != w_r.view(np.uint8).reshape(n, -1))
+                      .any(axis=1).sum())
+            badc = int((ch.cpu().numpy().view(np.uint16) != w_ch).sum())
+            res[f"{chain.name}/parse_read_plan{plan}"] = {"record_mismatches": bad,
+                                                          "chunk_mismatches": badc}
+            print(chain.name, f"parse_read plan {plan}", res[f"{chain.name}/parse_read_plan{plan}"],
+                  flush=True)
+        del arena, off, lens, d_so, d_sl, d_ps
+        torch.cuda.empty_cache()
     # flows on the VLAN chain
     arena, off, lens = ingot_amd.gen_frames(GenProfile.FLOWS, n, seed=args.seed)
+    flow16 = ctx.flow_hist(arena, off, lens, Chain.VlanUlp)  # no hashes: the 16-bit table
     hashes = torch.zeros(n, dtype=torch.int32, device="cuda")
     flow = ctx.flow_hist(arena, off, lens, Chain.VlanUlp, hashes=hashes)
     torch.cuda.synchronize()
@@ -81,7 +129,8 @@ def main():
     w_flow = oracle.flow_hist.last_flows
     res["flows/VlanUlp"] = {
         "hash_mismatches": int((hashes.cpu().numpy().view(np.uint32) != w_hash).sum()),
-        "flow_mismatches": int((flow.cpu().numpy().view(np.uint32) != w_flow).sum())}
+        "flow_mismatches": int((flow.cpu().numpy().view(np.uint32) != w_flow).sum()),
+        "flow16_mismatches": int((flow16.cpu().numpy().view(np.uint32) != w_flow).sum())}
     print("flows", res["flows/VlanUlp"], flush=True)
     out = {"frames_per_case": n, "seed": args.seed, "wall_s": round(time.time() - t0, 1),
            "cases": res,
