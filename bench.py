@@ -473,13 +473,14 @@ def kernel_family(mode: str, ring: bool) -> str:
     return "k_parse_pipe" if ring else "k_parse"
 
 
-def pmc_for(config: str, family: str, sha: str):
-    """The newest profiles/*_pmc_<config>.json taken on these kernel sources
-    whose profiled kernel is `family`; None (with the reason) otherwise."""
+def pmc_for(config: str, family: str, sha: str, n: int):
+    """The newest profiles/*_pmc_<config>.json taken on these kernel sources,
+    over launches of n frames, whose profiled kernel is `family`; None
+    otherwise."""
     for f in sorted(ROOT.glob(f"profiles/*_pmc_{config}.json"), reverse=True):
         t = json.loads(f.read_text())
         k = t.get("kernel") or (t.get("kernels") or [""])[0]
-        if t.get("sources_sha") != sha:
+        if t.get("sources_sha") != sha or t.get("frames_per_launch") != n:
             continue
         if f"::{family}<" not in k and not k.startswith(f"{family}<"):
             continue
@@ -825,7 +826,7 @@ def main():
     family = kernel_family(mode, ring)
     sha = kernel_sources_sha()
     traffic = None
-    t, pf = (pmc_for(args.config, family, sha) if args.record == 16 and not args.tune
+    t, pf = (pmc_for(args.config, family, sha, n) if args.record == 16 and not args.tune
              else (None, None))
     if t is not None:
         traffic = {"bytes_per_launch": t["traffic_bytes_per_launch"],

@@ -94,6 +94,7 @@ def main():
         "config": args.config,
         "kernel": sorted(KERNELS)[0],
         "sources_sha": bench.kernel_sources_sha(),
+        "frames_per_launch": bench.CONFIGS[args.config][1],
         "dispatches": [len(fetch), len(write)],
         "FETCH_SIZE_KiB_median": f_kib,
         "WRITE_SIZE_KiB_median": w_kib,
