@@ -292,10 +292,12 @@ class ModifyRunner:
 
 
 class ReadRunner:
-    """parse_read over chunk lists: arena k % R with the shared segment tables."""
+    """parse_read over chunk lists: arena k % R with the shared segment tables
+    (dense: one (offset << 16) | length entry per chunk,
+    ingot_gpu_parse_read_dense)."""
 
     def __init__(self, torch, lib, ctx, chain, n, arenas, seg_off, seg_len, pkt_seg, outs,
-                 streams):
+                 streams, dense=False):
         self.torch, self.streams = torch, streams
         reps, h, c = len(arenas), ctx._h, int(chain)
         aptrs = [a.data_ptr() for a in arenas]
@@ -303,6 +305,12 @@ class ReadRunner:
         so, sl, ps = seg_off.data_ptr(), seg_len.data_ptr(), pkt_seg.data_ptr()
         sps = [s.cuda_stream for s in streams]
         ns = len(sps)
+        if dense:
+            self.seg = ((seg_off << 16) | (seg_len.to(torch.int32) & 0xFFFF).to(torch.int64))
+            sd = self.seg.data_ptr()
+            self.launch = lambda k: lib.ingot_gpu_parse_read_dense(
+                h, aptrs[k % reps], sd, ps, n, c, 0, outptrs[k % reps], None, sps[k % ns])
+            return
         self.launch = lambda k: lib.ingot_gpu_parse_read(h, aptrs[k % reps], so, sl, ps, n, c,
                                                          outptrs[k % reps], None, sps[k % ns])
 
@@ -726,7 +734,7 @@ def main():
         seg_off, seg_len, pkt_seg, head_chunks = read_chunks(
             torch, off, stride, rlens.to(torch.int32), recs0, READ_CHUNKS[args.config], dev)
 
-    def runner(nstreams, record, flows_only=False):
+    def runner(nstreams, record, flows_only=False, dense=False):
         if flows:
             return FlowRunner(torch, lib, ctx, chain, n, arenas, off, lens, hists, flow_ids,
                               streams[:nstreams], idist.reduce_histogram_async, flows_only)
@@ -738,7 +746,7 @@ def main():
                                 streams[:nstreams])
         if mode == "read":
             return ReadRunner(torch, lib, ctx, chain, n, arenas, seg_off, seg_len, pkt_seg,
-                              outs, streams[:nstreams])
+                              outs, streams[:nstreams], dense)
         return Runner(torch, lib, ctx, chain, n, stride, arenas, off, lens, outs,
                       streams[:nstreams], record)
 
@@ -855,6 +863,13 @@ def main():
                 "us_per_step": round(ms * 1e3 / vsteps, 3),
                 "hbm_GBps": round(bpl / (ms / vsteps / 1e3) / 1e9, 1),
             }
+        if mode == "read":  # the same chunks as one dense 8-B entry each
+            r = runner(args.streams, 16, dense=True)
+            r.run(min(args.warmup, 50))
+            ms, _ = r.run(vsteps, gate)
+            variants[f"streams{args.streams}_dense_table"] = {
+                "value": round(n * vsteps / (ms / 1e3) / 1e6, 2),
+                "us_per_step": round(ms * 1e3 / vsteps, 3)}
 
     host_path = None
     if (world == 1 and mode == "parse" and args.record == 16 and not args.no_host_path

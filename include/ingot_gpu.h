@@ -534,6 +534,17 @@ int ingot_gpu_geneve_fields_read(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
                                  const uint32_t* d_pkt_seg, uint64_t n,
                                  ingot_geneve_fields* d_out, uint16_t* d_chunk,
                                  void* stream);
+/*
+ * ingot_gpu_parse_read with a dense chunk table: one 8-byte entry per chunk,
+ * d_seg[k] = (offset << 16) | length (offset < 2^48), instead of the u64 and
+ * u16 arrays — one load per chunk descriptor and no padding between them.
+ * fields = 0: d_out holds ingot_rec records; 1: ingot_fields blocks (EINVAL
+ * for GENEVE_OVER_V6); 2: ingot_geneve_fields blocks (GENEVE_OVER_V6 only).
+ */
+int ingot_gpu_parse_read_dense(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
+                               const uint64_t* d_seg, const uint32_t* d_pkt_seg,
+                               uint64_t n, int chain, int fields, void* d_out,
+                               uint16_t* d_chunk, void* stream);
 
 /* ---------------------------------------------------------------------------
  * In-place header rewrite: ingot's generated setters (packet/mod.rs:2097-2255;

@@ -370,6 +370,32 @@ class Context:
         _lib.check(rc, "ingot_gpu_parse_read")
         return out, chunk
 
+    def parse_read_dense(self, arena, seg, pkt_seg, chain: Chain, out=None, chunk=None,
+                         fields: Optional[str] = None, stream=None):
+        """parse_read over a dense chunk table (ingot_gpu_parse_read_dense):
+        seg[k] = (offset << 16) | length as int64/uint64, one entry per
+        chunk; pkt_seg int32/uint32 with n+1 bounds.  Returns (out, chunk)
+        as parse_read does."""
+        torch = _torch()
+        n = pkt_seg.numel() - 1
+        width = {None: REC_BYTES, "fields": FIELDS_BYTES,
+                 "geneve": GENEVE_FIELDS_DTYPE.itemsize}[fields]
+        if out is None:
+            out = torch.empty((n, width), dtype=torch.uint8, device=arena.device)
+        if chunk is None:
+            chunk = torch.empty(n, dtype=torch.int16, device=arena.device)
+        self._arg("arena", arena, _U8)
+        self._arg("pkt_seg", pkt_seg, _U32, n + 1)
+        self._arg("seg", seg, _U64)
+        self._arg("out", out, _U8, n * width)
+        self._arg("chunk", chunk, _U16, n)
+        self._on_device(arena=arena, seg=seg, pkt_seg=pkt_seg, out=out, chunk=chunk)
+        mode = {None: 0, "fields": 1, "geneve": 2}[fields]
+        _lib.check(self._lib.ingot_gpu_parse_read_dense(
+            self._h, _ptr(arena), _ptr(seg), _ptr(pkt_seg), n, int(chain), mode, _ptr(out),
+            _ptr(chunk), _stream(stream, self.device)), "ingot_gpu_parse_read_dense")
+        return out, chunk
+
     def parse_modify(self, arena, off, lens, chain: Chain, edits, stride: int = 0,
                      n: Optional[int] = None, out=None, stream=None):
         """Parse, then rewrite header fields in place (ingot's setters):

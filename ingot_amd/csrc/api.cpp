@@ -409,6 +409,23 @@ int ingot_gpu_geneve_fields_read(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
                            stream);
 }
 
+int ingot_gpu_parse_read_dense(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_seg,
+                               const uint32_t* d_pkt_seg, uint64_t n, int chain, int fields,
+                               void* d_out, uint16_t* d_chunk, void* stream) {
+    if (!ctx || !chain_ok(chain) || fields < 0 || fields > 2) return INGOT_GPU_EINVAL;
+    if ((fields == 1 && chain == INGOT_CHAIN_GENEVE_OVER_V6) ||
+        (fields == 2 && chain != INGOT_CHAIN_GENEVE_OVER_V6))
+        return INGOT_GPU_EINVAL;
+    if (n == 0) return INGOT_GPU_SUCCESS;
+    if (!d_arena || !d_seg || !d_pkt_seg || !d_out) return INGOT_GPU_EINVAL;
+    if (int e = enter(ctx)) return e;
+    // len == NULL selects the dense table (launch_parse)
+    ingot_gpu::ParseArgs a{d_arena, d_seg, nullptr, 0, n, d_out, d_pkt_seg, d_chunk};
+    return from_hip(ingot_gpu::launch_parse(a, ingot_gpu::LAYOUT_SEGMENTED, chain,
+                                            fields ? ingot_gpu::OUT_FIELDS : ingot_gpu::OUT_REC16,
+                                            tuning_for(ctx, d_arena), (hipStream_t)stream));
+}
+
 int ingot_gpu_parse_modify(ingot_gpu_ctx* ctx, uint8_t* d_arena, const uint64_t* d_off,
                            const uint16_t* d_len, uint32_t stride, uint64_t n, int chain,
                            const ingot_edit* edits, uint32_t n_edits, ingot_rec* d_out,

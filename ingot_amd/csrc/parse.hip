@@ -263,7 +263,7 @@ struct SegFrame : Frame<NCH> {
 // for the whole wave).  A packet's last chunk is taken to hold the payload
 // (an mblk chain's tail) and is read on demand like chunks past the fourth.
 // Offsets are logical as in SegFrame; `len` is the current chunk's end.
-template <int CS0, int CS1, int CS2, int CS3>
+template <int CS0, int CS1, int CS2, int CS3, bool DENSE = false>
 struct SegFrameP {
     static constexpr bool kRead = true;
     static constexpr bool kProbe = false;
@@ -326,7 +326,12 @@ struct SegFrameP {
         if (k == 1) enter(o1, l1, pb(1), staged(1, nseg));
         else if (k == 2) enter(o2, l2, pb(2), staged(2, nseg));
         else if (k == 3) enter(o3, l3, pb(3), staged(3, nseg));
-        else enter(seg_off[s0 + k], seg_len[s0 + k], 0u, 0u);
+        else if constexpr (DENSE) {
+            const uint64_t v = seg_off[s0 + k];  // (offset << 16) | length
+            enter(v >> 16, (uint32_t)(v & 0xffffu), 0u, 0u);
+        } else {
+            enter(seg_off[s0 + k], seg_len[s0 + k], 0u, 0u);
+        }
     }
 };
 
@@ -1345,9 +1350,9 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
 // frame window, the later non-final chunks plane by plane, then the walk —
 // no dependent descriptor or byte load for headers inside staged pieces.
 // One 64-packet tile per wave.
-template <int CS0, int CS1, int CS2, int CS3, int CHAIN, int MODE>
+template <int CS0, int CS1, int CS2, int CS3, int CHAIN, int MODE, bool DENSE = false>
 __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
-    using FR = SegFrameP<CS0, CS1, CS2, CS3>;
+    using FR = SegFrameP<CS0, CS1, CS2, CS3, DENSE>;
     constexpr uint32_t P = CS0 + CS1 + CS2 + CS3;
     constexpr uint32_t WAVE_DW = WAVE * P * 4u;
     constexpr bool TUN = CHAIN == INGOT_CHAIN_GENEVE_OVER_V6;
@@ -1363,14 +1368,30 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
         const uint32_t s0 = valid ? a.pkt_seg[i] : 0u;
         const uint32_t nseg = valid ? a.pkt_seg[i + 1] - s0 : 0u;
         FR fr;
-        fr.o0 = nseg > 0 ? a.off[s0] : 0u;
-        fr.o1 = nseg > 1 ? a.off[s0 + 1] : 0u;
-        fr.o2 = nseg > 2 ? a.off[s0 + 2] : 0u;
-        fr.o3 = nseg > 3 ? a.off[s0 + 3] : 0u;
-        fr.l0 = nseg > 0 ? a.len[s0] : 0u;
-        fr.l1 = nseg > 1 ? a.len[s0 + 1] : 0u;
-        fr.l2 = nseg > 2 ? a.len[s0 + 2] : 0u;
-        fr.l3 = nseg > 3 ? a.len[s0 + 3] : 0u;
+        if constexpr (DENSE) {
+            // one 8-B entry per chunk: (offset << 16) | length
+            const uint64_t v0 = nseg > 0 ? a.off[s0] : 0u;
+            const uint64_t v1 = nseg > 1 ? a.off[s0 + 1] : 0u;
+            const uint64_t v2 = nseg > 2 ? a.off[s0 + 2] : 0u;
+            const uint64_t v3 = nseg > 3 ? a.off[s0 + 3] : 0u;
+            fr.o0 = v0 >> 16;
+            fr.o1 = v1 >> 16;
+            fr.o2 = v2 >> 16;
+            fr.o3 = v3 >> 16;
+            fr.l0 = (uint32_t)(v0 & 0xffffu);
+            fr.l1 = (uint32_t)(v1 & 0xffffu);
+            fr.l2 = (uint32_t)(v2 & 0xffffu);
+            fr.l3 = (uint32_t)(v3 & 0xffffu);
+        } else {
+            fr.o0 = nseg > 0 ? a.off[s0] : 0u;
+            fr.o1 = nseg > 1 ? a.off[s0 + 1] : 0u;
+            fr.o2 = nseg > 2 ? a.off[s0 + 2] : 0u;
+            fr.o3 = nseg > 3 ? a.off[s0 + 3] : 0u;
+            fr.l0 = nseg > 0 ? a.len[s0] : 0u;
+            fr.l1 = nseg > 1 ? a.len[s0 + 1] : 0u;
+            fr.l2 = nseg > 2 ? a.len[s0 + 2] : 0u;
+            fr.l3 = nseg > 3 ? a.len[s0 + 3] : 0u;
+        }
         // chunk 0, packet-major: instruction k, lane L fills slot 64k + L =
         // packet q / CS0, piece (q mod CS0) ^ swz (16-B aligned absolute
         // addresses; pieces only below the chunk's end)
@@ -1441,24 +1462,28 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
     }
 }
 
-template <int CS0, int CS1, int CS2, int CS3, int MODE>
+template <int CS0, int CS1, int CS2, int CS3, int MODE, bool DENSE = false>
 hipError_t launch_read(const ParseArgs& a, int chain, uint32_t grid, hipStream_t s) {
     switch (chain) {
     case INGOT_CHAIN_UDP_PARSER:
-        hipLaunchKernelGGL((k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_UDP_PARSER, MODE>),
-                           dim3(grid), dim3(BLOCK), 0, s, a);
+        hipLaunchKernelGGL(
+            (k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_UDP_PARSER, MODE, DENSE>),
+            dim3(grid), dim3(BLOCK), 0, s, a);
         break;
     case INGOT_CHAIN_GENERIC_ULP:
-        hipLaunchKernelGGL((k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENERIC_ULP, MODE>),
-                           dim3(grid), dim3(BLOCK), 0, s, a);
+        hipLaunchKernelGGL(
+            (k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENERIC_ULP, MODE, DENSE>),
+            dim3(grid), dim3(BLOCK), 0, s, a);
         break;
     case INGOT_CHAIN_VLAN_ULP:
-        hipLaunchKernelGGL((k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_VLAN_ULP, MODE>),
-                           dim3(grid), dim3(BLOCK), 0, s, a);
+        hipLaunchKernelGGL(
+            (k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_VLAN_ULP, MODE, DENSE>),
+            dim3(grid), dim3(BLOCK), 0, s, a);
         break;
     default:
-        hipLaunchKernelGGL((k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENEVE_OVER_V6, MODE>),
-                           dim3(grid), dim3(BLOCK), 0, s, a);
+        hipLaunchKernelGGL(
+            (k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENEVE_OVER_V6, MODE, DENSE>),
+            dim3(grid), dim3(BLOCK), 0, s, a);
         break;
     }
     return hipGetLastError();
@@ -1788,6 +1813,12 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
     // (first mblk-style chunks are short header blocks), the rest from L2/HBM.
     if (layout_kind == LAYOUT_SEGMENTED) {
         if (mode != OUT_FIELDS && mode != OUT_REC16) return hipErrorInvalidValue;
+        // dense chunk table (ingot_gpu_parse_read_dense): no length array,
+        // one (offset << 16) | length entry per chunk
+        if (!a.len) {
+            return mode == OUT_FIELDS ? launch_read<4, 0, 0, 0, OUT_FIELDS, true>(a, chain, g, s)
+                                      : launch_read<4, 0, 0, 0, OUT_REC16, true>(a, chain, g, s);
+        }
         // INGOT_TUNE_READ_PLAN: 16-B pieces staged per chunk of the first four.
         // Measured (tools/abtune.py, us per launch): the
         // reference's one-header-per-chunk shape (c2r, 1 M) 33.3 on demand

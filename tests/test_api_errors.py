@@ -48,6 +48,20 @@ def test_parse_argument_errors(env):
     torch.cuda.synchronize()
 
 
+def test_parse_read_dense_argument_errors(env):
+    torch, ctx, lib, arena, off, lens, out = env
+    h, a, o, r = ctx._h, arena.data_ptr(), off.data_ptr(), out.data_ptr()
+    ps = torch.arange(11, dtype=torch.int32, device="cuda")
+    p = ps.data_ptr()
+    TUN = int(Chain.GeneveOverV6Tunnel)
+    assert lib.ingot_gpu_parse_read_dense(h, a, o, p, 10, TUN, 1, r, None, None) == EINVAL
+    assert lib.ingot_gpu_parse_read_dense(h, a, o, p, 10, 1, 2, r, None, None) == EINVAL
+    assert lib.ingot_gpu_parse_read_dense(h, a, o, p, 10, 1, 3, r, None, None) == EINVAL
+    assert lib.ingot_gpu_parse_read_dense(h, a, None, p, 10, 1, 0, r, None, None) == EINVAL
+    assert lib.ingot_gpu_parse_read_dense(h, None, None, None, 0, 1, 0, None, None, None) == 0
+    torch.cuda.synchronize()
+
+
 def test_modify_and_flow_argument_errors(env):
     torch, ctx, lib, arena, off, lens, out = env
     h, a, o, ln = ctx._h, arena.data_ptr(), off.data_ptr(), lens.data_ptr()

@@ -207,3 +207,27 @@ def test_reference_bench_shape(ctx, torch):
     assert recs.tobytes() == w_rec.tobytes()
     assert np.array_equal(chunk, w_chunk) and (w_chunk == 2).all()
     assert (w_rec["status"] == 0).all()
+
+
+@pytest.mark.parametrize("chain", list(Chain))
+def test_dense_chunk_table_matches(ctx, torch, chain):
+    """ingot_gpu_parse_read_dense ((offset << 16) | length per chunk) gives
+    the records, field blocks and chunk indices of the two-array form and
+    of the oracle, 1-8 chunks per packet."""
+    prof = GenProfile.GENEVE_ADVERSARIAL if chain == TUN else GenProfile.ADVERSARIAL
+    frames = frames_of(prof, 20_000, seed=101 + int(chain))
+    packets = split_many(frames, seed=103 + int(chain))
+    kind = "geneve" if chain == TUN else "fields"
+    out, recs, chunk, segs = run_device(ctx, torch, packets, chain, kind)
+    arena, seg_off, seg_len, pkt_seg = segs
+    dense = (seg_off.astype(np.uint64) << np.uint64(16)) | seg_len.astype(np.uint64)
+    d = (torch.from_numpy(arena).cuda(), torch.from_numpy(dense.view(np.int64)).cuda(),
+         torch.from_numpy(pkt_seg.view(np.int32)).cuda())
+    r2, c2 = ctx.parse_read_dense(*d, chain)
+    f2, _ = ctx.parse_read_dense(*d, chain, fields=kind)
+    torch.cuda.synchronize()
+    assert r2.cpu().numpy().tobytes() == recs.tobytes()
+    assert f2.cpu().numpy().tobytes() == out.tobytes()
+    assert np.array_equal(c2.cpu().numpy().view(np.uint16), chunk)
+    w_rec, _, w_chunk = oracle.parse_read_batch(*segs, chain)
+    assert recs.tobytes() == w_rec.tobytes() and np.array_equal(chunk, w_chunk)
