@@ -3,6 +3,7 @@
 per-step histogram all-reduce (every reduce waited before the timed region
 ends; a buffer reused only after its reduce) over several streams."""
 import numpy as np
+import pytest
 
 import bench
 import oracle
@@ -173,3 +174,74 @@ def test_flow_runner_overlaps_reduce_and_waits_before_reuse():
             assert log.index(("wait", k)) < after[0]
     # reduces overlap later steps: reduce k is still in flight at step k + 1
     assert log.index(("reduce", 1)) < log.index(("wait", 0))
+
+
+class _ClockStream:
+    """A stream with its own device clock; launches advance it."""
+
+    def __init__(self, t0=0.0):
+        self.t = t0
+        self.cuda_stream = 0
+
+    def wait_event(self, ev):
+        self.t = max(self.t, ev.t)
+
+
+class _ClockTorch:
+    class cuda:  # noqa: N801
+        class Event:
+            def __init__(self, enable_timing=False):
+                self.t = None
+
+            def record(self, s):
+                self.t = s.t
+
+            def elapsed_time(self, other):
+                return other.t - self.t
+
+        @staticmethod
+        def synchronize():
+            pass
+
+
+class _Gate:
+    def __init__(self, log):
+        self.log = log
+
+    def arm(self, streams):
+        self.log.append("arm")
+
+    def open(self):
+        self.log.append("open")
+
+
+def test_timed_region_spans_earliest_start_to_latest_end(monkeypatch):
+    """_timed: every stream stamps its own start and end; the region is the
+    earliest start to the latest end (no join of one stream into another),
+    and the doorbell gate opens after the held launches and again at the end
+    (idempotent), also when a launch fails."""
+    s0, s1 = _ClockStream(10.0), _ClockStream(10.5)
+    durations = {0: 3.0, 1: 2.0}
+    log = []
+
+    def launch(k):
+        s = (s0, s1)[k % 2]
+        s.t += durations[k % 2]
+        log.append(k)
+        return 0
+
+    monkeypatch.setattr(bench.Gate, "HOLD", 2)
+    ms, _ = bench._timed(_ClockTorch, [s0, s1], launch, 4, gate=_Gate(log))
+    # s0: 10 -> 16, s1: 10.5 -> 14.5; region = 16 - 10
+    assert ms == pytest.approx(6.0)
+    assert log[0] == "arm" and log[1:3] == [0, 1] and log[3] == "open" and log[-1] == "open"
+    # ungated: the other streams fork from streams[0]'s start event
+    a, b = _ClockStream(0.0), _ClockStream(5.0)
+    ms, _ = bench._timed(_ClockTorch, [a, b], lambda k: ([a, b][k % 2].__setattr__(
+        "t", [a, b][k % 2].t + 1.0), 0)[1], 2)
+    assert ms == pytest.approx(6.0)  # b starts at 5 (its own clock), ends at 6
+    # a failing launch still opens the gate before raising
+    log2 = []
+    with pytest.raises(RuntimeError):
+        bench._timed(_ClockTorch, [_ClockStream()], lambda k: -1, 3, gate=_Gate(log2))
+    assert log2 == ["arm", "open"]
