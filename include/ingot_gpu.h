@@ -423,6 +423,10 @@ void ingot_gpu_doorbell_destroy(ingot_gpu_doorbell* db);
  *                              {4,2,2,0}, 4 = {4,1,1,0}; 9 = no descriptor
  *                              prefetch: chunk 0 staged, later chunks'
  *                              descriptors and bytes read on demand
+ *   INGOT_TUNE_FLOW_KERNEL     ingot_gpu_flow_hist at the default windows:
+ *                              0 = stage, walk, hash, store per tile
+ *                              (default); 1 = the next tile's staging issued
+ *                              before the hash of this one
  */
 #define INGOT_TUNE_WINDOW_INDEXED 1
 #define INGOT_TUNE_WINDOW_STRIDED 2
@@ -434,6 +438,7 @@ void ingot_gpu_doorbell_destroy(ingot_gpu_doorbell* db);
 #define INGOT_TUNE_FLOW_TABLE 8
 #define INGOT_TUNE_SLOW_PATH 9
 #define INGOT_TUNE_READ_PLAN 10
+#define INGOT_TUNE_FLOW_KERNEL 11
 int ingot_gpu_ctx_set_tuning(ingot_gpu_ctx* ctx, int key, int value);
 int ingot_gpu_ctx_get_tuning(const ingot_gpu_ctx* ctx, int key);
 

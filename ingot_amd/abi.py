@@ -80,6 +80,7 @@ TUNE_WRITEBACK = 7
 TUNE_FLOW_TABLE = 8
 TUNE_SLOW_PATH = 9
 TUNE_READ_PLAN = 10
+TUNE_FLOW_KERNEL = 11
 
 
 class IngotRec(ctypes.Structure):

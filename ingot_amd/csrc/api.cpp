@@ -311,6 +311,7 @@ int ingot_gpu_ctx_set_tuning(ingot_gpu_ctx* ctx, int key, int value) {
     case INGOT_TUNE_FLOW_TABLE: ctx->tuning.flow_table = value; break;
     case INGOT_TUNE_SLOW_PATH: ctx->tuning.slow_path = value; break;
     case INGOT_TUNE_READ_PLAN: ctx->tuning.read_plan = value; break;
+    case INGOT_TUNE_FLOW_KERNEL: ctx->tuning.flow_kernel = value; break;
     default: ctx->tuning.max_blocks = (uint32_t)value; break;
     }
     return INGOT_GPU_SUCCESS;
@@ -329,6 +330,7 @@ int ingot_gpu_ctx_get_tuning(const ingot_gpu_ctx* ctx, int key) {
     case INGOT_TUNE_FLOW_TABLE: return ctx->tuning.flow_table;
     case INGOT_TUNE_SLOW_PATH: return ctx->tuning.slow_path;
     case INGOT_TUNE_READ_PLAN: return ctx->tuning.read_plan;
+    case INGOT_TUNE_FLOW_KERNEL: return ctx->tuning.flow_kernel;
     default: return INGOT_GPU_EINVAL;
     }
 }

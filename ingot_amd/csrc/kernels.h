@@ -108,6 +108,7 @@ struct Tuning {
     int flow_table = 0;    // flows: 0 = auto (16-bit table when it suffices), 32 = 32-bit
     int slow_path = 0;     // bytes past the window: 0 = per-lane loads, 1 = compacted re-stage
     int read_plan = 0;     // parse_read: LDS pieces per staged chunk (see launch_parse)
+    int flow_kernel = 0;   // flows: 0 = k_parse, 1 = hash overlapped with the next tile (k_flows)
     uint32_t cus = 256;  // compute units of the context's device (grid shaping)
     bool host_arena = false;  // per call: the arena is host memory (ingot_gpu_host_map)
 };

@@ -1489,6 +1489,123 @@ hipError_t launch_read(const ParseArgs& a, int chain, uint32_t grid, hipStream_t
     return hipGetLastError();
 }
 
+// Flow classification with the hash overlapped (INGOT_TUNE_FLOW_KERNEL = 1):
+// the persistent k_parse<…, OUT_FLOWS*> loop stages a tile, waits, walks,
+// hashes and stores, so the ~72 LDS table lookups per packet run while no
+// HBM request of that wave is in flight.  Here a wave reads its tile's hash
+// input words out of the LDS image into registers right after the walk,
+// issues the next tile's LDS-DMA into the same image (its descriptors were
+// loaded during the walk), and only then computes the Toeplitz hash from
+// the table — the next tile's HBM latency covers the hash.  One LDS image
+// per wave, as in k_parse.
+template <uint32_t NCH, int LAYOUT, int CHAIN, bool H16>
+__global__ __launch_bounds__(BLOCK) void k_flows(FlowArgs args) {
+    static_assert(LAYOUT == LAYOUT_INDEXED || LAYOUT == LAYOUT_STRIDED, "indexed or slots");
+    const ParseArgs& a = args.p;
+    constexpr bool TUN = CHAIN == INGOT_CHAIN_GENEVE_OVER_V6;
+    constexpr uint32_t WIN = NCH * 16u;
+    constexpr uint32_t WAVE_DW = WAVE * NCH * 4u;
+    constexpr uint32_t SKIP = LAYOUT == LAYOUT_INDEXED && !TUN ? INGOT_FLOW_SKIP : 0u;
+    __shared__ __attribute__((aligned(16))) uint32_t s_win[WAVES * WAVE_DW + 16];
+    __shared__ __attribute__((aligned(64))) uint32_t s_tab[H16 ? FLOW_TAB16 : FLOW_TAB];
+    if constexpr (H16) build_flow_table16(s_tab, args.w);
+    else build_flow_table(s_tab, args.w);
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & (WAVE - 1u);
+    const uint32_t wave = threadIdx.x / WAVE;
+    uint32_t* wimg = s_win + wave * WAVE_DW;
+    const uint64_t ntiles = (a.n + WAVE - 1u) / WAVE;
+    const uint64_t step = (uint64_t)gridDim.x * WAVES;
+    const uint32_t mis = (uint32_t)((uintptr_t)a.arena & 31u);
+
+    // this lane's frame of tile tt: offset and length
+    auto desc = [&](uint64_t tt, uint64_t& off, uint32_t& len) {
+        const uint64_t i = tt * WAVE + lane;
+        const bool valid = i < a.n;
+        if constexpr (LAYOUT == LAYOUT_STRIDED) {
+            off = i * a.stride;
+            len = valid ? (a.len ? (uint32_t)a.len[i] : a.stride) : 0u;
+            if (len > a.stride) len = a.stride;
+        } else {
+            off = valid ? a.off[i] : 0u;
+            len = valid ? (uint32_t)a.len[i] : 0u;
+        }
+    };
+    // the window of a frame (as k_parse): staged bytes and chunk count
+    auto window = [&](uint64_t off, uint32_t len, uint32_t& sh, int64_t& base, uint32_t& take,
+                      uint32_t& nch) {
+        sh = (uint32_t)((off + SKIP + mis) & 15u);
+        base = (int64_t)off + (int64_t)SKIP - (int64_t)sh;
+        if constexpr (SKIP == 0) {
+            take = len < WIN - sh ? len : WIN - sh;
+            nch = (sh + take + 15u) >> 4;
+        } else {
+            const uint32_t wend = SKIP + WIN - sh;
+            take = len < wend ? len : wend;
+            const int32_t staged = (int32_t)take - ((int32_t)SKIP - (int32_t)sh);
+            nch = staged > 0 ? ((uint32_t)staged + 15u) >> 4 : 0u;
+        }
+    };
+    auto stage = [&](uint64_t tt, int64_t base, uint32_t nch) {
+#pragma unroll
+        for (uint32_t k = 0; k < NCH; ++k) {
+            const uint32_t q = k * WAVE + lane;
+            const uint32_t pp = q / NCH;
+            const uint32_t c = (q - pp * NCH) ^ swz<NCH>(pp);
+            const uint32_t np = (uint32_t)__shfl((int)nch, (int)pp);
+            int64_t bp;
+            if constexpr (LAYOUT == LAYOUT_STRIDED) bp = (int64_t)((tt * WAVE + pp) * a.stride);
+            else bp = (int64_t)__shfl((long long)base, (int)pp);
+            if (c < np) stage16(a.arena + bp + 16u * c, wimg + k * WAVE * 4u, false);
+        }
+    };
+
+    uint64_t t = (uint64_t)blockIdx.x * WAVES + wave;
+    if (t >= ntiles) return;
+    uint64_t off;
+    uint32_t len, sh, take, nch;
+    int64_t base;
+    desc(t, off, len);
+    window(off, len, sh, base, take, nch);
+    stage(t, base, nch);
+    for (;;) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t staged
+        const uint64_t tn = t + step;
+        const bool more = tn < ntiles;
+        uint64_t offn = 0;
+        uint32_t lenn = 0;
+        if (more) desc(tn, offn, lenn);  // in flight during the walk
+        const uint64_t i = t * WAVE + lane;
+        const bool valid = i < a.n;
+        Frame<NCH> fr{(const lds_u32*)wimg, lane, sh - SKIP, take, len, a.arena + off};
+        Rec r;
+        walk<CHAIN, false>(fr, r, nullptr, nullptr);
+        FlowWords x;
+        const bool counted = valid && flow_words(fr, r, x);
+        // every lane's reads of the image have returned before the next
+        // tile's LDS-DMA overwrites it
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (more) {
+            window(offn, lenn, sh, base, take, nch);
+            stage(tn, base, nch);
+        }
+        uint32_t h = 0;
+        if (counted) {
+            if constexpr (H16) h = toeplitz9_16(x, s_tab);
+            else h = toeplitz9(x, s_tab);
+        }
+        if (valid) {
+            args.flow[i] = counted ? (h & args.bin_mask) : INGOT_FLOW_NONE;
+            if (args.hash) args.hash[i] = h;
+        }
+        if (!more) break;
+        t = tn;
+        off = offn;
+        len = lenn;
+    }
+}
+
 // Pipelined variant for fixed slots with no length array (C2-style rings):
 // each wave walks several tiles and keeps the next DEPTH-1 tiles' LDS-DMA in
 // flight while it parses the current one (DEPTH LDS images per wave, used
@@ -1961,11 +2078,42 @@ hipError_t launch_modify(const ModifyArgs& args, int layout_kind, int chain, con
 // its default window is 5 chunks from the chunk holding byte 12 (SKIP in
 // k_parse: 392 -> 384 us per C5 flow_hist vs 5 chunks from the frame start;
 // 4 chunks from byte 12: 387); the same tuning knobs override the size.
+template <uint32_t NCH, int LAYOUT, bool H16>
+hipError_t launch_flows_pipe(const FlowArgs& a, int chain, uint32_t grid, hipStream_t s,
+                             uint32_t cus) {
+    auto go = [&](auto kernel) {
+        uint32_t g = grid;
+        if (cus) {
+            const uint32_t cap = cus * resident_per_cu(kernel);
+            if (g > cap) g = cap;
+        }
+        hipLaunchKernelGGL(kernel, dim3(g), dim3(BLOCK), 0, s, a);
+    };
+    switch (chain) {
+    case INGOT_CHAIN_UDP_PARSER: go(k_flows<NCH, LAYOUT, INGOT_CHAIN_UDP_PARSER, H16>); break;
+    case INGOT_CHAIN_GENERIC_ULP: go(k_flows<NCH, LAYOUT, INGOT_CHAIN_GENERIC_ULP, H16>); break;
+    case INGOT_CHAIN_VLAN_ULP: go(k_flows<NCH, LAYOUT, INGOT_CHAIN_VLAN_ULP, H16>); break;
+    default: go(k_flows<NCH, LAYOUT, INGOT_CHAIN_GENEVE_OVER_V6, H16>); break;
+    }
+    return hipGetLastError();
+}
+
 template <int MODE>
 hipError_t launch_flows_mode(const FlowArgs& a, int layout_kind, int chain, const Tuning& t,
                              hipStream_t s) {
     const uint32_t g = grid_for(a.p.n, t.max_blocks);
     const uint32_t pc = t.max_blocks ? 0u : t.cus;
+    // INGOT_TUNE_FLOW_KERNEL = 1: the hash-overlapped kernel (k_flows) at the
+    // default windows.  Measured on C5 (tools/abtune.py, us per step incl.
+    // the histogram): 360.7 vs 363.6 on one stream, 350.2 vs
+    // 337.3 on the bench's two — not the default.
+    constexpr bool H16 = MODE == OUT_FLOWS16;
+    if (t.flow_kernel == 1 && !t.window_indexed && !t.window_strided) {
+        if (layout_kind == LAYOUT_STRIDED)
+            return a.p.stride <= 64u ? launch_flows_pipe<4, LAYOUT_STRIDED, H16>(a, chain, g, s, pc)
+                                     : launch_flows_pipe<5, LAYOUT_STRIDED, H16>(a, chain, g, s, pc);
+        return launch_flows_pipe<5, LAYOUT_INDEXED, H16>(a, chain, g, s, pc);
+    }
     if (layout_kind == LAYOUT_STRIDED) {
         switch (t.window_strided ? t.window_strided : (a.p.stride <= 64u ? 4 : 5)) {
         case 3: return launch_chain<3, LAYOUT_STRIDED, MODE>(a, chain, g, s, pc);
@@ -2022,6 +2170,8 @@ bool tuning_valid(int key, int value) {
         return value == 0 || value == 1;
     case INGOT_TUNE_READ_PLAN:
         return (value >= 0 && value <= 4) || value == 9;
+    case INGOT_TUNE_FLOW_KERNEL:
+        return value == 0 || value == 1;
     default:
         return false;
     }

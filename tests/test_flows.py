@@ -115,7 +115,8 @@ def test_flow_hist_bit_exact(profile, chain, stride):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("tune", [{}, {"win": 3}, {"win": 4}, {"win": 5}, {"win": 8},
-                                  {"blocks": 7}, {"blocks": 1, "win": 3}])
+                                  {"blocks": 7}, {"blocks": 1, "win": 3}, {"fk": 1},
+                                  {"fk": 1, "blocks": 3}])
 @pytest.mark.parametrize("profile,chain,stride", [
     ("FLOWS", "VlanUlp", None), ("ADVERSARIAL", "GenericUlp", None),
     ("GENEVE_ADVERSARIAL", "GeneveOverV6Tunnel", None), ("VLAN_V6EH", "VlanUlp", 256),
@@ -128,12 +129,14 @@ def test_flow_kernels_every_setting(tune, profile, chain, stride):
 
     import ingot_amd
     from ingot_amd import GenProfile
-    from ingot_amd.abi import TUNE_MAX_BLOCKS, TUNE_WINDOW_INDEXED, TUNE_WINDOW_STRIDED
+    from ingot_amd.abi import (TUNE_FLOW_KERNEL, TUNE_MAX_BLOCKS, TUNE_WINDOW_INDEXED,
+                               TUNE_WINDOW_STRIDED)
 
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     n = 100_003
     ctx = ingot_amd.Context(0)
+    ctx.set_tuning(TUNE_FLOW_KERNEL, tune.get("fk", 0))
     if "win" in tune:
         ctx.set_tuning(TUNE_WINDOW_STRIDED if stride else TUNE_WINDOW_INDEXED, tune["win"])
     if "blocks" in tune:
@@ -157,7 +160,8 @@ def test_flow_kernels_every_setting(tune, profile, chain, stride):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("table", [0, 32])
-@pytest.mark.parametrize("tune", [{}, {"win": 3}, {"win": 4}, {"win": 8}, {"blocks": 5}])
+@pytest.mark.parametrize("tune", [{}, {"win": 3}, {"win": 4}, {"win": 8}, {"blocks": 5},
+                                  {"fk": 1}])
 @pytest.mark.parametrize("bins", [1 << 16, 1024])
 @pytest.mark.parametrize("profile,chain,stride", [
     ("FLOWS", "VlanUlp", None), ("ADVERSARIAL", "GenericUlp", None),
@@ -171,14 +175,15 @@ def test_flow_bins_without_hashes(table, tune, bins, profile, chain, stride):
 
     import ingot_amd
     from ingot_amd import GenProfile
-    from ingot_amd.abi import (TUNE_FLOW_TABLE, TUNE_MAX_BLOCKS, TUNE_WINDOW_INDEXED,
-                               TUNE_WINDOW_STRIDED)
+    from ingot_amd.abi import (TUNE_FLOW_KERNEL, TUNE_FLOW_TABLE, TUNE_MAX_BLOCKS,
+                               TUNE_WINDOW_INDEXED, TUNE_WINDOW_STRIDED)
 
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     n = 100_003
     ctx = ingot_amd.Context(0)
     ctx.set_tuning(TUNE_FLOW_TABLE, table)
+    ctx.set_tuning(TUNE_FLOW_KERNEL, tune.get("fk", 0))
     if "win" in tune:
         ctx.set_tuning(TUNE_WINDOW_STRIDED if stride else TUNE_WINDOW_INDEXED, tune["win"])
     if "blocks" in tune:

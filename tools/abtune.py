@@ -7,7 +7,7 @@ cross-process/device variance that looks like a kernel property).
     python tools/abtune.py --config c2 --var streams=1 --var streams=2 --var rec=8
 
 A variant is a comma list of key=value: win_i, win_s, blocks, pipe, depth, pol,
-wb, ftab, slow, plan, streams, rec, mode (parse|flows|modify: the runner; default the config's).
+wb, ftab, slow, plan, fk, streams, rec, mode (parse|flows|modify: the runner; default the config's).
 """
 from __future__ import annotations
 
@@ -38,7 +38,7 @@ def main():
     from ingot_amd.abi import (TUNE_CACHE_POLICY, TUNE_MAX_BLOCKS, TUNE_PIPE_DEPTH,
                                TUNE_PIPELINE, TUNE_WINDOW_INDEXED, TUNE_WINDOW_STRIDED,
                                TUNE_WRITEBACK, TUNE_FLOW_TABLE, TUNE_SLOW_PATH,
-                               TUNE_READ_PLAN)
+                               TUNE_READ_PLAN, TUNE_FLOW_KERNEL)
 
     prof, n, stride, chain_name, _ = bench.CONFIGS[args.config]
     chain = Chain[chain_name]
@@ -84,6 +84,8 @@ def main():
             ctx.set_tuning(TUNE_SLOW_PATH, int(kv["slow"]))
         if "plan" in kv:
             ctx.set_tuning(TUNE_READ_PLAN, int(kv["plan"]))
+        if "fk" in kv:
+            ctx.set_tuning(TUNE_FLOW_KERNEL, int(kv["fk"]))
         ns, rb = int(kv.get("streams", 1)), int(kv.get("rec", 16))
         mode = kv.get("mode", bench.MODES.get(args.config, "parse"))
         if mode == "flows":
