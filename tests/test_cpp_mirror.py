@@ -50,3 +50,23 @@ def test_cpp_host_ring_example_on_device():
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 mismatches" in r.stdout
+
+
+@pytest.mark.gpu
+def test_cpp_doorbell_ring_on_device():
+    """tests/cpp/example_doorbell_ring.cpp: a C++ ring consumer enqueues 8
+    batches' parses behind doorbells before their frames exist; a producer
+    thread copies each slot in and rings; the first parse is held until its
+    doorbell and every record is UdpParser's."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    exe = ROOT / "tests" / "cpp" / "build" / "example_doorbell_ring"
+    if not exe.exists():
+        from ingot_amd.build import build_cpp_tests
+
+        build_cpp_tests()
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "first held: ok" in r.stdout
