@@ -7,7 +7,8 @@ cross-process/device variance that looks like a kernel property).
     python tools/abtune.py --config c2 --var streams=1 --var streams=2 --var rec=8
 
 A variant is a comma list of key=value: win_i, win_s, blocks, pipe, depth, pol,
-wb, ftab, slow, plan, fk, streams, rec, mode (parse|flows|modify: the runner; default the config's).
+wb, ftab, slow, plan, fk, streams, rec, fonly (1: the flows kernel alone, no
+histogram), mode (parse|flows|modify: the runner; default the config's).
 """
 from __future__ import annotations
 
@@ -93,7 +94,8 @@ def main():
                      for _ in range(reps)]
             fids = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(reps)]
             r = bench.FlowRunner(torch, lib, ctx, chain, n, arenas, off, lens, hists, fids,
-                                 streams[:ns], lambda h: None)
+                                 streams[:ns], lambda h: None,
+                                 flows_only=kv.get("fonly") == "1")
         elif mode == "read":
             r = bench.ReadRunner(torch, lib, ctx, chain, n, arenas, *segs, outs, streams[:ns])
         elif mode == "packed":
