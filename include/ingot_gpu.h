@@ -425,8 +425,11 @@ void ingot_gpu_doorbell_destroy(ingot_gpu_doorbell* db);
  *                              descriptors and bytes read on demand
  *   INGOT_TUNE_FLOW_KERNEL     ingot_gpu_flow_hist at the default windows:
  *                              0 = stage, walk, hash, store per tile
- *                              (default); 1 = the next tile's staging issued
- *                              before the hash of this one
+ *                              (default: one tile per wave with the 16-bit
+ *                              table, a persistent grid with the 32-bit one);
+ *                              1 = the next tile's staging issued before the
+ *                              hash of this one (persistent); 2 = the default
+ *                              kernel on a persistent grid
  */
 #define INGOT_TUNE_WINDOW_INDEXED 1
 #define INGOT_TUNE_WINDOW_STRIDED 2

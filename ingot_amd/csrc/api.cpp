@@ -504,6 +504,15 @@ int ingot_gpu_flow_hist_ws(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uin
         }
         a.w[b] = w;
     }
+    // the 16-bit table: entry (p, v) = low 16 bits of the XOR of the windows
+    // of v's set bits at nibble position p (bit 3 of v = input bit 4p)
+    for (uint32_t e = 0; e < 2 * ingot_gpu::FLOW_TAB16_DW; ++e) {
+        const uint32_t p = e / 16u, v = e & 15u;
+        uint32_t acc = 0;
+        for (uint32_t k = 0; k < 4; ++k)
+            if ((v >> (3u - k)) & 1u) acc ^= a.w[4u * p + k];
+        a.tab16[e / 2] |= (acc & 0xffffu) << (16u * (e & 1u));
+    }
     const hipStream_t s = (hipStream_t)stream;
     if (int e = from_hip(ingot_gpu::launch_flows(a, layout, chain, tuning_for(ctx, d_arena), s)))
         return e;

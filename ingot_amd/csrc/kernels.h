@@ -33,6 +33,10 @@ enum OutMode {
 // Toeplitz key windows: w[b] = the 32 key bits starting at input bit b, for
 // every bit of the longest input (IPv6 src|dst|ports = 36 bytes).
 constexpr uint32_t FLOW_INPUT_BITS = 36 * 8;
+// The 16-bit nibble table (OUT_FLOWS16), in dwords: 72 positions x 16 values
+// x 2 B.  Computed once per call on the host (api.cpp) and passed with the
+// kernel arguments, so a block loads it instead of building it.
+constexpr uint32_t FLOW_TAB16_DW = FLOW_INPUT_BITS / 4 * 16 / 2;
 
 struct ParseArgs {
     const uint8_t* arena;
@@ -54,6 +58,7 @@ struct FlowArgs {
     uint32_t bin_mask;
     uint32_t* hash;  // optional
     uint32_t w[FLOW_INPUT_BITS];
+    alignas(16) uint32_t tab16[FLOW_TAB16_DW];  // entry (p, v) at half-word 16p + v
 };
 
 // In-place rewrite (ingot_gpu_parse_modify): api.cpp resolves each ingot_edit's
@@ -108,7 +113,8 @@ struct Tuning {
     int flow_table = 0;    // flows: 0 = auto (16-bit table when it suffices), 32 = 32-bit
     int slow_path = 0;     // bytes past the window: 0 = per-lane loads, 1 = compacted re-stage
     int read_plan = 0;     // parse_read: LDS pieces per staged chunk (see launch_parse)
-    int flow_kernel = 0;   // flows: 0 = k_parse, 1 = hash overlapped with the next tile (k_flows)
+    int flow_kernel = 0;   // flows: 0 = k_parse (16-bit table: one tile per wave), 1 = hash
+                           // overlapped with the next tile (k_flows), 2 = k_parse persistent
     uint32_t cus = 256;  // compute units of the context's device (grid shaping)
     bool host_arena = false;  // per call: the arena is host memory (ingot_gpu_host_map)
 };

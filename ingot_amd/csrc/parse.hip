@@ -961,6 +961,7 @@ __device__ __forceinline__ void build_flow_table(uint32_t* tab, const uint32_t* 
 // flow bin (hash & bin_mask, bins <= 65,536) is unchanged; 2,304 B instead
 // of 4,608 per block.
 constexpr uint32_t FLOW_TAB16 = FLOW_POS * 16 / 2;  // dwords
+static_assert(FLOW_TAB16 == FLOW_TAB16_DW, "kernels.h's table size");
 
 __device__ __forceinline__ void build_flow_table16(uint32_t* tab, const uint32_t* W) {
     for (uint32_t d = threadIdx.x; d < FLOW_TAB16; d += BLOCK) {
@@ -975,6 +976,13 @@ __device__ __forceinline__ void build_flow_table16(uint32_t* tab, const uint32_t
         }
         tab[d] = two;
     }
+}
+
+// The same table, computed by the host (FlowArgs::tab16): 144 16-B loads
+// from the kernel arguments per block instead of 1,152 entries built.
+__device__ __forceinline__ void load_flow_table16(uint32_t* tab, const uint32_t* src) {
+    for (uint32_t d = threadIdx.x; d < FLOW_TAB16 / 4u; d += BLOCK)
+        reinterpret_cast<uint4*>(tab)[d] = reinterpret_cast<const uint4*>(src)[d];
 }
 
 // Flow classification (ingot_gpu_flow_hist): hash of src|dst|ports.
@@ -1167,7 +1175,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
     __shared__ __attribute__((aligned(64 * FLOW_COPIES)))
     uint32_t s_tab[FLOWS ? (H16 ? FLOW_TAB16 : FLOW_TAB) : 1];
     if constexpr (FLOWS) {
-        if constexpr (H16) build_flow_table16(s_tab, args.w);
+        if constexpr (H16) load_flow_table16(s_tab, args.tab16);
         else build_flow_table(s_tab, args.w);
         __syncthreads();
     }
@@ -1508,7 +1516,7 @@ __global__ __launch_bounds__(BLOCK) void k_flows(FlowArgs args) {
     constexpr uint32_t SKIP = LAYOUT == LAYOUT_INDEXED && !TUN ? INGOT_FLOW_SKIP : 0u;
     __shared__ __attribute__((aligned(16))) uint32_t s_win[WAVES * WAVE_DW + 16];
     __shared__ __attribute__((aligned(64))) uint32_t s_tab[H16 ? FLOW_TAB16 : FLOW_TAB];
-    if constexpr (H16) build_flow_table16(s_tab, args.w);
+    if constexpr (H16) load_flow_table16(s_tab, args.tab16);
     else build_flow_table(s_tab, args.w);
     __syncthreads();
 
@@ -2102,12 +2110,20 @@ template <int MODE>
 hipError_t launch_flows_mode(const FlowArgs& a, int layout_kind, int chain, const Tuning& t,
                              hipStream_t s) {
     const uint32_t g = grid_for(a.p.n, t.max_blocks);
-    const uint32_t pc = t.max_blocks ? 0u : t.cus;
+    constexpr bool H16 = MODE == OUT_FLOWS16;
+    // The 16-bit table comes with the kernel arguments (a block loads it in
+    // one 16-B load per thread), so the default grid is one tile per wave like
+    // the plain parse, the hardware dispatcher refilling CUs as blocks finish:
+    // C5 flows kernel 314.8 us vs 329.5 persistent (plain parse of the same
+    // frames 312.8; profiles/r02_flows_grid_ab.json).  The 32-bit table is
+    // built per block (1,152 entries from the key windows), so its grid is
+    // persistent; INGOT_TUNE_FLOW_KERNEL = 2 makes the 16-bit one persistent
+    // too.  Fixed max_blocks: grid-stride over that many blocks.
+    const uint32_t pc = t.max_blocks || (H16 && t.flow_kernel == 0) ? 0u : t.cus;
     // INGOT_TUNE_FLOW_KERNEL = 1: the hash-overlapped kernel (k_flows) at the
     // default windows.  Measured on C5 (tools/abtune.py, us per step incl.
     // the histogram): 360.7 vs 363.6 on one stream, 350.2 vs
     // 337.3 on the bench's two — not the default.
-    constexpr bool H16 = MODE == OUT_FLOWS16;
     if (t.flow_kernel == 1 && !t.window_indexed && !t.window_strided) {
         if (layout_kind == LAYOUT_STRIDED)
             return a.p.stride <= 64u ? launch_flows_pipe<4, LAYOUT_STRIDED, H16>(a, chain, g, s, pc)
@@ -2133,11 +2149,12 @@ hipError_t launch_flows_mode(const FlowArgs& a, int layout_kind, int chain, cons
 hipError_t launch_flows(const FlowArgs& a, int layout_kind, int chain, const Tuning& t,
                         hipStream_t s) {
     if (a.p.n == 0) return hipSuccess;
-    // Each block builds the table once, so the grid is persistent: exactly the
+    // With a table built per block, the grid is persistent: exactly the
     // blocks the device holds at once (resident_per_cu, per kernel instance),
-    // each wave walking tiles.  Measured on C5 (parse+hash+histogram, us per
-    // step): one tile per wave 546, 4 blocks per CU 434, 5 per CU 402, 6 / 8
-    // per CU (a second partial round) 511 / 443.  A double-buffered variant
+    // each wave walking tiles.  Measured on C5 (round 1, 32-bit table built
+    // per block; parse+hash+histogram, us per step): one tile per wave 546,
+    // 4 blocks per CU 434, 5 per CU 402, 6 / 8 per CU (a second partial
+    // round) 511 / 443.  A double-buffered variant
     // (next tile staged while hashing, 3 blocks per CU for its two images)
     // measured 526 vs 454 at the time.
     // Bins <= 65,536 and no full hash requested: the 16-bit table
@@ -2171,7 +2188,7 @@ bool tuning_valid(int key, int value) {
     case INGOT_TUNE_READ_PLAN:
         return (value >= 0 && value <= 4) || value == 9;
     case INGOT_TUNE_FLOW_KERNEL:
-        return value == 0 || value == 1;
+        return value >= 0 && value <= 2;
     default:
         return false;
     }

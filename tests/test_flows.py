@@ -116,7 +116,8 @@ def test_flow_hist_bit_exact(profile, chain, stride):
 @pytest.mark.gpu
 @pytest.mark.parametrize("tune", [{}, {"win": 3}, {"win": 4}, {"win": 5}, {"win": 8},
                                   {"blocks": 7}, {"blocks": 1, "win": 3}, {"fk": 1},
-                                  {"fk": 1, "blocks": 3}])
+                                  {"fk": 1, "blocks": 3}, {"fk": 2}, {"fk": 2, "win": 4},
+                                  {"fk": 2, "blocks": 3}])
 @pytest.mark.parametrize("profile,chain,stride", [
     ("FLOWS", "VlanUlp", None), ("ADVERSARIAL", "GenericUlp", None),
     ("GENEVE_ADVERSARIAL", "GeneveOverV6Tunnel", None), ("VLAN_V6EH", "VlanUlp", 256),
@@ -161,7 +162,7 @@ def test_flow_kernels_every_setting(tune, profile, chain, stride):
 @pytest.mark.gpu
 @pytest.mark.parametrize("table", [0, 32])
 @pytest.mark.parametrize("tune", [{}, {"win": 3}, {"win": 4}, {"win": 8}, {"blocks": 5},
-                                  {"fk": 1}])
+                                  {"fk": 1}, {"fk": 2}])
 @pytest.mark.parametrize("bins", [1 << 16, 1024])
 @pytest.mark.parametrize("profile,chain,stride", [
     ("FLOWS", "VlanUlp", None), ("ADVERSARIAL", "GenericUlp", None),
