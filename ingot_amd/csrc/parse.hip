@@ -262,6 +262,9 @@ struct SegFrame : Frame<NCH> {
 // π holds that piece of all 64 packets: one LDS-DMA instruction per piece
 // for the whole wave).  A packet's last chunk is taken to hold the payload
 // (an mblk chain's tail) and is read on demand like chunks past the fourth.
+// A chunk without planes of its own that lies inside chunk 0's window (chunks
+// cut from one buffer, like the reference bench's one chunk per header) is
+// staged with chunk 0's pieces and read from there.
 // Offsets are logical as in SegFrame; `len` is the current chunk's end.
 template <int CS0, int CS1, int CS2, int CS3, bool DENSE = false>
 struct SegFrameP {
@@ -278,6 +281,9 @@ struct SegFrameP {
     uint32_t s0, k, nseg;
     uint64_t o0, o1, o2, o3;  // the first four chunks' offsets and lengths
     uint32_t l0, l1, l2, l3;
+    int64_t b0;      // chunk 0's window: arena bytes [b0, b0 + span0) staged
+    uint32_t span0;
+    static constexpr uint32_t kW0 = 0xffffffffu;  // `plane` of a chunk read from that window
 
     static constexpr uint32_t cs(uint32_t e) {
         return e == 0 ? CS0 : e == 1 ? CS1 : e == 2 ? CS2 : e == 3 ? CS3 : 0;
@@ -288,7 +294,8 @@ struct SegFrameP {
     // staged chunk-relative byte b of the current chunk: a dword of the image
     __device__ __forceinline__ uint32_t dw(uint32_t b) const {
         const uint32_t c = b >> 4;
-        const uint32_t slot = k == 0 ? slot_of<CS0>(p, c) : WAVE * (CS0 + plane + c) + p;
+        const uint32_t slot =
+            k == 0 || plane == kW0 ? slot_of<CS0>(p, c) : WAVE * (CS0 + plane + c) + p;
         return win[slot * 4u + ((b >> 2) & 3u)];
     }
     __device__ __forceinline__ uint32_t be(uint32_t i, uint32_t n) const {
@@ -319,6 +326,14 @@ struct SegFrameP {
         plane = pl;
         sh = (uint32_t)((uintptr_t)(arena + o) & 15u);
         avail = c ? (l < 16u * c - sh ? l : 16u * c - sh) : 0u;
+        if (k != 0 && c == 0) {
+            const int64_t d = (int64_t)o - b0;
+            if (d >= 0 && d < (int64_t)span0) {
+                plane = kW0;
+                sh = (uint32_t)d;
+                avail = l < span0 - sh ? l : span0 - sh;
+            }
+        }
     }
     __device__ __forceinline__ void advance() {
         ++k;
@@ -1404,10 +1419,21 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
         // packet q / CS0, piece (q mod CS0) ^ swz (16-B aligned absolute
         // addresses; pieces only below the chunk's end)
         const uint32_t sh0 = (uint32_t)((uintptr_t)(a.arena + fr.o0) & 15u);
-        const uint32_t n0 = nseg ? (sh0 + (fr.l0 < 16u * CS0 - sh0 ? fr.l0 : 16u * CS0 - sh0) +
-                                    15u) >> 4
-                                 : 0u;
         const int64_t base0 = (int64_t)fr.o0 - (int64_t)sh0;
+        uint32_t ext = nseg ? sh0 + (fr.l0 < 16u * CS0 - sh0 ? fr.l0 : 16u * CS0 - sh0) : 0u;
+        // a later non-last chunk without planes that starts inside chunk 0's
+        // window: stage the window's pieces up to its end (or the window's)
+        auto widen = [&](uint32_t e, uint64_t o, uint32_t l) {
+            const int64_t d = (int64_t)o - base0;
+            if (FR::cs(e) == 0 && e + 1 < nseg && d >= 0 && d < (int64_t)(16u * CS0)) {
+                const uint32_t end = (uint32_t)d + l < 16u * CS0 ? (uint32_t)d + l : 16u * CS0;
+                ext = end > ext ? end : ext;
+            }
+        };
+        widen(1, fr.o1, fr.l1);
+        widen(2, fr.o2, fr.l2);
+        widen(3, fr.o3, fr.l3);
+        const uint32_t n0 = (ext + 15u) >> 4;
 #pragma unroll
         for (uint32_t k = 0; k < (uint32_t)CS0; ++k) {
             const uint32_t q = k * WAVE + lane;
@@ -1440,6 +1466,8 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
         fr.k = 0;
         fr.nseg = nseg;
         fr.L = 0;
+        fr.b0 = base0;
+        fr.span0 = 16u * n0;
         fr.enter(fr.o0, fr.l0, 0u, nseg ? CS0 : 0u);
         Rec r;
         if constexpr (MODE == OUT_FIELDS) {

@@ -231,3 +231,65 @@ def test_dense_chunk_table_matches(ctx, torch, chain):
     assert np.array_equal(c2.cpu().numpy().view(np.uint16), chunk)
     w_rec, _, w_chunk = oracle.parse_read_batch(*segs, chain)
     assert recs.tobytes() == w_rec.tobytes() and np.array_equal(chunk, w_chunk)
+
+
+def scatter(packets, seed):
+    """Place each packet's chunks in its own 256-B region in random order with
+    random gaps (some before chunk 0, some inside chunk 0's staged window with
+    gaps between them), and now and then let a chunk alias an earlier one's
+    bytes (a repeated chunk).  Returns the chunk tables."""
+    rng = np.random.default_rng(seed)
+    region = 256
+    arena = np.zeros(region * len(packets) + 64, dtype=np.uint8)
+    offs, lens, pkt = [], [], [0]
+    for i, chunks in enumerate(packets):
+        base = region * i
+        order = rng.permutation(len(chunks))
+        pos = base + int(rng.integers(0, 16))
+        at = {}
+        for j in order:
+            c = chunks[j]
+            if pos + len(c) > base + region:
+                pos = base  # too long for this layout: overlap is fine when content-equal
+                c = b""
+            arena[pos:pos + len(c)] = np.frombuffer(c, dtype=np.uint8)
+            at[j] = (pos, len(c))
+            pos += len(c) + int(rng.integers(0, 12))
+        seq = [at[j] for j in range(len(chunks))]
+        if len(seq) > 1 and rng.random() < 0.1:  # repeat chunk 0 as chunk 1
+            seq.insert(1, seq[0])
+        for o, ln in seq:
+            offs.append(o)
+            lens.append(ln)
+        pkt.append(len(offs))
+    return (arena, np.array(offs, dtype=np.uint64), np.array(lens, dtype=np.uint16),
+            np.array(pkt, dtype=np.uint32))
+
+
+@pytest.mark.parametrize("plan", [0, 2, 9])
+def test_scattered_and_aliased_chunks(torch, plan):
+    """Chunks out of memory order, with gaps, partly inside chunk 0's staged
+    window and partly outside, and repeated chunks: the staged reads of later
+    chunks come from wherever their bytes are (INGOT_TUNE_READ_PLAN 0 / 2 /
+    9), records and chunk indices equal the oracle's."""
+    from ingot_amd.abi import TUNE_READ_PLAN
+
+    c = ingot_amd.Context(0)
+    c.set_tuning(TUNE_READ_PLAN, plan)
+    for chain in Chain:
+        prof = GenProfile.GENEVE_ADVERSARIAL if chain == TUN else GenProfile.ADVERSARIAL
+        frames = frames_of(prof, 12_000, seed=131 + int(chain))
+        frames += frames_of(GenProfile.GENEVE if chain == TUN else GenProfile.VLAN_V6EH, 8_000,
+                            seed=137)
+        packets = [[bytes(x) for x in p] for p in split_many(frames, seed=139 + int(chain))]
+        arena, so, sl, ps = scatter(packets, seed=149 + int(chain))
+        d = (torch.from_numpy(arena).cuda(), torch.from_numpy(so.view(np.int64)).cuda(),
+             torch.from_numpy(sl.view(np.int16)).cuda(), torch.from_numpy(ps.view(np.int32)).cuda())
+        recs, chunk = c.parse_read(*d, chain)
+        torch.cuda.synchronize()
+        w_rec, _, w_chunk = oracle.parse_read_batch(arena, so, sl, ps, chain)
+        n = len(packets)
+        r = recs.cpu().numpy()
+        bad = np.nonzero((r.reshape(n, 16) != w_rec.view(np.uint8).reshape(n, 16)).any(1))[0]
+        assert bad.size == 0, (chain, bad[:5])
+        assert np.array_equal(chunk.cpu().numpy().view(np.uint16), w_chunk)
