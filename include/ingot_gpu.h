@@ -420,7 +420,8 @@ void ingot_gpu_doorbell_destroy(ingot_gpu_doorbell* db);
  *                              first four chunks (a packet's last chunk, the
  *                              payload, is never staged): 0 / 1 =
  *                              {4,0,0,0} (default), 2 = {2,2,2,0}, 3 =
- *                              {4,2,2,0}, 4 = {4,1,1,0}; 9 = no descriptor
+ *                              {4,2,2,0}, 4 = {4,1,1,0}, 5 = {3,0,0,0},
+ *                              6 = {2,0,0,0}; 9 = no descriptor
  *                              prefetch: chunk 0 staged, later chunks'
  *                              descriptors and bytes read on demand
  *   INGOT_TUNE_FLOW_KERNEL     ingot_gpu_flow_hist at the default windows:

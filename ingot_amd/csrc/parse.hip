@@ -254,8 +254,8 @@ struct SegFrame : Frame<NCH> {
     }
 };
 
-// parse_read with the header chunks staged (k_parse_read): the first four
-// chunks' descriptors are loaded up front; chunk 0 gets CS0 16-B slots per
+// parse_read with the header chunks staged (k_parse_read): the descriptors
+// of the first four chunks, except a packet's last, are loaded up front; chunk 0 gets CS0 16-B slots per
 // packet (packet-major, like a frame's window: a packet's pieces sit side by
 // side, so the wave's requests for one frame coalesce) and each later chunk
 // e < 4 that is not the packet's last one gets CS_e pieces in planes (plane
@@ -338,9 +338,12 @@ struct SegFrameP {
     __device__ __forceinline__ void advance() {
         ++k;
         L = len;
-        if (k == 1) enter(o1, l1, pb(1), staged(1, nseg));
-        else if (k == 2) enter(o2, l2, pb(2), staged(2, nseg));
-        else if (k == 3) enter(o3, l3, pb(3), staged(3, nseg));
+        // chunks 1..3 that are not the packet's last had their descriptors
+        // loaded with chunk 0's; the last chunk (the payload) and chunks past
+        // the fourth are looked up when the walk reaches them
+        if (k + 1 < nseg && k == 1) enter(o1, l1, pb(1), staged(1, nseg));
+        else if (k + 1 < nseg && k == 2) enter(o2, l2, pb(2), staged(2, nseg));
+        else if (k + 1 < nseg && k == 3) enter(o3, l3, pb(3), staged(3, nseg));
         else if constexpr (DENSE) {
             const uint64_t v = seg_off[s0 + k];  // (offset << 16) | length
             enter(v >> 16, (uint32_t)(v & 0xffffu), 0u, 0u);
@@ -1392,11 +1395,12 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
         const uint32_t nseg = valid ? a.pkt_seg[i + 1] - s0 : 0u;
         FR fr;
         if constexpr (DENSE) {
-            // one 8-B entry per chunk: (offset << 16) | length
+            // one 8-B entry per chunk: (offset << 16) | length; chunks 1..3
+            // only when not the packet's last (SegFrameP::advance)
             const uint64_t v0 = nseg > 0 ? a.off[s0] : 0u;
-            const uint64_t v1 = nseg > 1 ? a.off[s0 + 1] : 0u;
-            const uint64_t v2 = nseg > 2 ? a.off[s0 + 2] : 0u;
-            const uint64_t v3 = nseg > 3 ? a.off[s0 + 3] : 0u;
+            const uint64_t v1 = nseg > 2 ? a.off[s0 + 1] : 0u;
+            const uint64_t v2 = nseg > 3 ? a.off[s0 + 2] : 0u;
+            const uint64_t v3 = nseg > 4 ? a.off[s0 + 3] : 0u;
             fr.o0 = v0 >> 16;
             fr.o1 = v1 >> 16;
             fr.o2 = v2 >> 16;
@@ -1407,13 +1411,13 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
             fr.l3 = (uint32_t)(v3 & 0xffffu);
         } else {
             fr.o0 = nseg > 0 ? a.off[s0] : 0u;
-            fr.o1 = nseg > 1 ? a.off[s0 + 1] : 0u;
-            fr.o2 = nseg > 2 ? a.off[s0 + 2] : 0u;
-            fr.o3 = nseg > 3 ? a.off[s0 + 3] : 0u;
+            fr.o1 = nseg > 2 ? a.off[s0 + 1] : 0u;
+            fr.o2 = nseg > 3 ? a.off[s0 + 2] : 0u;
+            fr.o3 = nseg > 4 ? a.off[s0 + 3] : 0u;
             fr.l0 = nseg > 0 ? a.len[s0] : 0u;
-            fr.l1 = nseg > 1 ? a.len[s0 + 1] : 0u;
-            fr.l2 = nseg > 2 ? a.len[s0 + 2] : 0u;
-            fr.l3 = nseg > 3 ? a.len[s0 + 3] : 0u;
+            fr.l1 = nseg > 2 ? a.len[s0 + 1] : 0u;
+            fr.l2 = nseg > 3 ? a.len[s0 + 2] : 0u;
+            fr.l3 = nseg > 4 ? a.len[s0 + 3] : 0u;
         }
         // chunk 0, packet-major: instruction k, lane L fills slot 64k + L =
         // packet q / CS0, piece (q mod CS0) ^ swz (16-B aligned absolute
@@ -1989,6 +1993,8 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
         case 2: return launch_read<2, 2, 2, 0, OUT_REC16>(a, chain, g, s);
         case 3: return launch_read<4, 2, 2, 0, OUT_REC16>(a, chain, g, s);
         case 4: return launch_read<4, 1, 1, 0, OUT_REC16>(a, chain, g, s);
+        case 5: return launch_read<3, 0, 0, 0, OUT_REC16>(a, chain, g, s);
+        case 6: return launch_read<2, 0, 0, 0, OUT_REC16>(a, chain, g, s);
         default: return launch_read<4, 0, 0, 0, OUT_REC16>(a, chain, g, s);
         }
     }
@@ -2214,7 +2220,7 @@ bool tuning_valid(int key, int value) {
     case INGOT_TUNE_SLOW_PATH:
         return value == 0 || value == 1;
     case INGOT_TUNE_READ_PLAN:
-        return (value >= 0 && value <= 4) || value == 9;
+        return (value >= 0 && value <= 6) || value == 9;
     case INGOT_TUNE_FLOW_KERNEL:
         return value >= 0 && value <= 2;
     default:
