@@ -94,7 +94,7 @@ ROTATE_CAP_BYTES = 64 << 30
 # DESIGN.md §5): short launches overlap their ramp-up/drain on 2 (C2 12.3 vs
 # 15.2 us, C2m 20.5 vs 25.0) or 3 (C3s 112.5 vs 115.1); long gather-bound
 # launches gain nothing (C3 606 / 618, C4 324 / 324, C6 392 / 393 us on 1 / 2).
-STREAMS = {"c2": 2, "c2m": 2, "c3": 1, "c3p": 1, "c3r": 2, "c3s": 3, "c4": 1, "c5": 2,
+STREAMS = {"c2": 2, "c2m": 2, "c3": 1, "c3p": 1, "c3r": 1, "c3s": 3, "c4": 1, "c5": 2,
            "c6": 1, "c2r": 2}
 FLOW_BINS = 1 << 16
 
