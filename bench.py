@@ -820,9 +820,11 @@ def main():
     # back, so region/K = one launch incl. the dependent-launch boundary; this
     # is what rocprofv3's per-dispatch mean measures).  In the pipelined
     # schedule two launches overlap, so per-dispatch durations are not per-step.
+    # Its own floor of warm-up and launches, so that a short run (--steps 1
+    # --warmup 0) does not report a cold single launch as the kernel's rate.
     iso = runner(1, args.record, flows_only=True)
-    iso.run(min(args.warmup, 50))
-    iso_steps = min(args.steps, 1000)
+    iso.run(max(10, min(args.warmup, 50)))
+    iso_steps = max(20, min(args.steps, 1000))
     ms_iso, _ = iso.run(iso_steps, gate)
     launch_ms = ms_iso / iso_steps
     achieved = bytes_launch / (launch_ms / 1e3) / 1e9
