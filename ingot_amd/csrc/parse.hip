@@ -981,23 +981,9 @@ __device__ __forceinline__ void build_flow_table(uint32_t* tab, const uint32_t* 
 constexpr uint32_t FLOW_TAB16 = FLOW_POS * 16 / 2;  // dwords
 static_assert(FLOW_TAB16 == FLOW_TAB16_DW, "kernels.h's table size");
 
-__device__ __forceinline__ void build_flow_table16(uint32_t* tab, const uint32_t* W) {
-    for (uint32_t d = threadIdx.x; d < FLOW_TAB16; d += BLOCK) {
-        uint32_t two = 0;
-#pragma unroll
-        for (uint32_t h = 0; h < 2; ++h) {
-            const uint32_t e = 2u * d + h, p = e / 16u, v = e & 15u;
-            uint32_t acc = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) acc ^= ((v >> (3u - k)) & 1u) ? W[4u * p + k] : 0u;
-            two |= (acc & 0xffffu) << (16u * h);
-        }
-        tab[d] = two;
-    }
-}
-
-// The same table, computed by the host (FlowArgs::tab16): 144 16-B loads
-// from the kernel arguments per block instead of 1,152 entries built.
+// Computed by the host (api.cpp: FlowArgs::tab16, from the same key windows)
+// and loaded per block: 144 16-B loads from the kernel arguments instead of
+// 1,152 entries built from W.
 __device__ __forceinline__ void load_flow_table16(uint32_t* tab, const uint32_t* src) {
     for (uint32_t d = threadIdx.x; d < FLOW_TAB16 / 4u; d += BLOCK)
         reinterpret_cast<uint4*>(tab)[d] = reinterpret_cast<const uint4*>(src)[d];

@@ -262,3 +262,27 @@ def test_flow_hist_many_slices():
                       workspace=ctx.flow_hist_workspace(n, 1))
         torch.cuda.synchronize()
         assert int(h1.cpu()[0]) == int((f != 0xFFFFFFFF).sum())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fk", [0, 1, 2])
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 4097, 262_145])
+def test_flow_ids_ragged_batches(n, fk):
+    """Ragged batch sizes on every flows grid (one tile per wave, the
+    hash-overlapped and the persistent kernel): flow ids equal the oracle's."""
+    import torch
+
+    import ingot_amd
+    from ingot_amd import GenProfile
+    from ingot_amd.abi import TUNE_FLOW_KERNEL
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ctx = ingot_amd.Context(0)
+    ctx.set_tuning(TUNE_FLOW_KERNEL, fk)
+    arena, off, lens = ingot_amd.gen_frames(GenProfile.FLOWS, n, seed=n + 7)
+    flow = ctx.flow_hist(arena, off, lens, Chain.VlanUlp, n=n)
+    torch.cuda.synchronize()
+    oracle.flow_hist(arena.cpu().numpy(), off.cpu().numpy(), lens.cpu().numpy(), Chain.VlanUlp,
+                     n=n)
+    assert (flow.cpu().numpy().view(np.uint32) == oracle.flow_hist.last_flows).all()
