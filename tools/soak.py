@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Validation tool: determinism soak of the pipelined kernels.  Thousands of
-launches of the ring kernel (C2 slots, 2 streams), the flow kernel
-(persistent grid) and the packed-layout parse, each output compared on the
+launches of the ring kernel (C2 slots, 2 streams), the flow kernels
+(persistent grid with full hashes; one tile per wave with the 16-bit table,
+2 streams), parse_read over the reference bench's one-chunk-per-header
+shape (2 streams) and the packed-layout parse, each output compared on the
 device with the first run's over the same arena (which the parity tests pin
 to the oracle) — an intermittent race in LDS-image reuse or the persistent
 grids would show up as a mismatch.  Writes gpurun_out/soak.json.
@@ -69,6 +71,45 @@ def main():
         bad += int(not (torch.equal(f, f0) and torch.equal(h, h0)))
     torch.cuda.synchronize()
     res["flow_kernel"] = {"launches": args.iters // 10, "mismatching_launches": bad}
+
+    # flow ids only (16-bit table, one tile per wave), steps over 2 streams
+    g0 = ctx.flow_hist(arena, off, lens, Chain.VlanUlp)
+    torch.cuda.synchronize()
+    gout = [torch.empty_like(g0) for _ in range(4)]
+    acc = [torch.zeros((), dtype=torch.int64, device="cuda") for _ in s]
+    for it in range(args.iters):
+        k, st = it % 4, s[it % 2]
+        ctx.flow_hist(arena, off, lens, Chain.VlanUlp, flow=gout[k], stream=st)
+        with torch.cuda.stream(st):
+            acc[it % 2] += (gout[k] != g0).any().to(torch.int64)
+    torch.cuda.synchronize()
+    res["flow_kernel_16bit"] = {"launches": args.iters,
+                                "mismatching_launches": int(sum(a.item() for a in acc))}
+    del gout
+
+    # parse_read, one chunk per header (chunks cut from the C2 slots, staged
+    # from chunk 0's window), steps over 2 streams
+    import bench
+    sl_arena = ingot_amd.gen_frames(GenProfile.V4UDP64, n, stride=64)[0]
+    recs0 = ctx.parse_strided(sl_arena, 64, n, Chain.UdpParser)
+    torch.cuda.synchronize()
+    rl = torch.full((n,), 64, dtype=torch.int32, device="cuda")
+    seg_off, seg_len, pkt_seg, _ = bench.read_chunks(
+        torch, None, 64, rl, ingot_amd.records_to_numpy(recs0), "per_header", "cuda")
+    r0, c0 = ctx.parse_read(sl_arena, seg_off, seg_len, pkt_seg, Chain.UdpParser)
+    torch.cuda.synchronize()
+    routs = [torch.empty_like(r0) for _ in range(4)]
+    acc = [torch.zeros((), dtype=torch.int64, device="cuda") for _ in s]
+    for it in range(args.iters):
+        k, st = it % 4, s[it % 2]
+        ctx.parse_read(sl_arena, seg_off, seg_len, pkt_seg, Chain.UdpParser, out=routs[k],
+                       stream=st)
+        with torch.cuda.stream(st):
+            acc[it % 2] += (routs[k] != r0).any().to(torch.int64)
+    torch.cuda.synchronize()
+    res["parse_read_per_header"] = {"launches": args.iters,
+                                    "mismatching_launches": int(sum(a.item() for a in acc))}
+    del routs, sl_arena
 
     # packed layout (tile scan + in-kernel prefix scan)
     want = ctx.parse(arena, off, lens, Chain.VlanUlp)
