@@ -926,7 +926,8 @@ def main():
                 "streams": args.streams,
                 "arena_copies_rotated": reps,
                 "parallelism": (f"{args.scaling} scaling, contiguous share per GPU x{world}" +
-                                (f"; RCCL all-reduce (sum) of the {FLOW_BINS} x u32 flow "
+                                (f"; {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} "
+                                 f"all-reduce (sum) of the {FLOW_BINS} x u32 flow "
                                  "histogram every step" if flows else
                                  " (no data-path collective)")),
                 "ok_fraction": round(ok_frac, 6),
