@@ -954,6 +954,9 @@ __device__ __forceinline__ void apply_edit(const FR& f, EditSink& sink, uint32_t
 // blocks per CU instead of 5, worth more than the conflicts cost.  Built once
 // per block (the flows grid is persistent).
 constexpr uint32_t FLOW_POS = FLOW_INPUT_BITS / 4;
+#ifndef INGOT_REC_SKIP
+#define INGOT_REC_SKIP 12
+#endif
 #ifndef INGOT_FLOW_SKIP
 #define INGOT_FLOW_SKIP 12
 #endif
@@ -1189,8 +1192,17 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
     uint32_t* wimg = s_win + wave * WAVE_DW;
     const uint64_t ntiles = (a.n + WAVE - 1u) / WAVE;
     const uint32_t mis = (uint32_t)((uintptr_t)a.arena & 31u);  // arena address mod 32
+    // Record modes never read the MAC addresses either (walk<CHAIN, false>
+    // reads Ethernet's ethertype only), so frames addressed by offset start
+    // their window at the chunk holding byte 12 too.
+    // (NCH = 0, nothing staged: no skip — the window's end SKIP + WIN - sh
+    // would underflow.)
+    constexpr bool RECM = MODE == OUT_REC16 || MODE == OUT_REC8;
     constexpr uint32_t SKIP =
-        FLOWS && LAYOUT == LAYOUT_INDEXED && !TUN ? INGOT_FLOW_SKIP : 0u;
+        NCH == 0 ? 0u
+        : FLOWS && LAYOUT == LAYOUT_INDEXED && !TUN ? INGOT_FLOW_SKIP
+        : RECM && !SLOW && (LAYOUT == LAYOUT_INDEXED || LAYOUT == LAYOUT_PACKED) ? INGOT_REC_SKIP
+                                                                                  : 0u;
     static_assert(SKIP <= 12u, "the walk reads the ethertype at frame byte 12");
 
     for (uint64_t t = (uint64_t)blockIdx.x * WAVES + wave; t < ntiles;
