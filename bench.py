@@ -96,6 +96,13 @@ ROTATE_CAP_BYTES = 64 << 30
 # launches gain nothing (C3 606 / 618, C4 324 / 324, C6 392 / 393 us on 1 / 2).
 STREAMS = {"c2": 2, "c2m": 2, "c3": 1, "c3p": 1, "c3r": 1, "c3s": 3, "c4": 1, "c5": 2,
            "c6": 1, "c2r": 2}
+# Staggered streams (gated regions with >= 2 streams): stream i starts
+# i * STAGGER_US behind stream 0 (ingot_gpu_stream_delay), so the streams'
+# launches do not ramp up and drain in lockstep.  0 = start together.
+# Measured (tools/stagger_ab.py, interleaved, 20-step regions after a 5-step
+# warm-up as the driver runs them; profiles/r02_stagger_ab.json): C2 12.32-12.38
+# -> 12.18-12.20 us/step at 5-7 us, 12.5 at 12 us; 200-step regions unchanged.
+STAGGER_US = {"c2": 6.0}
 FLOW_BINS = 1 << 16
 
 
@@ -391,17 +398,21 @@ class Gate:
     HOLD = 64
     WATCHDOG_S = 20.0
 
-    def __init__(self, ingot_amd, ctx):
+    def __init__(self, ingot_amd, ctx, stagger_us=0.0):
         import threading
 
         self.db = ingot_amd.Doorbell(ctx)
+        self.ctx = ctx
+        self.stagger_ns = int(round(stagger_us * 1000))
         self.seq = 0
         self._threading = threading
 
     def arm(self, streams):
         self.seq += 1
-        for s in streams:
+        for i, s in enumerate(streams):
             self.db.wait(self.seq, s)
+            if i and self.stagger_ns:
+                self.ctx.stream_delay(i * self.stagger_ns, s)
         seq, db = self.seq, self.db
         self._timer = self._threading.Timer(self.WATCHDOG_S, lambda: db.ring(seq))
         self._timer.daemon = True
@@ -630,6 +641,9 @@ def main():
                     help="skip the live host-inclusive (PCIe) measurement")
     ap.add_argument("--no-gate", action="store_true",
                     help="time from host submission (no doorbell-held first launches)")
+    ap.add_argument("--stagger-us", type=float, default=None,
+                    help="gated, >= 2 streams: stream i starts i * this many us behind "
+                         "stream 0 (default: the config's STAGGER_US, else 0)")
     ap.add_argument("--plan", action="store_true",
                     help="print the ranks' shares and exit without touching a GPU")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
@@ -760,9 +774,14 @@ def main():
     gate_note = "off (--no-gate)"
     if not args.no_gate and not (flows and world > 1 and args.dist_backend == "gloo"):
         try:
-            gate = Gate(ingot_amd, ctx)
+            stagger = (args.stagger_us if args.stagger_us is not None
+                       else STAGGER_US.get(args.config, 0.0))
+            gate = Gate(ingot_amd, ctx, stagger)
             gate_note = (f"first {Gate.HOLD} launches held behind a doorbell "
                          "(ingot_gpu_doorbell_wait); region from the first step's start")
+            if stagger and args.streams > 1:
+                gate_note += (f"; stream i starts i x {stagger:g} us behind stream 0 "
+                              "(ingot_gpu_stream_delay), inside the region")
         except RuntimeError as e:
             gate_note = f"unavailable ({e}); region from host submission"
     main_run = runner(args.streams, args.record)

@@ -381,6 +381,18 @@ int ingot_gpu_doorbell_ring(ingot_gpu_doorbell* db, uint32_t value);
 void ingot_gpu_doorbell_destroy(ingot_gpu_doorbell* db);
 
 /*
+ * Staggered streams.  A consumer that alternates its batches over two (or
+ * more) streams keeps one launch ramping up while another drains; started
+ * together, the streams' launches ramp and drain in lockstep and that
+ * overlap is lost until they drift apart.  ingot_gpu_stream_delay enqueues
+ * on `stream` a one-wave wait of `ns` nanoseconds of the device's wall clock
+ * (everything enqueued after it starts that much later); enqueued right after
+ * a doorbell wait, it starts a second stream behind the first.
+ * ENODEV when the device reports no wall-clock rate.
+ */
+int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
+
+/*
  * Tuning knobs (results never depend on them).  Defaults are the measured
  * best on MI355X; value 0 restores the default.
  *   INGOT_TUNE_WINDOW_INDEXED  16-B chunks staged in LDS per packed frame:
@@ -395,10 +407,14 @@ void ingot_gpu_doorbell_destroy(ingot_gpu_doorbell* db);
  *                              (double-buffered LDS).  0 = on, 2 blocks per CU
  *                              (default); 1 = off; k >= 2 = k tiles per wave
  *   INGOT_TUNE_CACHE_POLICY    0 = measured default (non-temporal record
- *                              stores; non-temporal staging loads in the
- *                              ring kernel only); else bit 0: stage frame
+ *                              stores; the ring kernel: non-temporal staging
+ *                              loads and, for 16-B records, device-scope
+ *                              record stores); else bit 0: stage frame
  *                              bytes with non-temporal loads, bit 1:
- *                              non-temporal record stores (4 = neither)
+ *                              non-temporal record stores (4 = neither);
+ *                              bits 3-5, when non-zero, set the record
+ *                              stores' cache bits instead of bit 1: 1 sc1,
+ *                              2 sc1 nt, 3 sc0 sc1, 4 sc0 sc1 nt, 5 sc0
  *   INGOT_TUNE_PIPE_DEPTH      the multi-tile ring kernel's tiles in flight
  *                              per wave (LDS images): 2 (default), 3 or 4
  *                              (the rewrite ring kernel: 2 or 3)

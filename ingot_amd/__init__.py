@@ -133,6 +133,16 @@ class Context:
     def get_tuning(self, key: int) -> int:
         return int(self._lib.ingot_gpu_ctx_get_tuning(self._h, int(key)))
 
+    def stream_delay(self, ns: int, stream=None) -> None:
+        """ingot_gpu_stream_delay: work enqueued on `stream` after this call
+        starts `ns` nanoseconds (device wall clock) later — staggers the
+        streams of a multi-stream ring consumer."""
+        if not 0 <= int(ns) < (1 << 32):
+            raise ValueError(f"ns out of range: {ns}")
+        _lib.check(self._lib.ingot_gpu_stream_delay(self._h, int(ns),
+                                                    _stream(stream, self.device)),
+                   "ingot_gpu_stream_delay")
+
     def parse_packed(self, arena, lens, chain: Chain, out=None, off_out=None, workspace=None,
                      stream=None):
         """ingot_gpu_parse_packed: frames back to back in `arena`, only their

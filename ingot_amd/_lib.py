@@ -41,6 +41,7 @@ SIGNATURES = {
                                                ctypes.c_void_p]),
     "ingot_gpu_doorbell_ring": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
     "ingot_gpu_doorbell_destroy": (None, [ctypes.c_void_p]),
+    "ingot_gpu_stream_delay": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
     "ingot_gpu_ctx_set_tuning": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "ingot_gpu_ctx_get_tuning": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ingot_gpu_parse": (

@@ -19,6 +19,7 @@
 struct ingot_gpu_ctx {
     int device;
     ingot_gpu::Tuning tuning;
+    uint32_t wall_khz = 0;  // the device's constant-rate wall clock (stream delays)
     // device address ranges of host memory mapped by ingot_gpu_host_map
     std::mutex mu;
     std::vector<std::pair<uintptr_t, uintptr_t>> host;
@@ -161,6 +162,10 @@ int ingot_gpu_ctx_create(int device, ingot_gpu_ctx** out) {
     ingot_gpu_ctx* c = new (std::nothrow) ingot_gpu_ctx{device, {}};
     if (!c) return INGOT_GPU_ENOMEM;
     if (prop.multiProcessorCount > 0) c->tuning.cus = (uint32_t)prop.multiProcessorCount;
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess &&
+        khz > 0)
+        c->wall_khz = (uint32_t)khz;
     *out = c;
     return INGOT_GPU_SUCCESS;
 }
@@ -291,6 +296,15 @@ int ingot_gpu_doorbell_ring(ingot_gpu_doorbell* db, uint32_t value) {
     if (!db) return INGOT_GPU_EINVAL;
     __atomic_store_n(db->word, value, __ATOMIC_SEQ_CST);
     return INGOT_GPU_SUCCESS;
+}
+
+int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream) {
+    if (!ctx) return INGOT_GPU_EINVAL;
+    if (ns == 0) return INGOT_GPU_SUCCESS;
+    if (!ctx->wall_khz) return INGOT_GPU_ENODEV;
+    if (int e = enter(ctx)) return e;
+    const uint64_t ticks = ((uint64_t)ns * ctx->wall_khz + 999999u) / 1000000u;
+    return from_hip(ingot_gpu::launch_delay(ticks, (hipStream_t)stream));
 }
 
 void ingot_gpu_doorbell_destroy(ingot_gpu_doorbell* db) {

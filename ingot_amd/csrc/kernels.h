@@ -101,6 +101,10 @@ constexpr uint32_t PACKED_GROUP = 128;
 size_t packed_workspace(uint64_t n);
 hipError_t launch_tile_bases(const uint16_t* len, uint64_t n, void* work, hipStream_t s);
 
+// One wave that holds its stream for `ticks` of the device's constant-rate
+// wall clock (ingot_gpu_stream_delay, packed.hip).
+hipError_t launch_delay(uint64_t ticks, hipStream_t s);
+
 // Per-context tuning (0 = measured default); see INGOT_TUNE_* in ingot_gpu.h.
 struct Tuning {
     int window_indexed = 0;

@@ -58,29 +58,38 @@ __device__ __forceinline__ void stage16(const uint8_t* src, uint32_t* dst, bool 
     else __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)dst, 16, 0, 0);
 }
 
-// One record per lane; `nt` = INGOT_TUNE_CACHE_POLICY bit 1.  The nt store
-// is written as asm: with a plain-store twin in the other branch the compiler
-// merges the two and drops the nontemporal hint.  (An extra store the waitcnt
-// pass cannot see only makes its vmcnt waits stricter; the s_nop covers the
-// store-data VGPR hazard the hazard recognizer cannot see in asm.)
+// One record per lane; `pol` = the INGOT_TUNE_CACHE_POLICY bits: bit 1 stores
+// non-temporal; bits 3-5 (when non-zero) pick the store's scope bits instead
+// (1 sc1, 2 sc1 nt, 3 sc0 sc1, 4 sc0 sc1 nt, 5 sc0: A/B of where the records'
+// dirty lines sit at the end of the kernel).  The stores are written as asm:
+// with a plain-store twin in the other branch the compiler merges the two and
+// drops the hint.  (An extra store the waitcnt pass cannot see only makes its
+// vmcnt waits stricter; the s_nop covers the store-data VGPR hazard the
+// hazard recognizer cannot see in asm.)
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void store_rec(uint4* dst, const uint4& v, bool nt) {
-    if (nt) {
-        const u32x4 x{v.x, v.y, v.z, v.w};
-        asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(dst), "v"(x) : "memory");
-    } else {
-        *dst = v;
+#define INGOT_ST(op, bits) asm volatile(op " %0, %1, off " bits "\n\ts_nop 1" ::"v"(dst), "v"(x) : "memory")
+#define INGOT_ST_SWITCH(op)                                    \
+    switch ((pol >> 3) & 7u) {                                 \
+    case 1: INGOT_ST(op, "sc1"); return;                       \
+    case 2: INGOT_ST(op, "sc1 nt"); return;                    \
+    case 3: INGOT_ST(op, "sc0 sc1"); return;                   \
+    case 4: INGOT_ST(op, "sc0 sc1 nt"); return;                \
+    case 5: INGOT_ST(op, "sc0"); return;                       \
+    default: if (pol & 2u) { INGOT_ST(op, "nt"); return; }     \
     }
+__device__ __forceinline__ void store_rec(uint4* dst, const uint4& v, uint32_t pol) {
+    const u32x4 x{v.x, v.y, v.z, v.w};
+    INGOT_ST_SWITCH("global_store_dwordx4")
+    *dst = v;
 }
-__device__ __forceinline__ void store_rec(uint2* dst, const uint2& v, bool nt) {
-    if (nt) {
-        const u32x2 x{v.x, v.y};
-        asm volatile("global_store_dwordx2 %0, %1, off nt\n\ts_nop 1" ::"v"(dst), "v"(x) : "memory");
-    } else {
-        *dst = v;
-    }
+__device__ __forceinline__ void store_rec(uint2* dst, const uint2& v, uint32_t pol) {
+    const u32x2 x{v.x, v.y};
+    INGOT_ST_SWITCH("global_store_dwordx2")
+    *dst = v;
 }
+#undef INGOT_ST_SWITCH
+#undef INGOT_ST
 
 // Slot (16-B unit) of chunk c of packet p inside a wave's LDS image.
 // NCH = 4: g(p) = (p>>2)&3; NCH = 8: g(p) = (p>>1)&7 (see header comment);
@@ -1321,7 +1330,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
             }
         } else if constexpr (MODE == OUT_REC8) {
             walk<CHAIN, false>(fr, r, nullptr, nullptr);
-            if (valid) store_rec(static_cast<uint2*>(a.out) + i, pack8(r), a.policy & 2u);
+            if (valid) store_rec(static_cast<uint2*>(a.out) + i, pack8(r), a.policy);
         } else if constexpr (MODE == OUT_MODIFY) {
             // parse, then the setters in order (each sees the previous
             // edits' bytes: put8 updates HBM and the staged window)
@@ -1358,7 +1367,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
             walk<CHAIN, false>(fr, r, nullptr, nullptr);
             if constexpr (SLOW)
                 slow_rewalk<NCH, CHAIN>(fr, r, valid, wimg, lane, a.arena, base, sh, len);
-            if (valid) store_rec(static_cast<uint4*>(a.out) + i, pack(r), a.policy & 2u);
+            if (valid) store_rec(static_cast<uint4*>(a.out) + i, pack(r), a.policy);
         }
         if constexpr (LAYOUT == LAYOUT_SEGMENTED) {
             if (valid && a.chunk) a.chunk[i] = (uint16_t)fr.k;
@@ -1492,7 +1501,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
             }
         } else {
             walk<CHAIN, false>(fr, r, nullptr, nullptr);
-            if (valid) store_rec(static_cast<uint4*>(a.out) + i, pack(r), a.policy & 2u);
+            if (valid) store_rec(static_cast<uint4*>(a.out) + i, pack(r), a.policy);
         }
         if (valid && a.chunk) a.chunk[i] = (uint16_t)fr.k;
         // the next tile's LDS-DMA overwrites this image: every lane's reads
@@ -1660,7 +1669,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse_pipe(ParseArgs a) {
     const uint64_t ntiles = (a.n + WAVE - 1u) / WAVE;
     const uint64_t step = (uint64_t)gridDim.x * WAVES;
     const uint32_t take = a.stride < WIN ? a.stride : WIN;
-    const bool nt_ld = a.policy & 1u, nt_st = a.policy & 2u;
+    const bool nt_ld = a.policy & 1u;
 
     auto stage = [&](uint64_t tt, uint32_t* img) {
 #pragma unroll
@@ -1679,8 +1688,8 @@ __global__ __launch_bounds__(BLOCK) void k_parse_pipe(ParseArgs a) {
         Rec r;
         walk<CHAIN, false>(fr, r, nullptr, nullptr);
         if (i < a.n) {
-            if constexpr (MODE == OUT_REC8) store_rec(static_cast<uint2*>(a.out) + i, pack8(r), nt_st);
-            else store_rec(static_cast<uint4*>(a.out) + i, pack(r), nt_st);
+            if constexpr (MODE == OUT_REC8) store_rec(static_cast<uint2*>(a.out) + i, pack8(r), a.policy);
+            else store_rec(static_cast<uint4*>(a.out) + i, pack(r), a.policy);
         }
     };
 
@@ -1781,7 +1790,7 @@ __global__ __launch_bounds__(BLOCK) void k_modify_pipe(ModifyArgs m) {
                 }
             }
         }
-        if (valid && a.out) store_rec(static_cast<uint4*>(a.out) + i, pack(r), a.policy & 2u);
+        if (valid && a.out) store_rec(static_cast<uint4*>(a.out) + i, pack(r), a.policy);
         // every lane's staged edits are in LDS before any lane reads them back
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1796,7 +1805,7 @@ __global__ __launch_bounds__(BLOCK) void k_modify_pipe(ModifyArgs m) {
                 const uint32_t* src = img + q * 4u;
                 const uint4 v = make_uint4(src[0], src[1], src[2], src[3]);
                 store_rec(reinterpret_cast<uint4*>(arena + (tt * WAVE + pp) * a.stride + 16u * c),
-                          v, a.policy & 2u);
+                          v, a.policy);
             }
         }
     };
@@ -1956,13 +1965,18 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
     // staged non-temporal only by the ring kernel, whose window is the whole
     // 64-B slot (C2 single stream 16.8 -> 15.1 us, two streams 13.5 -> 12.2);
     // elsewhere bytes past the window are re-read from L2, and nt staging
-    // costs 19% (C3) / 15% (C3s).  4 = plain loads and stores.
+    // costs 19% (C3) / 15% (C3s).  The ring kernel's 16-B records are stored
+    // at device scope (`sc1`, written through the XCD's L2) instead of nt:
+    // 2 streams 12.32 -> 11.90 us/step, 1 stream 15.33 -> 15.19 (interleaved
+    // A/B, profiles/r02_store_scope_ab.json); 8-B records, the rewrite ring
+    // and the packed / slotted kernels gain nothing from it (or lose: C3 sc1
+    // without nt 588 -> 608 us).  4 = plain loads and stores.
     const bool ring = t.pipeline != 1 && !t.window_strided && layout_kind == LAYOUT_STRIDED &&
                       !a.len && chain != INGOT_CHAIN_GENEVE_OVER_V6 && a.stride >= 64u &&
                       (a.stride == 64u || !t.host_arena) &&
                       (mode == OUT_REC16 || mode == OUT_REC8);
-    if (t.cache_policy == 0) a.policy = mode == OUT_FIELDS ? 0u : ring ? 3u : 2u;
-    else a.policy = (uint32_t)t.cache_policy & 3u;
+    if (t.cache_policy == 0) a.policy = mode == OUT_FIELDS ? 0u : ring ? (mode == OUT_REC16 ? 11u : 3u) : 2u;
+    else a.policy = (uint32_t)t.cache_policy & 0x3bu;
     const uint32_t g = grid_for(a.n, t.max_blocks);
     // parse_read over chunk lists: chunk 0 staged in a 4-chunk (64-B) window
     // (first mblk-style chunks are short header blocks), the rest from L2/HBM.
@@ -2090,7 +2104,7 @@ hipError_t launch_modify(const ModifyArgs& args, int layout_kind, int chain, con
     if (t.pipeline != 1 && !t.window_strided && layout_kind == LAYOUT_STRIDED && !a.p.len &&
         !tun && a.p.stride >= 64u) {
         a.wb = t.writeback ? (uint32_t)t.writeback : kModifyRingWb;
-        a.p.policy = t.cache_policy ? (uint32_t)t.cache_policy & 3u : kModifyRingPolicy;
+        a.p.policy = t.cache_policy ? (uint32_t)t.cache_policy & 0x3bu : kModifyRingPolicy;
         const uint64_t tiles = (a.p.n + WAVE - 1) / WAVE;
         uint64_t blocks;
         if (t.pipeline > 1) {
@@ -2207,8 +2221,8 @@ bool tuning_valid(int key, int value) {
         return value >= 0;
     case INGOT_TUNE_PIPELINE:
         return value >= 0 && value <= 64;
-    case INGOT_TUNE_CACHE_POLICY:
-        return value >= 0 && value <= 4;
+    case INGOT_TUNE_CACHE_POLICY:  // 0-4, or bits 0-1 with a store variant in bits 3-5
+        return (value >= 0 && value <= 4) || (value >= 8 && value < 48 && ((value >> 3) & 7) <= 5);
     case INGOT_TUNE_PIPE_DEPTH:
         return value == 0 || (value >= 2 && value <= 4);
     case INGOT_TUNE_WRITEBACK:

@@ -84,3 +84,34 @@ def test_ring_releases_several_streams(env):
     for o in outs:
         assert np.array_equal(o.cpu().numpy().reshape(-1), want.view(np.uint8).reshape(-1))
     db.close()
+
+
+def test_stream_delay_holds_the_stream(env):
+    """ingot_gpu_stream_delay: work enqueued after it starts `ns` later (device
+    wall clock); 0 is a no-op; the parse behind it is unchanged."""
+    torch, ctx = env
+    s = torch.cuda.Stream()
+    arena, _, _ = ingot_amd.gen_frames(GenProfile.V4UDP64, 4096, stride=64)
+    torch.cuda.synchronize()
+    for ns in (0, 20_000, 200_000):
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        ctx.stream_delay(ns, s)
+        b.record(s)
+        got = ctx.parse_strided(arena, 64, 4096, Chain.UdpParser, stream=s)
+        s.synchronize()
+        us = a.elapsed_time(b) * 1e3
+        assert ns / 1e3 <= us + 1.0, (ns, us)  # one 100-MHz tick of slack
+        assert us < ns / 1e3 + 2_000, (ns, us)
+        want = oracle.parse_batch(arena.cpu().numpy(), None, None, Chain.UdpParser, stride=64,
+                                  n=4096)
+        assert got.cpu().numpy().tobytes() == want.tobytes()
+
+
+def test_stream_delay_rejects_bad_arguments(env):
+    _, ctx = env
+    with pytest.raises(ValueError):
+        ctx.stream_delay(-1)
+    with pytest.raises(ValueError):
+        ctx.stream_delay(1 << 32)
