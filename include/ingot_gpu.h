@@ -414,7 +414,9 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              non-temporal record stores (4 = neither);
  *                              bits 3-5, when non-zero, set the record
  *                              stores' cache bits instead of bit 1: 1 sc1,
- *                              2 sc1 nt, 3 sc0 sc1, 4 sc0 sc1 nt, 5 sc0
+ *                              2 sc1 nt, 3 sc0 sc1, 4 sc0 sc1 nt, 5 sc0;
+ *                              bits 6-8, when non-zero, the staging loads'
+ *                              instead of bit 0 (same codes, 6 sc0 nt)
  *   INGOT_TUNE_PIPE_DEPTH      the multi-tile ring kernel's tiles in flight
  *                              per wave (LDS images): 2 (default), 3 or 4
  *                              (the rewrite ring kernel: 2 or 3)

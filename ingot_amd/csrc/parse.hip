@@ -57,6 +57,24 @@ __device__ __forceinline__ void stage16(const uint8_t* src, uint32_t* dst, bool 
     if (nt) __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)dst, 16, 0, 2);
     else __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)dst, 16, 0, 0);
 }
+// The same with the policy word: bits 6-8, when non-zero, pick the staging
+// loads' cache bits instead of bit 0 (1 sc1, 2 sc1 nt, 3 sc0 sc1, 4 sc0 sc1
+// nt, 5 sc0, 6 sc0 nt) — A/B of where the frame lines are allocated.
+__device__ __forceinline__ void stage16p(const uint8_t* src, uint32_t* dst, uint32_t pol) {
+#define INGOT_LD(bits) __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)dst, 16, 0, bits)
+    switch ((pol >> 6) & 7u) {
+    case 1: INGOT_LD(16); return;
+    case 2: INGOT_LD(18); return;
+    case 3: INGOT_LD(17); return;
+    case 4: INGOT_LD(19); return;
+    case 5: INGOT_LD(1); return;
+    case 6: INGOT_LD(3); return;
+    default:
+        if (pol & 1u) INGOT_LD(2);
+        else INGOT_LD(0);
+    }
+#undef INGOT_LD
+}
 
 // One record per lane; `pol` = the INGOT_TUNE_CACHE_POLICY bits: bit 1 stores
 // non-temporal; bits 3-5 (when non-zero) pick the store's scope bits instead
@@ -1285,7 +1303,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
             } else {
                 bp = (int64_t)__shfl((long long)base, (int)pp);
             }
-            if (c < np) stage16(a.arena + bp + 16u * c, wimg + k * WAVE * 4u, a.policy & 1u);
+            if (c < np) stage16p(a.arena + bp + 16u * c, wimg + k * WAVE * 4u, a.policy);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
@@ -1669,7 +1687,6 @@ __global__ __launch_bounds__(BLOCK) void k_parse_pipe(ParseArgs a) {
     const uint64_t ntiles = (a.n + WAVE - 1u) / WAVE;
     const uint64_t step = (uint64_t)gridDim.x * WAVES;
     const uint32_t take = a.stride < WIN ? a.stride : WIN;
-    const bool nt_ld = a.policy & 1u;
 
     auto stage = [&](uint64_t tt, uint32_t* img) {
 #pragma unroll
@@ -1679,7 +1696,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse_pipe(ParseArgs a) {
             const uint32_t c = (q - pp * NCH) ^ swz<NCH>(pp);
             uint64_t slot = tt * WAVE + pp;
             if (slot >= a.n) slot = a.n - 1u;  // a valid address for the tail tile
-            stage16(a.arena + slot * a.stride + 16u * c, img + k * WAVE * 4u, nt_ld);
+            stage16p(a.arena + slot * a.stride + 16u * c, img + k * WAVE * 4u, a.policy);
         }
     };
     auto parse = [&](uint64_t tt, const uint32_t* img) {
@@ -1976,7 +1993,7 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
                       (a.stride == 64u || !t.host_arena) &&
                       (mode == OUT_REC16 || mode == OUT_REC8);
     if (t.cache_policy == 0) a.policy = mode == OUT_FIELDS ? 0u : ring ? (mode == OUT_REC16 ? 11u : 3u) : 2u;
-    else a.policy = (uint32_t)t.cache_policy & 0x3bu;
+    else a.policy = (uint32_t)t.cache_policy & 0x1fbu;
     const uint32_t g = grid_for(a.n, t.max_blocks);
     // parse_read over chunk lists: chunk 0 staged in a 4-chunk (64-B) window
     // (first mblk-style chunks are short header blocks), the rest from L2/HBM.
@@ -2221,8 +2238,9 @@ bool tuning_valid(int key, int value) {
         return value >= 0;
     case INGOT_TUNE_PIPELINE:
         return value >= 0 && value <= 64;
-    case INGOT_TUNE_CACHE_POLICY:  // 0-4, or bits 0-1 with a store variant in bits 3-5
-        return (value >= 0 && value <= 4) || (value >= 8 && value < 48 && ((value >> 3) & 7) <= 5);
+    case INGOT_TUNE_CACHE_POLICY:  // 0-4, or bits 0-1 with store (3-5) / load (6-8) variants
+        return (value >= 0 && value <= 4) ||
+               (value >= 8 && value < 512 && ((value >> 3) & 7) <= 5 && ((value >> 6) & 7) <= 6);
     case INGOT_TUNE_PIPE_DEPTH:
         return value == 0 || (value >= 2 && value <= 4);
     case INGOT_TUNE_WRITEBACK:

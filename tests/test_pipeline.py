@@ -17,7 +17,8 @@ pytestmark = pytest.mark.gpu
                                            (8, 0, 0), (16, 0, 0), (0, 3, 0), (2, 3, 1),
                                            (5, 3, 2), (0, 4, 3), (3, 4, 0), (1, 0, 3),
                                            (0, 0, 4), (1, 0, 4), (0, 0, 11), (0, 0, 19),
-                                           (0, 0, 27), (0, 0, 35), (0, 0, 43), (1, 0, 26)])
+                                           (0, 0, 27), (0, 0, 35), (0, 0, 43), (1, 0, 26), (0, 0, 75),
+                                           (0, 0, 267), (1, 0, 386)])
 @pytest.mark.parametrize("n", [1, 63, 65, 100_003, 1 << 20])
 def test_pipelined_ring_bit_exact(tpw, depth, pol, n):
     import torch
