@@ -396,9 +396,13 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  * Tuning knobs (results never depend on them).  Defaults are the measured
  * best on MI355X; value 0 restores the default.
  *   INGOT_TUNE_WINDOW_INDEXED  16-B chunks staged in LDS per packed frame:
- *                              2,3,4,5,6,8,9, or 100 = no staging (default 2
- *                              for records, 3 for fields / rewrites, 8 for
- *                              the tunnel chain, 5 in mapped host memory)
+ *                              2,3,4,5,6,8,9, or 100 = no staging; 20 + k:
+ *                              record / flow modes, a window from byte 12's
+ *                              chunk to the end of the 128-B line its second
+ *                              chunk lies in, at most k chunks (packed
+ *                              frames: k = 2, 3, 5 or 8).  Default 25 for
+ *                              records, 3 for fields / rewrites, 5 for flows
+ *                              and in mapped host memory, 8 for the tunnel
  *   INGOT_TUNE_WINDOW_STRIDED  16-B chunks staged per slot: 2,3,4,5,8 or 100
  *                              (default 4 for slots <= 64 B, else 3)
  *   INGOT_TUNE_MAX_BLOCKS      grid cap in 256-thread blocks (0 = one

@@ -1282,7 +1282,18 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
             take = NCH == 0 ? 0u : (len < WIN - sh ? len : WIN - sh);
             nch = (sh + take + 15u) >> 4;
         } else {
-            const uint32_t wend = SKIP + WIN - sh;  // frame byte after the window
+            uint32_t wend = SKIP + WIN - sh;  // frame byte after the window
+            if (a.linewin) {
+                // Line-completing window: stage up to the end of the 128-B
+                // line the second chunk lies in (at least 2 chunks, at most
+                // NCH).  HBM moves those lines whole anyway; staging the
+                // rest of them spares the walk re-reading their bytes past
+                // a fixed window from L2 after the line has been evicted.
+                const uint32_t lp = (uint32_t)((uintptr_t)(a.arena + base) >> 4) & 7u;
+                uint32_t want = lp == 7u ? 9u : 8u - lp;
+                if (want > NCH) want = NCH;
+                wend = SKIP + 16u * want - sh;
+            }
             take = len < wend ? len : wend;
             const int32_t staged = (int32_t)take - ((int32_t)SKIP - (int32_t)sh);
             nch = staged > 0 ? ((uint32_t)staged + 15u) >> 4 : 0u;
@@ -2080,15 +2091,27 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
         if (w == 5) return launch_mode<5, LAYOUT_STRIDED>(a, chain, mode, g, s);
         return launch_mode<8, LAYOUT_STRIDED>(a, chain, mode, g, s);
     }
-    // Records on frames addressed by offset: 2 chunks from the one holding
-    // byte 12 (the walk reads the ethertype, IPv4 ihl / protocol and the IPv6
-    // next header there; TCP's data offset and EH chains are read past the
-    // window): C3 587 -> 575 us, C4 302 -> 301 (round 2, interleaved,
-    // profiles/r02_window_ab.json); field and rewrite modes read more of each
-    // header and keep 3.
-    const int wrec = (mode == OUT_REC16 || mode == OUT_REC8) ? 2 : 3;
+    // Records on frames addressed by offset (device arenas, not the tunnel):
+    // a line-completing window (ParseArgs::linewin) from the chunk holding
+    // byte 12 to the end of the 128-B line its second chunk lies in, at most
+    // 5 chunks.  The walk reads the ethertype, IPv4 ihl / protocol and the
+    // IPv6 next header in its first two chunks; the rest of that line comes
+    // along in the same HBM fetch, so TCP's data offset and EH bytes there
+    // are read from LDS instead of from an L2 line that has often been
+    // evicted by then.  PMC read bytes per C3 frame: fixed 2 chunks 217,
+    // 3 chunks 206, line-completing 172 — the line floor of the walk's bytes
+    // is 169 (tools/line_floor.py); us per launch C3 562 -> 544, C3p 583 ->
+    // 553, C4 302 -> 288 (round 2, interleaved; profiles/r02_window_ab.json).
+    // Flows (which need the 5-tuple past the first line) and the tunnel's
+    // 128-B outer span lose with it; field and rewrite modes keep 3 chunks.
+    int wi = t.window_indexed;
+    if (!wi && (mode == OUT_REC16 || mode == OUT_REC8) && !tun && !host) wi = 25;
+    if (wi > 20) {  // 20 + k: line-completing, up to k chunks
+        a.linewin = 1;
+        wi -= 20;
+    }
     if (layout_kind == LAYOUT_PACKED) {
-        switch (t.window_indexed ? t.window_indexed : tun ? 8 : host ? 5 : wrec) {
+        switch (wi ? wi : tun ? 8 : host ? 5 : 3) {
         case 2: return launch_mode<2, LAYOUT_PACKED>(a, chain, mode, g, s);
         case 3: return launch_mode<3, LAYOUT_PACKED>(a, chain, mode, g, s);
         case 8: return launch_mode<8, LAYOUT_PACKED>(a, chain, mode, g, s);
@@ -2100,7 +2123,7 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
     if (t.slow_path == 1 && mode == OUT_REC16 && !host && !t.window_indexed)
         return tun ? launch_chain<8, LAYOUT_INDEXED, OUT_REC16, ParseArgs, 1>(a, chain, g, s)
                    : launch_chain<3, LAYOUT_INDEXED, OUT_REC16, ParseArgs, 1>(a, chain, g, s);
-    switch (t.window_indexed ? t.window_indexed : tun ? 8 : host ? 5 : wrec) {
+    switch (wi ? wi : tun ? 8 : host ? 5 : 3) {
     case 100: return launch_mode<0, LAYOUT_INDEXED>(a, chain, mode, g, s);
     case 2: return launch_mode<2, LAYOUT_INDEXED>(a, chain, mode, g, s);
     case 3: return launch_mode<3, LAYOUT_INDEXED>(a, chain, mode, g, s);
@@ -2209,7 +2232,19 @@ hipError_t launch_flows_mode(const FlowArgs& a, int layout_kind, int chain, cons
         default: return launch_chain<5, LAYOUT_STRIDED, MODE>(a, chain, g, s, pc);
         }
     }
-    switch (t.window_indexed ? t.window_indexed : 5) {
+    int wi = t.window_indexed;
+    if (wi > 20) {  // line-completing windows (ParseArgs::linewin), up to wi - 20 chunks
+        FlowArgs b = a;
+        b.p.linewin = 1;
+        switch (wi - 20) {
+        case 3: return launch_chain<3, LAYOUT_INDEXED, MODE>(b, chain, g, s, pc);
+        case 4: return launch_chain<4, LAYOUT_INDEXED, MODE>(b, chain, g, s, pc);
+        case 6: return launch_chain<6, LAYOUT_INDEXED, MODE>(b, chain, g, s, pc);
+        case 8: return launch_chain<8, LAYOUT_INDEXED, MODE>(b, chain, g, s, pc);
+        default: return launch_chain<5, LAYOUT_INDEXED, MODE>(b, chain, g, s, pc);
+        }
+    }
+    switch (wi ? wi : 5) {
     case 3: return launch_chain<3, LAYOUT_INDEXED, MODE>(a, chain, g, s, pc);
     case 4: return launch_chain<4, LAYOUT_INDEXED, MODE>(a, chain, g, s, pc);
     case 6: return launch_chain<6, LAYOUT_INDEXED, MODE>(a, chain, g, s, pc);
@@ -2237,9 +2272,9 @@ hipError_t launch_flows(const FlowArgs& a, int layout_kind, int chain, const Tun
 
 bool tuning_valid(int key, int value) {
     switch (key) {
-    case INGOT_TUNE_WINDOW_INDEXED:
+    case INGOT_TUNE_WINDOW_INDEXED:  // 20 + k: line-completing, up to k chunks
         return value == 0 || (value >= 2 && value <= 6) || value == 8 || value == 9 ||
-               value == 100;
+               value == 100 || (value >= 22 && value <= 26) || value == 28 || value == 29;
     case INGOT_TUNE_WINDOW_STRIDED:
         return value == 0 || (value >= 2 && value <= 5) || value == 8 || value == 100;
     case INGOT_TUNE_MAX_BLOCKS:

@@ -117,7 +117,8 @@ def test_flow_hist_bit_exact(profile, chain, stride):
 @pytest.mark.parametrize("tune", [{}, {"win": 3}, {"win": 4}, {"win": 5}, {"win": 8},
                                   {"blocks": 7}, {"blocks": 1, "win": 3}, {"fk": 1},
                                   {"fk": 1, "blocks": 3}, {"fk": 2}, {"fk": 2, "win": 4},
-                                  {"fk": 2, "blocks": 3}])
+                                  {"fk": 2, "blocks": 3}, {"win": 25}, {"win": 26}, {"win": 28},
+                                  {"fk": 2, "win": 25}, {"win": 25, "blocks": 3}])
 @pytest.mark.parametrize("profile,chain,stride", [
     ("FLOWS", "VlanUlp", None), ("ADVERSARIAL", "GenericUlp", None),
     ("GENEVE_ADVERSARIAL", "GeneveOverV6Tunnel", None), ("VLAN_V6EH", "VlanUlp", 256),
@@ -138,7 +139,7 @@ def test_flow_kernels_every_setting(tune, profile, chain, stride):
     n = 100_003
     ctx = ingot_amd.Context(0)
     ctx.set_tuning(TUNE_FLOW_KERNEL, tune.get("fk", 0))
-    if "win" in tune:
+    if "win" in tune and not (stride and tune["win"] > 20):  # 20 + k: offset-addressed only
         ctx.set_tuning(TUNE_WINDOW_STRIDED if stride else TUNE_WINDOW_INDEXED, tune["win"])
     if "blocks" in tune:
         ctx.set_tuning(TUNE_MAX_BLOCKS, tune["blocks"])
@@ -162,7 +163,7 @@ def test_flow_kernels_every_setting(tune, profile, chain, stride):
 @pytest.mark.gpu
 @pytest.mark.parametrize("table", [0, 32])
 @pytest.mark.parametrize("tune", [{}, {"win": 3}, {"win": 4}, {"win": 8}, {"blocks": 5},
-                                  {"fk": 1}, {"fk": 2}])
+                                  {"fk": 1}, {"fk": 2}, {"win": 25}])
 @pytest.mark.parametrize("bins", [1 << 16, 1024])
 @pytest.mark.parametrize("profile,chain,stride", [
     ("FLOWS", "VlanUlp", None), ("ADVERSARIAL", "GenericUlp", None),
@@ -185,7 +186,7 @@ def test_flow_bins_without_hashes(table, tune, bins, profile, chain, stride):
     ctx = ingot_amd.Context(0)
     ctx.set_tuning(TUNE_FLOW_TABLE, table)
     ctx.set_tuning(TUNE_FLOW_KERNEL, tune.get("fk", 0))
-    if "win" in tune:
+    if "win" in tune and not (stride and tune["win"] > 20):  # 20 + k: offset-addressed only
         ctx.set_tuning(TUNE_WINDOW_STRIDED if stride else TUNE_WINDOW_INDEXED, tune["win"])
     if "blocks" in tune:
         ctx.set_tuning(TUNE_MAX_BLOCKS, tune["blocks"])

@@ -226,13 +226,21 @@ def test_every_window_setting_is_bit_exact(torch):
     sarena, _, slens = ingot_amd.gen_frames(GenProfile.VLAN_V6EH, 40_000, seed=32, stride=256)
     want_i = {c: oracle_all(arena, off, lens, c) for c in Chain}
     want_s = {c: oracle_all(sarena, None, slens, c, stride=256, n=40_000) for c in Chain}
-    for w in (2, 3, 4, 5, 6, 8, 9, 100):
+    for w in (2, 3, 4, 5, 6, 8, 9, 100, 22, 23, 24, 25, 26, 28, 29):
         c = ingot_amd.Context(0)
         c.set_tuning(TUNE_WINDOW_INDEXED, w)
-        if w != 6 and w != 9:
+        if w in (2, 3, 4, 5, 8, 100):
             c.set_tuning(TUNE_WINDOW_STRIDED, w)
         for chain in Chain:
             r = c.parse(arena, off, lens, chain)
+            if w > 20:  # line-completing windows: 8-B records and packed frames too
+                r8 = c.parse_compact(arena, off, lens, chain) if chain != TUN else None
+                rp = c.parse_packed(arena, lens, chain)
+                torch.cuda.synchronize()
+                assert rp.cpu().numpy().tobytes() == want_i[chain][0].tobytes(), (w, chain)
+                if r8 is not None:
+                    w8 = ingot_amd.rec16_to_rec8(want_i[chain][0])
+                    assert r8.cpu().numpy().tobytes() == w8.tobytes(), (w, chain)
             f = dev_fields(c, arena, off, lens, chain)
             rs = c.parse_strided(sarena, 256, 40_000, chain, lens=slens)
             fs = dev_fields(c, sarena, None, slens, chain, stride=256, n=40_000)
