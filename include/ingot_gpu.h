@@ -400,9 +400,11 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              record / flow modes, a window from byte 12's
  *                              chunk to the end of the 128-B line its second
  *                              chunk lies in, at most k chunks (packed
- *                              frames: k = 2, 3, 5 or 8).  Default 25 for
- *                              records, 3 for fields / rewrites, 5 for flows
- *                              and in mapped host memory, 8 for the tunnel
+ *                              frames: k = 2, 3, 5 or 8); 1000 + 10 m + k:
+ *                              the same from at least m chunks.  Defaults:
+ *                              records 25 (the tunnel chain 1069; packed
+ *                              tunnel frames 8), flows 1045, fields /
+ *                              rewrites 3 (tunnel 8), mapped host memory 5
  *   INGOT_TUNE_WINDOW_STRIDED  16-B chunks staged per slot: 2,3,4,5,8 or 100
  *                              (default 4 for slots <= 64 B, else 3)
  *   INGOT_TUNE_MAX_BLOCKS      grid cap in 256-thread blocks (0 = one

@@ -50,7 +50,7 @@ struct ParseArgs {
     uint64_t* off_out = nullptr;        // LAYOUT_PACKED, optional: the computed offsets
     const uint32_t* tile_local = nullptr;  // LAYOUT_PACKED: tile prefix within its group
     uint32_t policy = 0;                // INGOT_TUNE_CACHE_POLICY bits (launch_parse sets it)
-    uint32_t linewin = 0;  // windows from byte 12: end at the 128-B line end (>= 2 chunks)
+    uint32_t linewin = 0;  // windows from byte 12: >= linewin chunks, then to the line end
 };
 
 struct FlowArgs {

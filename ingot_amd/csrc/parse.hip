@@ -1285,12 +1285,12 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
             uint32_t wend = SKIP + WIN - sh;  // frame byte after the window
             if (a.linewin) {
                 // Line-completing window: stage up to the end of the 128-B
-                // line the second chunk lies in (at least 2 chunks, at most
-                // NCH).  HBM moves those lines whole anyway; staging the
+                // line chunk linewin - 1 lies in (at least linewin chunks, at
+                // most NCH).  HBM moves those lines whole anyway; staging the
                 // rest of them spares the walk re-reading their bytes past
                 // a fixed window from L2 after the line has been evicted.
                 const uint32_t lp = (uint32_t)((uintptr_t)(a.arena + base) >> 4) & 7u;
-                uint32_t want = lp == 7u ? 9u : 8u - lp;
+                uint32_t want = ((lp + a.linewin + 7u) & ~7u) - lp;
                 if (want > NCH) want = NCH;
                 wend = SKIP + 16u * want - sh;
             }
@@ -2102,12 +2102,18 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
     // 3 chunks 206, line-completing 172 — the line floor of the walk's bytes
     // is 169 (tools/line_floor.py); us per launch C3 562 -> 544, C3p 583 ->
     // 553, C4 302 -> 288 (round 2, interleaved; profiles/r02_window_ab.json).
-    // Flows (which need the 5-tuple past the first line) and the tunnel's
-    // 128-B outer span lose with it; field and rewrite modes keep 3 chunks.
+    // The tunnel chain's records (outer headers ~80 B, the inner chain past
+    // them) take at least 6 chunks, then to the line end, at most 9: C6 400 ->
+    // 394 us (fixed 8; a minimum of 2 loses: 468).  Field and rewrite modes
+    // keep fixed windows.
     int wi = t.window_indexed;
-    if (!wi && (mode == OUT_REC16 || mode == OUT_REC8) && !tun && !host) wi = 25;
-    if (wi > 20) {  // 20 + k: line-completing, up to k chunks
-        a.linewin = 1;
+    if (!wi && (mode == OUT_REC16 || mode == OUT_REC8) && !host)
+        wi = !tun ? 25 : layout_kind == LAYOUT_INDEXED ? 1069 : 0;
+    if (wi > 1000) {  // 1000 + 10 m + k: line-completing, m to k chunks
+        a.linewin = (uint32_t)(wi - 1000) / 10u;
+        wi = (wi - 1000) % 10;
+    } else if (wi > 20 && wi < 100) {  // 20 + k: line-completing, 2 to k chunks
+        a.linewin = 2;
         wi -= 20;
     }
     if (layout_kind == LAYOUT_PACKED) {
@@ -2232,11 +2238,16 @@ hipError_t launch_flows_mode(const FlowArgs& a, int layout_kind, int chain, cons
         default: return launch_chain<5, LAYOUT_STRIDED, MODE>(a, chain, g, s, pc);
         }
     }
+    // Device arenas: a line-completing window of 4 to 5 chunks (the 5-tuple
+    // of an untagged v4 frame ends 26 B past byte 12's chunk, a v6 one 46 B):
+    // C5 flows kernel 330 -> 326 us (fixed 5; 4 to 6 chunks 367, 3 to 5 392;
+    // round 2, interleaved, profiles/r02_window_ab.json).
     int wi = t.window_indexed;
-    if (wi > 20) {  // line-completing windows (ParseArgs::linewin), up to wi - 20 chunks
+    if (!wi && !t.host_arena && layout_kind == LAYOUT_INDEXED) wi = 1045;
+    if (wi > 20 && wi != 100) {  // line-completing windows (ParseArgs::linewin)
         FlowArgs b = a;
-        b.p.linewin = 1;
-        switch (wi - 20) {
+        b.p.linewin = wi > 1000 ? (uint32_t)(wi - 1000) / 10u : 2u;
+        switch (wi > 1000 ? (wi - 1000) % 10 : wi - 20) {
         case 3: return launch_chain<3, LAYOUT_INDEXED, MODE>(b, chain, g, s, pc);
         case 4: return launch_chain<4, LAYOUT_INDEXED, MODE>(b, chain, g, s, pc);
         case 6: return launch_chain<6, LAYOUT_INDEXED, MODE>(b, chain, g, s, pc);
@@ -2274,7 +2285,10 @@ bool tuning_valid(int key, int value) {
     switch (key) {
     case INGOT_TUNE_WINDOW_INDEXED:  // 20 + k: line-completing, up to k chunks
         return value == 0 || (value >= 2 && value <= 6) || value == 8 || value == 9 ||
-               value == 100 || (value >= 22 && value <= 26) || value == 28 || value == 29;
+               value == 100 || (value >= 22 && value <= 26) || value == 28 || value == 29 ||
+               (value > 1000 && value < 1100 && (value - 1000) / 10 >= 1 &&
+                (value - 1000) / 10 <= (value - 1000) % 10 &&
+                ((value - 1000) % 10 >= 2 && (value - 1000) % 10 != 7));
     case INGOT_TUNE_WINDOW_STRIDED:
         return value == 0 || (value >= 2 && value <= 5) || value == 8 || value == 100;
     case INGOT_TUNE_MAX_BLOCKS:

@@ -118,7 +118,8 @@ def test_flow_hist_bit_exact(profile, chain, stride):
                                   {"blocks": 7}, {"blocks": 1, "win": 3}, {"fk": 1},
                                   {"fk": 1, "blocks": 3}, {"fk": 2}, {"fk": 2, "win": 4},
                                   {"fk": 2, "blocks": 3}, {"win": 25}, {"win": 26}, {"win": 28},
-                                  {"fk": 2, "win": 25}, {"win": 25, "blocks": 3}])
+                                  {"fk": 2, "win": 25}, {"win": 25, "blocks": 3}, {"win": 1045},
+                                  {"win": 1058}])
 @pytest.mark.parametrize("profile,chain,stride", [
     ("FLOWS", "VlanUlp", None), ("ADVERSARIAL", "GenericUlp", None),
     ("GENEVE_ADVERSARIAL", "GeneveOverV6Tunnel", None), ("VLAN_V6EH", "VlanUlp", 256),

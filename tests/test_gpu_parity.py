@@ -226,7 +226,7 @@ def test_every_window_setting_is_bit_exact(torch):
     sarena, _, slens = ingot_amd.gen_frames(GenProfile.VLAN_V6EH, 40_000, seed=32, stride=256)
     want_i = {c: oracle_all(arena, off, lens, c) for c in Chain}
     want_s = {c: oracle_all(sarena, None, slens, c, stride=256, n=40_000) for c in Chain}
-    for w in (2, 3, 4, 5, 6, 8, 9, 100, 22, 23, 24, 25, 26, 28, 29):
+    for w in (2, 3, 4, 5, 6, 8, 9, 100, 22, 23, 24, 25, 26, 28, 29, 1045, 1069, 1099):
         c = ingot_amd.Context(0)
         c.set_tuning(TUNE_WINDOW_INDEXED, w)
         if w in (2, 3, 4, 5, 8, 100):
