@@ -152,7 +152,11 @@ struct Frame {
             const uint32_t b = sh + i;
             const uint32_t a = b & ~3u;
             const uint32_t d0 = dw(a);
-            const uint32_t d1 = ((b & 3u) + n > 4u) ? dw(a + 4u) : 0u;
+            // the second dword only when the bytes straddle it (then it lies
+            // inside the staged chunks); clamped so that a speculated read
+            // stays inside this packet's slots too
+            const uint32_t a1 = a + 4u < 16u * NCH ? a + 4u : a;
+            const uint32_t d1 = ((b & 3u) + n > 4u) ? dw(a1) : 0u;
             const uint32_t x = __builtin_amdgcn_alignbyte(d1, d0, b & 3u);  // bytes b.. little-endian
             v = __builtin_bswap32(x) >> (32u - 8u * n);
         } else if constexpr (PROBE) {
@@ -1201,9 +1205,11 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
     constexpr bool TUN = CHAIN == INGOT_CHAIN_GENEVE_OVER_V6;
     constexpr uint32_t WIN = NCH * 16u;
     constexpr uint32_t WAVE_DW = WAVE * NCH * 4u;  // dwords per wave image
-    // +16 dwords: the second dword of a pair read may run past the last image.
+    // No slack past the last image: every LDS read stays inside its packet's
+    // slots (Frame::be clamps the second dword of a pair, be_words the chunk),
+    // so 5-chunk images take exactly 20 KiB per block and 8 blocks fit a CU.
     // NCH = 0: no staging, every read goes to L2/HBM.
-    __shared__ __attribute__((aligned(16))) uint32_t s_win[WAVES * WAVE_DW + 16];
+    __shared__ __attribute__((aligned(16))) uint32_t s_win[NCH ? WAVES * WAVE_DW : 16];
     constexpr bool FLOWS = MODE == OUT_FLOWS || MODE == OUT_FLOWS16;
     constexpr bool H16 = MODE == OUT_FLOWS16;
     __shared__ __attribute__((aligned(64 * FLOW_COPIES)))
