@@ -33,7 +33,7 @@ FRAG, HOP, DST, RT, MOB, HIP, SHIM, EXP1, EXP2 = 44, 0, 60, 43, 135, 139, 140, 2
 RFC6564 = (HOP, DST, RT, MOB, HIP, SHIM, EXP1, EXP2)
 
 
-def needed_positions(buf, base, off, lens, rec, chain):
+def needed_positions(buf, base, off, lens, rec, chain, flows=False):
     """Frame-relative positions the record walk reads, as a list of
     (positions, valid) arrays (absolute arena offsets)."""
     out = []
@@ -77,6 +77,13 @@ def needed_positions(buf, base, off, lens, rec, chain):
         pos = np.where(has, pos + ln, pos)
         nh = np.where(has, nxt, nh)
     add(l4 + 12, l4k == 1)
+    if flows:  # the 5-tuple the flow hash reads (addresses, then ports)
+        for k in range(12, 20):
+            add(l3 + k, v4)
+        for k in range(8, 40):
+            add(l3 + k, v6)
+        for k in range(4):
+            add(l4 + k, (l4k == 1) | (l4k == 2))
     return out
 
 
@@ -85,6 +92,8 @@ def main():
     ap.add_argument("--config", default="c4")
     ap.add_argument("--frames", type=int, default=1 << 21)
     ap.add_argument("--windows", default="2,3,5,8")
+    ap.add_argument("--flows", action="store_true",
+                    help="add the 5-tuple bytes (flow mode) and line-completing 4-5 chunk windows")
     args = ap.parse_args()
     import torch
 
@@ -116,7 +125,7 @@ def main():
         glob = len(np.unique(k & ((1 << 36) - 1))) / m
         return per_tile, glob
 
-    need = needed_positions(buf, base, off_h, len_h, recs, chain)
+    need = needed_positions(buf, base, off_h, len_h, recs, chain, args.flows)
     res = {"config": args.config, "frames": m, "arena_base_mod_4096": int(base),
            "ok_fraction": float((recs["status"] == 0).mean())}
     lt, lg = lines(need)
@@ -133,6 +142,19 @@ def main():
         res[f"needed_plus_window{w}"] = {"lines_per_frame_tile": round(lt, 4),
                                          "lines_per_frame_global": round(lg, 4),
                                          "read_bytes_per_frame": round(lt * 128 + 10, 2)}
+    # line-completing windows: from byte 12's chunk, at least m chunks, then
+    # to the end of that line, at most k (INGOT_TUNE_WINDOW_INDEXED 1000+10m+k)
+    for m_, k_ in ((2, 5), (4, 5)):
+        a0 = ((base + off_h + 12) & ~15) - base
+        lp = ((base + a0) >> 4) & 7
+        want = np.minimum(((lp + m_ + 7) & ~7) - lp, k_)
+        groups = list(need)
+        for c in range(k_):
+            cs = a0 + 16 * c
+            groups.append((cs, (c < want) & (cs < off_h + len_h)))
+        lt, lg = lines(groups)
+        res[f"needed_plus_linewin{m_}_{k_}"] = {"lines_per_frame_tile": round(lt, 4),
+                                              "read_bytes_per_frame": round(lt * 128 + 10, 2)}
     pmc = [ROOT / "profiles" / f"r02_pmc_{args.config}.json"]
     if pmc[-1].exists():
         p = json.loads(pmc[-1].read_text())
