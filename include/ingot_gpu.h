@@ -447,7 +447,9 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              payload, is never staged): 0 / 1 =
  *                              {4,0,0,0} (default), 2 = {2,2,2,0}, 3 =
  *                              {4,2,2,0}, 4 = {4,1,1,0}, 5 = {3,0,0,0},
- *                              6 = {2,0,0,0}; 9 = no descriptor
+ *                              6 = {2,0,0,0}; 7 / 8 = chunk 0 in a
+ *                              line-completing window of 2 / 4 to 8 pieces
+ *                              (to the end of its 128-B line); 9 = no descriptor
  *                              prefetch: chunk 0 staged, later chunks'
  *                              descriptors and bytes read on demand
  *   INGOT_TUNE_FLOW_KERNEL     ingot_gpu_flow_hist at the default windows:

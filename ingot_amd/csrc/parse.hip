@@ -1466,13 +1466,23 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
         // addresses; pieces only below the chunk's end)
         const uint32_t sh0 = (uint32_t)((uintptr_t)(a.arena + fr.o0) & 15u);
         const int64_t base0 = (int64_t)fr.o0 - (int64_t)sh0;
-        uint32_t ext = nseg ? sh0 + (fr.l0 < 16u * CS0 - sh0 ? fr.l0 : 16u * CS0 - sh0) : 0u;
+        // chunk 0's window: CS0 pieces, or (a.linewin = m) a line-completing
+        // window — at least m pieces, then to the end of that 128-B line
+        // (k_parse's windows), at most CS0
+        uint32_t want = CS0;
+        if (a.linewin) {
+            const uint32_t lp = (uint32_t)((uintptr_t)(a.arena + base0) >> 4) & 7u;
+            want = ((lp + a.linewin + 7u) & ~7u) - lp;
+            if (want > (uint32_t)CS0) want = CS0;
+        }
+        const uint32_t wlim = 16u * want;
+        uint32_t ext = nseg ? sh0 + (fr.l0 < wlim - sh0 ? fr.l0 : wlim - sh0) : 0u;
         // a later non-last chunk without planes that starts inside chunk 0's
         // window: stage the window's pieces up to its end (or the window's)
         auto widen = [&](uint32_t e, uint64_t o, uint32_t l) {
             const int64_t d = (int64_t)o - base0;
-            if (FR::cs(e) == 0 && e + 1 < nseg && d >= 0 && d < (int64_t)(16u * CS0)) {
-                const uint32_t end = (uint32_t)d + l < 16u * CS0 ? (uint32_t)d + l : 16u * CS0;
+            if (FR::cs(e) == 0 && e + 1 < nseg && d >= 0 && d < (int64_t)wlim) {
+                const uint32_t end = (uint32_t)d + l < wlim ? (uint32_t)d + l : wlim;
                 ext = end > ext ? end : ext;
             }
         };
@@ -1514,7 +1524,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
         fr.L = 0;
         fr.b0 = base0;
         fr.span0 = 16u * n0;
-        fr.enter(fr.o0, fr.l0, 0u, nseg ? CS0 : 0u);
+        fr.enter(fr.o0, fr.l0, 0u, nseg ? want : 0u);
         Rec r;
         if constexpr (MODE == OUT_FIELDS) {
             using OutT = typename std::conditional<TUN, ingot_geneve_fields, ingot_fields>::type;
@@ -2041,6 +2051,12 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
         case 4: return launch_read<4, 1, 1, 0, OUT_REC16>(a, chain, g, s);
         case 5: return launch_read<3, 0, 0, 0, OUT_REC16>(a, chain, g, s);
         case 6: return launch_read<2, 0, 0, 0, OUT_REC16>(a, chain, g, s);
+        case 7:  // line-completing chunk-0 windows of 2 / 4 to 8 pieces
+        case 8: {
+            ParseArgs b = a;
+            b.linewin = t.read_plan == 7 ? 2u : 4u;
+            return launch_read<8, 0, 0, 0, OUT_REC16>(b, chain, g, s);
+        }
         default: return launch_read<4, 0, 0, 0, OUT_REC16>(a, chain, g, s);
         }
     }
@@ -2313,7 +2329,7 @@ bool tuning_valid(int key, int value) {
     case INGOT_TUNE_SLOW_PATH:
         return value == 0 || value == 1;
     case INGOT_TUNE_READ_PLAN:
-        return (value >= 0 && value <= 6) || value == 9;
+        return (value >= 0 && value <= 9);
     case INGOT_TUNE_FLOW_KERNEL:
         return value >= 0 && value <= 2;
     default:
