@@ -444,12 +444,13 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *   INGOT_TUNE_READ_PLAN       ingot_gpu_parse_read (16-B records): 16-B
  *                              pieces staged in LDS for each of a packet's
  *                              first four chunks (a packet's last chunk, the
- *                              payload, is never staged): 0 / 1 =
- *                              {4,0,0,0} (default), 2 = {2,2,2,0}, 3 =
- *                              {4,2,2,0}, 4 = {4,1,1,0}, 5 = {3,0,0,0},
- *                              6 = {2,0,0,0}; 7 / 8 = chunk 0 in a
- *                              line-completing window of 2 / 4 to 8 pieces
- *                              (to the end of its 128-B line); 9 = no descriptor
+ *                              payload, is never staged): 0 / 11 = chunk 0
+ *                              in a line-completing window of 3 to 5 pieces
+ *                              (to the end of the 128-B line its third piece
+ *                              lies in; default), 1 = {4,0,0,0}, 2 =
+ *                              {2,2,2,0}, 3 = {4,2,2,0}, 4 = {4,1,1,0},
+ *                              5 = {3,0,0,0}, 6 = {2,0,0,0}, 7 / 8 / 10 =
+ *                              line-completing 2-8 / 4-8 / 2-5; 9 = no descriptor
  *                              prefetch: chunk 0 staged, later chunks'
  *                              descriptors and bytes read on demand
  *   INGOT_TUNE_FLOW_KERNEL     ingot_gpu_flow_hist at the default windows:

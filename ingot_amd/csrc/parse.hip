@@ -2037,15 +2037,19 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
         // reference's one-header-per-chunk shape (c2r, 1 M) 33.3 on demand
         // (9) / 25.1 {4,0,0,0} / 24.2 {2,2,2,0} / 27.0 {4,2,2,0}; header +
         // payload chunks (c3r, 16.7 M) 651 / 667 / 681 / 769 — extra planes
-        // cost occupancy on the gather-bound shape.  Default {4,0,0,0}: the
-        // descriptor prefetch (no dependent descriptor loads) at the legacy
-        // kernel's LDS footprint.
+        // cost occupancy on the gather-bound shape.  Default (round 2): chunk
+        // 0 in a line-completing window of 3 to 5 pieces (to the end of the
+        // 128-B line its third piece lies in; k_parse's windows, DESIGN.md
+        // §4): c3r 676 -> 651 us, c2r 23.05 -> 23.24; 3 to 8 pieces reads 15%
+        // fewer bytes but loses occupancy (724 us).  1 = the round-1 {4,0,0,0}.
         if (t.read_plan == 9) {
             return mode == OUT_FIELDS ? launch_chain<4, LAYOUT_SEGMENTED, OUT_FIELDS>(a, chain, g, s)
                                       : launch_chain<4, LAYOUT_SEGMENTED, OUT_REC16>(a, chain, g, s);
         }
         if (mode == OUT_FIELDS) return launch_read<4, 0, 0, 0, OUT_FIELDS>(a, chain, g, s);
-        switch (t.read_plan) {
+        // chunk pools in mapped host memory keep the round-1 window (every
+        // staged piece is a PCIe read there)
+        switch (t.read_plan ? t.read_plan : t.host_arena ? 1 : 11) {
         case 2: return launch_read<2, 2, 2, 0, OUT_REC16>(a, chain, g, s);
         case 3: return launch_read<4, 2, 2, 0, OUT_REC16>(a, chain, g, s);
         case 4: return launch_read<4, 1, 1, 0, OUT_REC16>(a, chain, g, s);
@@ -2057,7 +2061,17 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
             b.linewin = t.read_plan == 7 ? 2u : 4u;
             return launch_read<8, 0, 0, 0, OUT_REC16>(b, chain, g, s);
         }
-        default: return launch_read<4, 0, 0, 0, OUT_REC16>(a, chain, g, s);
+        case 10: {  // ... of 2 to 5 pieces (11, the default: 3 to 5)
+            ParseArgs b = a;
+            b.linewin = 2u;
+            return launch_read<5, 0, 0, 0, OUT_REC16>(b, chain, g, s);
+        }
+        case 1: return launch_read<4, 0, 0, 0, OUT_REC16>(a, chain, g, s);
+        default: {  // 11
+            ParseArgs b = a;
+            b.linewin = 3u;
+            return launch_read<5, 0, 0, 0, OUT_REC16>(b, chain, g, s);
+        }
         }
     }
     // Staged window (16-B chunks per frame); defaults measured on MI355X with
@@ -2329,7 +2343,7 @@ bool tuning_valid(int key, int value) {
     case INGOT_TUNE_SLOW_PATH:
         return value == 0 || value == 1;
     case INGOT_TUNE_READ_PLAN:
-        return (value >= 0 && value <= 9);
+        return (value >= 0 && value <= 11);
     case INGOT_TUNE_FLOW_KERNEL:
         return value >= 0 && value <= 2;
     default:

@@ -104,7 +104,7 @@ def main():
         d_so = torch.from_numpy(seg_off).cuda()
         d_sl = torch.from_numpy(seg_len.view(np.int16)).cuda()
         d_ps = torch.from_numpy(pkt_seg.view(np.int32)).cuda()
-        for plan in (0, 2, 3, 7, 8, 9):
+        for plan in (0, 1, 2, 3, 7, 8, 9, 10):
             c2 = ingot_amd.Context(0)
             c2.set_tuning(TUNE_READ_PLAN, plan)
             r, ch = c2.parse_read(arena, d_so, d_sl, d_ps, chain)
