@@ -22,11 +22,11 @@ DESC = {
     "c6": "C6 8.4 M Geneve-over-IPv6 (OPTE inbound)"}
 NOTES = {
     "c2": "ring kernel, 2 streams", "c2m": "whole 128-B lines read and rewritten (§1c)",
-    "c2r": "§1b (round 1: 31.5); dense table {dense}", "c3": "line-gather bound (§4)",
-    "c3p": "offsets scanned on the device (§1d)", "c3r": "§1b; dense table {dense}",
+    "c2r": "§1b (round 1: 31.5); dense table {dense}", "c3": "line-completing window; line-gather bound (§4)",
+    "c3p": "offsets scanned on the device (§1d)", "c3r": "§1b, chunk 0 line-completing (was 2.55×); dense table {dense}",
     "c3s": "3 streams", "c4": "",
     "c5": "frac: the flows kernel; step adds count + reduce (+ all-reduce at N>1)",
-    "c6": "8-chunk window"}
+    "c6": "6–9-chunk line-completing window"}
 
 
 def main():
