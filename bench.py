@@ -140,15 +140,74 @@ def host_inclusive_live(torch, ingot_amd, ctx, arena, off, lens, stride, chain, 
     return out
 
 
+def _read(path):
+    try:
+        return Path(path).read_text().strip()
+    except OSError:
+        return None
+
+
+def host_cpu_share():
+    """The CPUs this process may really use: its affinity mask, capped by the
+    tightest CPU quota of its cgroup or any ancestor (cgroup v2 `cpu.max`,
+    v1 `cpu.cfs_quota_us / cpu.cfs_period_us`).  os.cpu_count() on the GPU
+    box reports the whole machine; its share is a quota.  Returns (cpus to
+    pin one worker each to, description)."""
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else \
+        list(range(os.cpu_count() or 1))
+    quota, where = None, None
+    paths = {}
+    for line in (_read("/proc/self/cgroup") or "").splitlines():
+        hid, ctrls, path = line.split(":", 2)
+        if hid == "0":
+            paths["v2"] = path
+        elif "cpu" in ctrls.split(","):
+            paths["v1"] = path
+
+    def ancestors(root, path):
+        parts = [x for x in path.split("/") if x]
+        for k in range(len(parts), -1, -1):
+            yield Path(root, *parts[:k])
+
+    cands = []
+    if "v2" in paths:
+        for d in ancestors("/sys/fs/cgroup", paths["v2"]):
+            v = _read(d / "cpu.max")
+            if v and not v.startswith("max"):
+                q, per = v.split()
+                cands.append((int(q) / int(per), str(d / "cpu.max")))
+    for root in ("/sys/fs/cgroup/cpu", "/sys/fs/cgroup/cpu,cpuacct"):
+        for d in ancestors(root, paths.get("v1", "/")):
+            q, per = _read(d / "cpu.cfs_quota_us"), _read(d / "cpu.cfs_period_us")
+            if q and per and int(q) > 0:
+                cands.append((int(q) / int(per), str(d / "cpu.cfs_quota_us")))
+    if cands:
+        quota, where = min(cands)
+    n = len(aff) if quota is None else max(1, min(len(aff), int(quota)))
+    eff = None
+    if "v2" in paths:
+        eff = _read(Path("/sys/fs/cgroup", *[x for x in paths["v2"].split("/") if x],
+                         "cpuset.cpus.effective"))
+    return aff[:n], {"host_cpus": os.cpu_count(), "affinity_cpus": len(aff),
+                     "cpu_quota": None if quota is None else round(quota, 3),
+                     "cpu_quota_source": where, "cpuset_cpus_effective": eff,
+                     "effective_cpus": n}
+
+
 def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode="parse",
                  segs=None):
     """Time the oracle (the C restatement of ingot's parse) on the host's
-    cores over the same frames, bounded: all os.cpu_count() threads (the
-    figure reported) and 1 thread.  Each worker repeats its contiguous share
-    of the sample `passes` times per call, so thread start-up (one pthread
-    per CPU per call) is amortised; a share is then cache-resident after the
-    first pass — generous to the CPU.  mode "read": parse_read over `segs` =
-    (seg_off, seg_len, pkt_seg); "modify": parse + the same setter in place."""
+    cores over the same frames, bounded: one worker pinned to each CPU this
+    process may use (host_cpu_share: affinity mask capped by the cgroup CPU
+    quota — not os.cpu_count(), which on the GPU box counts the whole
+    machine), and 1 worker.  Each worker repeats its contiguous share of the
+    sample `passes` times per call, so thread start-up is amortised; a share
+    is then cache-resident after the first pass — generous to the CPU.  The
+    all-worker figure is the median of three sub-runs (spread reported).
+    mode "read": parse_read over `segs` = (seg_off, seg_len, pkt_seg);
+    "modify": parse + the same setter in place."""
+    import ctypes
+
     import oracle
     from ingot_amd import EditOp, Field
 
@@ -172,9 +231,11 @@ def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode
             oracle.parse_batch(arena_np, off_np, lens_np, chain, stride=stride, n=n,
                                nthreads=t, lib=lib)
 
-    host = os.cpu_count() or 1
-    res = {}
-    for t, budget in ((1, budget_s / 2), (host, budget_s)):
+    cpus, share = host_cpu_share()
+    pin = (ctypes.c_int * len(cpus))(*cpus)
+    lib.oracle_set_affinity(ctypes.cast(pin, ctypes.c_void_p), len(cpus))
+
+    def measure(t, budget):
         lib.oracle_set_passes(1)
         one_call(t)  # warm (page faults, thread stacks)
         t0 = time.perf_counter()
@@ -189,24 +250,30 @@ def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode
             el = time.perf_counter() - t0
             if el > budget:
                 break
-        res[t] = (calls * passes * n / el / 1e6, calls * passes, el)
-    lib.oracle_set_passes(1)
-    mp, reps, el = res[host]
-    what = {"parse": "parse_slice", "read": "parse_read", "modify": "parse + set_destination"}
+        return calls * passes * n / el / 1e6, calls * passes, el
+
     try:
-        affinity = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        affinity = host
+        single = measure(1, budget_s / 2)
+        runs = sorted((measure(len(cpus), budget_s / 3) for _ in range(3)), key=lambda r: r[0])
+    finally:
+        lib.oracle_set_passes(1)
+        lib.oracle_set_affinity(None, 0)
+    mp, reps, el = runs[1]
+    spread = (runs[2][0] - runs[0][0]) / mp if mp else 0.0
+    what = {"parse": "parse_slice", "read": "parse_read", "modify": "parse + set_destination"}
     return {
-        "value": round(mp, 3), "unit": "Mpkt/s", "cores": host, "kind": "port",
+        "value": round(mp, 3), "unit": "Mpkt/s", "cores": len(cpus), "kind": "port",
         "sample": f"{reps} passes x {n} frames of the benchmark batch (same bytes), "
-                  f"{el:.2f} s wall on {host} threads (every host CPU; each thread repeats "
-                  f"its share, cache-resident after the first pass); C restatement of ingot "
-                  f"{what.get(mode, mode)} (oracle/), -march={arch}",
-        "single_core_value": round(res[1][0], 3),
+                  f"{el:.2f} s wall on {len(cpus)} threads, each pinned to one of the CPUs "
+                  f"this process may use (affinity capped by the cgroup CPU quota); median of 3 "
+                  f"runs; each thread repeats its share, cache-resident after the first pass; "
+                  f"C restatement of ingot {what.get(mode, mode)} (oracle/), -march={arch}",
+        "single_core_value": round(single[0], 3),
+        "scaling_vs_single": round(mp / single[0], 2) if single[0] else None,
+        "run_spread": round(spread, 4),
+        "runs": [round(r[0], 3) for r in runs],
         "cpu_model": _cpu_model(),
-        "host_cpus": host,
-        "affinity_cpus": affinity,
+        **share,
     }
 
 
@@ -248,6 +315,60 @@ class Runner:
     def run(self, steps, gate=None):
         """Time `steps` launches (see _timed)."""
         return _timed(self.torch, self.streams, self.launch, steps, gate=gate)
+
+
+def ring_group(steps: int, cap: int = 64) -> int:
+    """Batches per ring launch: the largest divisor of `steps` up to `cap`
+    (INGOT_RING_MAX_BATCHES), so every launch of a run covers the same
+    number of batches and rocprofv3's per-dispatch mean of k_parse_ring is
+    the launch the line's roofline divides by (20 steps: one launch of 20)."""
+    steps = max(1, int(steps))
+    return max(d for d in range(1, min(cap, steps) + 1) if steps % d == 0)
+
+
+class RingRunner:
+    """The persistent ring consumer (ingot_gpu_parse_ring): steps k .. k+G-1
+    are one launch of G batches, batch k reading arena k % R and writing its
+    own record buffer k % len(outs) (every batch's records are stored inside
+    the region).  One stream; launches back to back."""
+
+    def __init__(self, torch, lib, ctx, chain, n, stride, arenas, outs, stream, record_bytes,
+                 group):
+        import ctypes
+
+        import ingot_amd
+
+        self.torch, self.streams, self.group = torch, [stream], group
+        reps, nout = len(arenas), len(outs)
+        h, c, sp = ctx._h, int(chain), stream.cuda_stream
+        aptrs = [a.data_ptr() for a in arenas]
+        optrs = [o.data_ptr() for o in outs]
+        tables = {}
+
+        def table(k, m):
+            key = (k % (reps * nout), m)
+            if key not in tables:
+                t = (ingot_amd.RingBatch * m)()
+                for j in range(m):
+                    t[j].d_arena, t[j].d_out = aptrs[(k + j) % reps], optrs[(k + j) % nout]
+                tables[key] = t
+            return tables[key]
+
+        def launch(k, m):
+            return lib.ingot_gpu_parse_ring(h, ctypes.cast(table(k, m), ctypes.c_void_p), m,
+                                            stride, n, c, record_bytes, None, 0, 0, None, sp)
+
+        self.launch = launch
+
+    def run(self, steps, gate=None):
+        """Time `steps` batches as launches of `group` batches."""
+        return _timed(self.torch, self.streams, self.launch, steps, gate=gate, group=self.group)
+
+    def warm(self, steps, gate=None):
+        """Untimed: `steps` rounded up to whole groups (every launch of the
+        run the same size)."""
+        g = self.group
+        return self.run(max(g, -(-steps // g) * g), gate)
 
 
 class PackedRunner:
@@ -368,6 +489,10 @@ class FlowRunner:
                                                 hist.numel(), flows[k % reps].data_ptr(), None,
                                                 hist.data_ptr(), self.work[k % S].data_ptr(),
                                                 wbytes, st.cuda_stream)
+                # never enqueue a collective behind an unrung doorbell
+                # (gate_policy "until_collective"): ring it first
+                if self._gate is not None:
+                    self._gate.open()
                 w = reduce_fn(hist)
             if w is not None:
                 works[k] = w
@@ -379,9 +504,14 @@ class FlowRunner:
                     works.pop(k).wait()
 
         self.launch, self.finish = launch, finish
+        self._gate = None
 
     def run(self, steps, gate=None):
-        return _timed(self.torch, self.streams, self.launch, steps, self.finish, gate=gate)
+        self._gate = gate
+        try:
+            return _timed(self.torch, self.streams, self.launch, steps, self.finish, gate=gate)
+        finally:
+            self._gate = None
 
 
 class Gate:
@@ -423,14 +553,15 @@ class Gate:
         self._timer.cancel()
 
 
-def _timed(torch, streams, launch, steps, finish=None, gate=None):
-    """Run `steps` launches; returns (ms, wall s).  Every stream stamps a
+def _timed(torch, streams, launch, steps, finish=None, gate=None, group=1):
+    """Run `steps` steps; returns (ms, wall s).  Every stream stamps a
     start event before its first launch and an end event after its last one;
     the region is the earliest start to the latest end (all on the device
     clock).  Ungated, the other streams fork from streams[0]'s start event;
     gated, every stream waits on the doorbell instead.  No stream joins
     another at the end: a cross-stream event wait costs ~7 us of device time
-    that would land inside the region (tools/region_probe.py)."""
+    that would land inside the region (tools/region_probe.py).  group > 1:
+    launch(k, m) runs steps k .. k+m-1 (the ring consumer)."""
     s0 = streams[0]
     w0 = time.perf_counter()
     if gate is not None:
@@ -448,11 +579,13 @@ def _timed(torch, streams, launch, steps, finish=None, gate=None):
                 e = torch.cuda.Event(enable_timing=True)
                 e.record(s)
                 starts.append(e)
-        for k in range(steps):
-            rc = launch(k)
+        held = 0
+        for k in range(0, steps, group):
+            rc = launch(k) if group == 1 else launch(k, min(group, steps - k))
             if rc:
                 raise RuntimeError(f"launch failed: {rc}")
-            if gate is not None and k + 1 == Gate.HOLD:
+            held += 1
+            if gate is not None and held == Gate.HOLD:
                 gate.open()
         if finish is not None:
             finish()
@@ -496,7 +629,9 @@ def pmc_for(config: str, family: str, sha: str, n: int):
     """The newest profiles/*_pmc_<config>.json taken on these kernel sources,
     over launches of n frames, whose profiled kernel is `family`; None
     otherwise."""
-    for f in sorted(ROOT.glob(f"profiles/*_pmc_{config}.json"), reverse=True):
+    files = list(ROOT.glob(f"profiles/*_pmc_{config}.json")) + \
+        list(ROOT.glob(f"profiles/*_pmc_{config}_ring.json"))
+    for f in sorted(files, key=lambda f: f.name, reverse=True):
         t = json.loads(f.read_text())
         k = t.get("kernel") or (t.get("kernels") or [""])[0]
         if t.get("sources_sha") != sha or t.get("frames_per_launch") != n:
@@ -623,6 +758,25 @@ def plan(args, world, rank):
         dist.destroy_process_group()
 
 
+def gate_policy(flows: bool, world: int, backend: str, no_gate: bool) -> str:
+    """How the timed region starts.
+      "off"   — from host submission: --no-gate, or the gloo rehearsal of
+                config 5 at N > 1, whose histogram reduce copies through the
+                host (a held stream would block it);
+      "until_collective" — config 5 over RCCL at N > 1: launches are held
+                behind the doorbell only up to the first collective of the
+                region; the runner rings it before issuing any all-reduce, so
+                no collective is ever enqueued while a stream of this process
+                waits on an unrung doorbell (a held stream would hold RCCL's
+                hardware queue too, include/ingot_gpu.h);
+      "hold"  — everything else: the first Gate.HOLD launches are held."""
+    if no_gate:
+        return "off"
+    if flows and world > 1:
+        return "off" if backend == "gloo" else "until_collective"
+    return "hold"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -635,10 +789,17 @@ def main():
     ap.add_argument("--streams", type=int, default=0,
                     help="streams the steps alternate over (0 = the config's measured best)")
     ap.add_argument("--record", type=int, default=16, choices=(16, 8))
+    ap.add_argument("--timing", default="auto", choices=("auto", "ring", "launches"),
+                    help="ring: the persistent ring consumer (ingot_gpu_parse_ring, one launch "
+                         "per group of up to 64 batches); launches: one launch per batch over "
+                         "the config's streams; auto: ring where the ring kernel serves the "
+                         "config (fixed slots, no length array: c2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the live host-inclusive (PCIe) measurement")
+    ap.add_argument("--no-sublines", action="store_true",
+                    help="c2: skip the C3 (mixed 64-1500 B) sub-line")
     ap.add_argument("--no-gate", action="store_true",
                     help="time from host submission (no doorbell-held first launches)")
     ap.add_argument("--stagger-us", type=float, default=None,
@@ -682,9 +843,6 @@ def main():
     import torch.distributed as dist
 
     import ingot_amd
-    from ingot_amd import Chain, GenProfile
-
-    from ingot_amd import dist as idist
 
     # one GPU per rank; a --dist-backend gloo rehearsal may fold ranks onto
     # fewer GPUs (e.g. the 1-GPU test box)
@@ -697,25 +855,56 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(args.dist_backend)
-
-    prof_name, _, stride, chain_name, desc = CONFIGS[args.config]
-    profile, chain = GenProfile[prof_name], Chain[chain_name]
     ctx = ingot_amd.Context(local)
     from ingot_amd import abi
 
     for kv in args.tune:
         k, v = kv.split("=")
         ctx.set_tuning(getattr(abi, f"TUNE_{k.upper()}"), int(v))
-    lib = ingot_amd.load_library()
-    mode = MODES.get(args.config, "parse")
+    env = (torch, dist, ingot_amd, ingot_amd.load_library(), ctx, world, rank, local, dev)
+    result = run_config(args, args.config, env)
+    # The metric names 64-1500 B frames: the default (c2) line carries the
+    # mixed-frame config (BASELINE.json configs[2]) as a sub-line of its own,
+    # timed by the same rules, with its own roofline and CPU baseline.
+    if args.config == "c2" and not args.no_sublines and not args.tune:
+        sub = argparse.Namespace(**vars(args))
+        sub.config, sub.streams, sub.record, sub.timing = "c3", STREAMS["c3"], 16, "auto"
+        sub.no_variants, sub.no_host_path = True, True
+        sub.stagger_us = None
+        r3 = run_config(sub, "c3", env)
+        if result is not None:
+            result["sublines"] = {"c3": r3}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run_config(args, config, env):
+    """One config's bench line (rank 0 returns the dict, other ranks None)."""
+    torch, dist, ingot_amd, lib, ctx, world, rank, local, dev = env
+    from ingot_amd import Chain, GenProfile
+    from ingot_amd import dist as idist
+
+    prof_name, _, stride, chain_name, desc = CONFIGS[config]
+    profile, chain = GenProfile[prof_name], Chain[chain_name]
+    mode = MODES.get(config, "parse")
     flows = mode == "flows"
+    no_variants = args.no_variants or flows
+    # the persistent ring consumer serves fixed slots without a length array
+    # (the ring kernel's layout), 16- or 8-B records, not the tunnel chain
+    ring_ok = (mode == "parse" and stride is not None and stride >= 64 and prof_name == "V4UDP64"
+               and chain != Chain.GeneveOverV6Tunnel)
+    use_ring = args.timing == "ring" or (args.timing == "auto" and ring_ok)
+    if use_ring and not ring_ok:
+        raise SystemExit(f"--timing ring: {config} is not a slot ring without lengths")
+    streams_n = 1 if use_ring else args.streams
 
     # --- data: this rank's share (pure in (seed, index)) + R copies ---
-    first, n, n_total = frames_for_rank(args.config, args.scaling, rank, world)
+    first, n, n_total = frames_for_rank(config, args.scaling, rank, world)
     arena, off, lens = ingot_amd.gen_frames(profile, n, first=first, stride=stride,
                                             device=local)
-    if flows:
-        args.no_variants = True
     # >= 512 MiB of distinct arenas (the 256 MiB MALL cannot serve a step from
     # the previous one), and a copy per stream in flight (launches running
     # together never read the same bytes) — up to ROTATE_CAP_BYTES; above it
@@ -723,13 +912,18 @@ def main():
     # only single-stream variants
     need = max(1, -(-(args.rotate_mib << 20) // arena.numel()))
     # (config 5's runner rotates its histograms with the arenas: >= 4)
-    reps = max(need, args.streams, 4 if flows or not args.no_variants else 1)
+    reps = max(need, streams_n, 4 if flows or not no_variants else 1)
     multi_stream_variants = True
     if arena.numel() * reps > ROTATE_CAP_BYTES:
-        reps = max(need, args.streams)
+        reps = max(need, streams_n)
         multi_stream_variants = False
     arenas = [arena] + [arena.clone() for _ in range(reps - 1)]
     outs = [torch.empty((n, 16), dtype=torch.uint8, device=dev) for _ in range(reps)]
+    G = ring_group(args.steps)
+    ring_outs = None
+    if use_ring:  # every batch of a ring launch writes its own record buffer
+        ring_outs = outs + [torch.empty((n, 16), dtype=torch.uint8, device=dev)
+                            for _ in range(max(0, G - reps))]
     torch.cuda.synchronize(dev)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
                                                   for _ in range(max(3, args.streams - 1))]
@@ -737,6 +931,10 @@ def main():
     if flows:
         hists = [torch.zeros(FLOW_BINS, dtype=torch.int32, device=dev) for _ in range(reps)]
         flow_ids = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(reps)]
+        if world > 1:  # communicators up before any gated region (eager, ungated)
+            idist.reduce_histogram(hists[0])
+            hists[0].zero_()
+            torch.cuda.synchronize(dev)
     recs0 = None
     if mode == "read":
         # mblk-style packets over the same frames (chunks inside each frame)
@@ -746,9 +944,12 @@ def main():
         rlens = lens if lens is not None else torch.full((n,), stride, dtype=torch.int32,
                                                          device=dev).to(torch.uint16)
         seg_off, seg_len, pkt_seg, head_chunks = read_chunks(
-            torch, off, stride, rlens.to(torch.int32), recs0, READ_CHUNKS[args.config], dev)
+            torch, off, stride, rlens.to(torch.int32), recs0, READ_CHUNKS[config], dev)
 
-    def runner(nstreams, record, flows_only=False, dense=False):
+    def runner(nstreams, record, flows_only=False, dense=False, ring=False, group=G):
+        if ring:
+            return RingRunner(torch, lib, ctx, chain, n, stride, arenas,
+                              ring_outs if record == 16 else outs8, streams[0], record, group)
         if flows:
             return FlowRunner(torch, lib, ctx, chain, n, arenas, off, lens, hists, flow_ids,
                               streams[:nstreams], idist.reduce_histogram_async, flows_only)
@@ -765,27 +966,41 @@ def main():
                       streams[:nstreams], record)
 
     if mode in ("modify", "read", "packed") and args.record == 8:
-        ap.error("8-B records are not offered for this config")
+        raise SystemExit("8-B records are not offered for this config")
     if chain == Chain.GeneveOverV6Tunnel and args.record == 8:
-        ap.error("8-B records are not offered for the tunnel chain (include/ingot_gpu.h)")
-    # the doorbell gate needs every launch of the region to be asynchronous:
-    # the gloo rehearsal's histogram reduce copies through the host
+        raise SystemExit("8-B records are not offered for the tunnel chain (include/ingot_gpu.h)")
+    outs8 = None
+    if use_ring and args.record == 8:
+        outs8 = [torch.empty((n, 8), dtype=torch.uint8, device=dev) for _ in range(max(G, reps))]
+    policy = gate_policy(flows, world, args.dist_backend, args.no_gate)
     gate = None
-    gate_note = "off (--no-gate)"
-    if not args.no_gate and not (flows and world > 1 and args.dist_backend == "gloo"):
+    gate_note = {"off": "off (--no-gate)" if args.no_gate else
+                 "off (gloo rehearsal: the histogram reduce copies through the host)"}.get(policy)
+    if policy != "off":
         try:
             stagger = (args.stagger_us if args.stagger_us is not None
-                       else STAGGER_US.get(args.config, 0.0))
+                       else STAGGER_US.get(config, 0.0))
             gate = Gate(ingot_amd, ctx, stagger)
             gate_note = (f"first {Gate.HOLD} launches held behind a doorbell "
                          "(ingot_gpu_doorbell_wait); region from the first step's start")
-            if stagger and args.streams > 1:
+            if policy == "until_collective":
+                gate_note = ("launches held behind a doorbell until the first RCCL collective "
+                             "of the region, which is issued only after the ring")
+            if stagger and streams_n > 1:
                 gate_note += (f"; stream i starts i x {stagger:g} us behind stream 0 "
                               "(ingot_gpu_stream_delay), inside the region")
         except RuntimeError as e:
             gate_note = f"unavailable ({e}); region from host submission"
-    main_run = runner(args.streams, args.record)
-    main_run.run(args.warmup, gate)
+    if use_ring:
+        gate_note = (f"persistent ring consumer: ingot_gpu_parse_ring, {args.steps // G} "
+                     f"launch(es) of {G} batches on one stream (k_parse_ring; every batch reads "
+                     f"its own 1 M-frame arena copy and writes its own 1 M records inside the "
+                     f"region); " + (gate_note or ""))
+    main_run = runner(streams_n, args.record, ring=use_ring)
+    if use_ring:
+        main_run.warm(args.warmup, gate)
+    else:
+        main_run.run(args.warmup, gate)
 
     # --- timed region: K steps, barrier + sync on both sides ---
     if world > 1:
@@ -833,29 +1048,40 @@ def main():
         step_rd, step_wr = rd + 4 * n, 4 * n + FLOW_BINS * 4
     if mode == "modify":  # no records; the 2 rewritten bytes per packet
         wr = step_wr = 2 * n
-    bytes_launch = rd + wr
     pipelined_gbs = (step_rd + step_wr) / (ms_step / 1e3) / 1e9
-    # Roofline of the kernel itself: a single-stream pass (launches back to
-    # back, so region/K = one launch incl. the dependent-launch boundary; this
-    # is what rocprofv3's per-dispatch mean measures).  In the pipelined
-    # schedule two launches overlap, so per-dispatch durations are not per-step.
-    # Its own floor of warm-up and launches, so that a short run (--steps 1
-    # --warmup 0) does not report a cold single launch as the kernel's rate.
-    iso = runner(1, args.record, flows_only=True)
-    iso.run(max(10, min(args.warmup, 50)))
-    iso_steps = max(20, min(args.steps, 1000))
-    ms_iso, _ = iso.run(iso_steps, gate)
-    launch_ms = ms_iso / iso_steps
+    # Roofline of the dominant kernel: launches back to back on one stream,
+    # region / launches = one launch's duration, what rocprofv3's
+    # per-dispatch mean of that kernel measures.  Per-batch launches: a
+    # single-stream pass (in the pipelined schedule two launches overlap, so
+    # per-dispatch durations are not per-step).  The ring: launches of the
+    # same G batches as the timed region's.  Its own floor of warm-up and
+    # launches, so that a short run (--steps 1 --warmup 0) does not report a
+    # cold single launch as the kernel's rate.
+    if use_ring:
+        iso = main_run
+        iso_launches = max(4, min(50, 1000 // G))
+        iso.warm(G)
+        ms_iso, _ = iso.run(iso_launches * G, gate)
+        launch_ms = ms_iso / iso_launches
+        per_launch = G
+    else:
+        iso = runner(1, args.record, flows_only=True)
+        iso.run(max(10, min(args.warmup, 50)))
+        iso_steps = max(20, min(args.steps, 1000))
+        ms_iso, _ = iso.run(iso_steps, gate)
+        launch_ms = ms_iso / iso_steps
+        per_launch = 1
+    bytes_launch = (rd + wr) * per_launch
     achieved = bytes_launch / (launch_ms / 1e3) / 1e9
     ok_frac = float((recs_np["status"] == 0).mean())
     # the multi-tile ring kernels serve slot rings without a length array
     # (launch_parse / launch_modify in parse.hip); everything else is k_parse
-    ring = (mode in ("parse", "modify") and stride is not None and stride >= 64
-            and lens is None and chain != Chain.GeneveOverV6Tunnel)
-    family = kernel_family(mode, ring)
+    ring_k = (mode in ("parse", "modify") and stride is not None and stride >= 64
+              and lens is None and chain != Chain.GeneveOverV6Tunnel)
+    family = "k_parse_ring" if use_ring else kernel_family(mode, ring_k)
     sha = kernel_sources_sha()
     traffic = None
-    t, pf = (pmc_for(args.config, family, sha, n) if args.record == 16 and not args.tune
+    t, pf = (pmc_for(config, family, sha, n * per_launch) if args.record == 16 and not args.tune
              else (None, None))
     if t is not None:
         traffic = {"bytes_per_launch": t["traffic_bytes_per_launch"],
@@ -866,23 +1092,36 @@ def main():
 
     # --- variants (outside the timed region; same data) ---
     variants = {}
-    if not args.no_variants:
+    if not no_variants:
         vsteps = min(args.steps, 1000)
-        for ns, rb in ((1, 16), (2, 8), (1, 8), (4, 16)):
-            if (ns, rb) == (args.streams, args.record):
+        combos = [(1, 16), (2, 8), (1, 8), (4, 16)]
+        if use_ring:  # the per-batch launches the ring replaces, and 8-B ring records
+            combos = [(2, 16), (1, 16), (2, 8), ("ring", 8)]
+        for ns, rb in combos:
+            if not use_ring and (ns, rb) == (args.streams, args.record):
                 continue
-            if ns > 1 and not multi_stream_variants:
+            if ns != "ring" and ns > 1 and not multi_stream_variants:
                 continue
             if rb == 8 and (chain == Chain.GeneveOverV6Tunnel or mode != "parse"):
                 continue
-            r = runner(ns, rb)
-            r.run(min(args.warmup, 50))
+            if ns == "ring":
+                if outs8 is None:
+                    outs8 = [torch.empty((n, 8), dtype=torch.uint8, device=dev)
+                             for _ in range(max(G, reps))]
+                r = runner(1, rb, ring=True)
+                r.warm(min(args.warmup, 50), gate)
+                name = f"ring_rec{rb}"
+            else:
+                r = runner(ns, rb)
+                r.run(min(args.warmup, 50), gate if ns > 1 else None)
+                name = f"{'launches_' if use_ring else ''}streams{ns}_rec{rb}"
             ms, _ = r.run(vsteps, gate)
             bpl = rd + (rb * n if mode != "modify" else wr)
-            variants[f"streams{ns}_rec{rb}"] = {
+            variants[name] = {
                 "value": round(n * vsteps / (ms / 1e3) / 1e6, 2),
                 "us_per_step": round(ms * 1e3 / vsteps, 3),
                 "hbm_GBps": round(bpl / (ms / vsteps / 1e3) / 1e9, 1),
+                "read_frac": round(rd / (ms / vsteps / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             }
         if mode == "read":  # the same chunks as one dense 8-B entry each
             r = runner(args.streams, 16, dense=True)
@@ -892,100 +1131,120 @@ def main():
                 "value": round(n * vsteps / (ms / 1e3) / 1e6, 2),
                 "us_per_step": round(ms * 1e3 / vsteps, 3)}
 
+    if flows and not args.tune:
+        # the plain parse (16-B records) of the same frames, one stream, as
+        # the flows kernel's roofline pass: the cost of the hash and the flow
+        # window, from one run (k_parse beside k_parse<..., OUT_FLOWS16> in a
+        # rocprofv3 trace of this command)
+        r = Runner(torch, lib, ctx, chain, n, stride, arenas, off, lens, outs, streams[:1], 16)
+        r.run(max(10, min(args.warmup, 50)))
+        vsteps = max(20, min(args.steps, 1000))
+        ms, _ = r.run(vsteps, gate if policy == "hold" else None)
+        us = ms * 1e3 / vsteps
+        variants["plain_parse_streams1_rec16"] = {
+            "us_per_launch": round(us, 3),
+            "flows_kernel_us_per_launch": round(launch_ms * 1e3, 3),
+            "flows_over_plain": round(launch_ms * 1e3 / us, 4),
+            "frac": round((rd + 16 * n) / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+        }
+
     host_path = None
     if (world == 1 and mode == "parse" and args.record == 16 and not args.no_host_path
             and not args.tune):
         host_path = host_inclusive_live(torch, ingot_amd, ctx, arenas[0], off, lens, stride,
                                         chain, n)
 
-    if rank == 0:
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            m = min(n, 1 << 20)  # bounded sample: the first 1M frames of the batch
-            if off is not None:
-                o_np = off[:m].cpu().numpy()
-                end = int(o_np[-1]) + int(lens_np[m - 1])
-                a_np = arenas[0][:end + 64].cpu().numpy()
-            else:
-                o_np, a_np = None, arenas[0][:m * stride].cpu().numpy()
-            l_np = lens_np[:m] if lens_np is not None else None
-            segs = None
-            if mode == "read":
-                ps = pkt_seg[:m + 1].cpu().numpy().view(np.uint32)
-                ns_ = int(ps[-1])
-                segs = (seg_off[:ns_].cpu().numpy().view(np.uint64),
-                        seg_len[:ns_].to(torch.int32).cpu().numpy().astype(np.uint16), ps)
-            cpu = cpu_baseline(a_np, o_np, l_np, stride or 0, m, chain, args.cpu_budget,
-                               mode="parse" if flows else mode, segs=segs)
-        kname = {"modify": ", parse + setters",
-                 "read": ", LAYOUT_SEGMENTED (parse_read)",
-                 "packed": ", LAYOUT_PACKED + k_tile_sums/k_group_scan",
-                 "flows": ", OUT_FLOWS16 (parse + Toeplitz hash; the step adds "
-                          "k_flow_count16 / k_flow_reduce16)"}.get(mode, "")
-        result = {
-            "metric": METRIC,
-            "value": round(value, 2),
-            "unit": "Mpkt/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_step, 5),
-            "higher_is_better": True,
-            "scaling": args.scaling,
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic (device-generated, seed 20250808)",
-            "config": {
-                "workload": desc,
-                "frames_per_gpu": n,
-                "frames_total": n_total,
-                "chain": chain_name,
-                "layout": f"strided {stride} B" if stride else "packed, u64 offsets + u16 lengths",
-                "record_bytes": args.record,
-                "streams": args.streams,
-                "arena_copies_rotated": reps,
-                "parallelism": (f"{args.scaling} scaling, contiguous share per GPU x{world}" +
-                                (f"; {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} "
-                                 f"all-reduce (sum) of the {FLOW_BINS} x u32 flow "
-                                 "histogram every step" if flows else
-                                 " (no data-path collective)")),
-                "ok_fraction": round(ok_frac, 6),
-                "timing": gate_note,
-            },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic["bytes_per_launch"] if traffic else None,
-                "traffic_detail": traffic,
-                "kernel": (traffic or {}).get("kernel") or
-                          f"{family} (ingot_amd/csrc/parse.hip){kname}",
-                "kernel_sources_sha": sha,
-                "launch_mean_us": round(launch_ms * 1e3, 3),
-                "launch_timing": "single-stream pass, HIP events, region/K",
-                "pipelined_GBps": round(pipelined_gbs, 1),
-                "pipelined_frac": round(pipelined_gbs / HBM_PEAK_GBS, 4),
-                "pipelined_read_frac": round(step_rd / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                "algorithmic_bytes_per_launch": bytes_launch,
-                "read_bytes_per_launch": rd,
-                "write_bytes_per_launch": wr,
-                "read_frac": round(rd / (launch_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                "frac_of_measured_copy_ceiling": round(achieved / HBM_MEASURED_GBS, 4),
-                "read_frac_of_measured_copy_ceiling": round(
-                    rd / (launch_ms / 1e3) / 1e9 / HBM_MEASURED_GBS, 4),
-            },
-            "ms_per_step_ungated": ungated,
-            "variants": variants,
-            "cpu_baseline": cpu,
-            "wall_s_timed_region": round(wall, 4),
-            "host_inclusive": host_path,
-        }
-        print(json.dumps(result), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    if rank != 0:
+        return None
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        m = min(n, 1 << 20)  # bounded sample: the first 1M frames of the batch
+        if off is not None:
+            o_np = off[:m].cpu().numpy()
+            end = int(o_np[-1]) + int(lens_np[m - 1])
+            a_np = arenas[0][:end + 64].cpu().numpy()
+        else:
+            o_np, a_np = None, arenas[0][:m * stride].cpu().numpy()
+        l_np = lens_np[:m] if lens_np is not None else None
+        segs = None
+        if mode == "read":
+            ps = pkt_seg[:m + 1].cpu().numpy().view(np.uint32)
+            ns_ = int(ps[-1])
+            segs = (seg_off[:ns_].cpu().numpy().view(np.uint64),
+                    seg_len[:ns_].to(torch.int32).cpu().numpy().astype(np.uint16), ps)
+        cpu = cpu_baseline(a_np, o_np, l_np, stride or 0, m, chain, args.cpu_budget,
+                           mode="parse" if flows else mode, segs=segs)
+    kname = {"modify": ", parse + setters",
+             "read": ", LAYOUT_SEGMENTED (parse_read)",
+             "packed": ", LAYOUT_PACKED + k_tile_sums/k_group_scan",
+             "flows": ", OUT_FLOWS16 (parse + Toeplitz hash; the step adds "
+                      "k_flow_count16 / k_flow_reduce16)"}.get(mode, "")
+    read_frac_step = step_rd / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS
+    return {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "Mpkt/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 5),
+        "higher_is_better": True,
+        "scaling": args.scaling,
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (device-generated, seed 20250808)",
+        "config": {
+            "workload": desc,
+            "frames_per_gpu": n,
+            "frames_total": n_total,
+            "chain": chain_name,
+            "layout": f"strided {stride} B" if stride else "packed, u64 offsets + u16 lengths",
+            "record_bytes": args.record,
+            "streams": streams_n,
+            "arena_copies_rotated": reps,
+            "parallelism": (f"{args.scaling} scaling, contiguous share per GPU x{world}" +
+                            (f"; {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} "
+                             f"all-reduce (sum) of the {FLOW_BINS} x u32 flow "
+                             "histogram every step" if flows else
+                             " (no data-path collective)")),
+            "ok_fraction": round(ok_frac, 6),
+            "timing": gate_note,
+            "timing_mode": "ring" if use_ring else "launches",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic["bytes_per_launch"] if traffic else None,
+            "traffic_detail": traffic,
+            "kernel": (traffic or {}).get("kernel") or
+                      f"{family} (ingot_amd/csrc/parse.hip){kname}",
+            "kernel_sources_sha": sha,
+            "batches_per_launch": per_launch,
+            "launch_mean_us": round(launch_ms * 1e3, 3),
+            "launch_timing": ("ring launches of the region's batch count back to back, one "
+                              "stream, HIP events, region / launches" if use_ring else
+                              "single-stream pass, HIP events, region/K"),
+            "pipelined_GBps": round(pipelined_gbs, 1),
+            "pipelined_frac": round(pipelined_gbs / HBM_PEAK_GBS, 4),
+            "pipelined_read_frac": round(read_frac_step, 4),
+            "north_star_read_frac": round(read_frac_step, 4),
+            "north_star_read_frac_def": ("HBM-read roofline fraction of the timed region: "
+                                         "algorithmic read bytes per step / ms_per_step / 8 TB/s"),
+            "algorithmic_bytes_per_launch": bytes_launch,
+            "read_bytes_per_batch": rd,
+            "write_bytes_per_batch": wr,
+            "read_frac": round(rd * per_launch / (launch_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "frac_of_measured_copy_ceiling": round(achieved / HBM_MEASURED_GBS, 4),
+        },
+        "ms_per_step_ungated": ungated,
+        "variants": variants,
+        "cpu_baseline": cpu,
+        "wall_s_timed_region": round(wall, 4),
+        "host_inclusive": host_path,
+    }
 
 
 if __name__ == "__main__":

@@ -372,6 +372,17 @@ int ingot_gpu_host_unmap(ingot_gpu_ctx* ctx, void* host);
  *     doorbell is eventually rung: a stream left waiting never drains.
  *   ingot_gpu_doorbell_destroy: only after every wait on it has been passed.
  * ENODEV when the device cannot wait on memory values.
+ *
+ * A doorbell wait holds a whole HARDWARE queue, not just its stream: HIP
+ * maps streams round-robin onto GPU_MAX_HW_QUEUES hardware queues (4 by
+ * default), and the command processor stops at the wait packet, so every
+ * other stream mapped to that queue (a producer's copy stream, RCCL's
+ * stream, torch's current stream) stalls behind it until the ring.  A
+ * producer must therefore publish frames from the host, or from a stream
+ * known to sit on another hardware queue; publishing with GPU work that
+ * shares the held queue and ringing only after that work completes
+ * deadlocks (tests/test_doorbell.py::test_held_queue_blocks_its_streams).
+ * ingot_gpu_parse_ring's in-kernel doorbell has no such constraint.
  */
 typedef struct ingot_gpu_doorbell ingot_gpu_doorbell;
 int ingot_gpu_doorbell_create(ingot_gpu_ctx* ctx, ingot_gpu_doorbell** out,
@@ -379,6 +390,47 @@ int ingot_gpu_doorbell_create(ingot_gpu_ctx* ctx, ingot_gpu_doorbell** out,
 int ingot_gpu_doorbell_wait(ingot_gpu_doorbell* db, uint32_t value, void* stream);
 int ingot_gpu_doorbell_ring(ingot_gpu_doorbell* db, uint32_t value);
 void ingot_gpu_doorbell_destroy(ingot_gpu_doorbell* db);
+
+/*
+ * Persistent ring consumer.  One launch parses `nbatches` (<=
+ * INGOT_RING_MAX_BATCHES) batches of `n` frames in fixed slots of `stride`
+ * bytes (>= 64, a multiple of 16; no length array, like
+ * ingot_gpu_parse_strided with d_len NULL): batch b from batches[b].d_arena
+ * into batches[b].d_out (n ingot_rec when record_bytes is 16, n ingot_rec8
+ * when 8; not GENEVE_OVER_V6).  The records are exactly those of
+ * ingot_gpu_parse_strided over each batch.  Instead of one launch per batch
+ * (each paying a grid ramp-up and drain), every wave walks its share of all
+ * the batches' tiles in order, keeping the next tile's LDS-DMA in flight
+ * across batch boundaries.
+ *
+ *   db == NULL: every batch is resident when the launch starts.
+ *   db != NULL: a wave stages tiles of batch b only once the doorbell word
+ *     is >= db_first + b (the producer rings db_first + b after batch b's
+ *     frames are in memory; rings may cover several batches at once).  The
+ *     wave polls the word (one lane, with sleeps) only when it reaches a batch
+ *     not yet known published, then invalidates its caches (system-scope
+ *     acquire), so frames written by the host, a copy engine or another
+ *     kernel after the launch started are seen.  A wave that waits more than
+ *     `timeout_ms` (1..60000) for a batch stops: the batches from there on
+ *     keep whatever their record buffers held, and *d_status (optional,
+ *     device memory, caller-zeroed) gets bit 0 set.  Every launch therefore
+ *     ends, rung or not.
+ * The arenas are read-only for the launch; a batch buffer must not be
+ * rewritten while the launch may still read it (a ring reuses a slot only
+ * after the launch that consumes it has completed).  Unlike a
+ * doorbell_wait, the polling kernel holds no hardware queue: other streams
+ * (a producer's copies included) keep running beside it.
+ */
+#define INGOT_RING_MAX_BATCHES 64
+typedef struct ingot_ring_batch {
+    const uint8_t* d_arena; /* n slots of `stride` bytes, 16-B aligned */
+    void* d_out;            /* n records */
+} ingot_ring_batch;
+int ingot_gpu_parse_ring(ingot_gpu_ctx* ctx, const ingot_ring_batch* batches,
+                         uint32_t nbatches, uint32_t stride, uint64_t n, int chain,
+                         uint32_t record_bytes, const ingot_gpu_doorbell* db,
+                         uint32_t db_first, uint32_t timeout_ms, uint32_t* d_status,
+                         void* stream);
 
 /*
  * Staggered streams.  A consumer that alternates its batches over two (or
@@ -452,7 +504,10 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              5 = {3,0,0,0}, 6 = {2,0,0,0}, 7 / 8 / 10 =
  *                              line-completing 2-8 / 4-8 / 2-5; 9 = no descriptor
  *                              prefetch: chunk 0 staged, later chunks'
- *                              descriptors and bytes read on demand
+ *                              descriptors and bytes read on demand.  Chunk
+ *                              pools in mapped host memory (ingot_gpu_host_map)
+ *                              default to 1, and ingot_gpu_parse_read_dense
+ *                              always stages {4,0,0,0} (the knob is ignored)
  *   INGOT_TUNE_FLOW_KERNEL     ingot_gpu_flow_hist at the default windows:
  *                              0 = stage, walk, hash, store per tile
  *                              (default: one tile per wave with the 16-bit
@@ -460,6 +515,10 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              1 = the next tile's staging issued before the
  *                              hash of this one (persistent); 2 = the default
  *                              kernel on a persistent grid
+ *   INGOT_TUNE_RING_GRID       ingot_gpu_parse_ring: 256-thread blocks per
+ *                              CU (1..8; 0 = measured default).  The ring's
+ *                              tiles in flight per wave follow
+ *                              INGOT_TUNE_PIPE_DEPTH
  */
 #define INGOT_TUNE_WINDOW_INDEXED 1
 #define INGOT_TUNE_WINDOW_STRIDED 2
@@ -472,6 +531,7 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
 #define INGOT_TUNE_SLOW_PATH 9
 #define INGOT_TUNE_READ_PLAN 10
 #define INGOT_TUNE_FLOW_KERNEL 11
+#define INGOT_TUNE_RING_GRID 12
 int ingot_gpu_ctx_set_tuning(ingot_gpu_ctx* ctx, int key, int value);
 int ingot_gpu_ctx_get_tuning(const ingot_gpu_ctx* ctx, int key);
 
@@ -578,6 +638,8 @@ int ingot_gpu_geneve_fields_read(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
  * u16 arrays — one load per chunk descriptor and no padding between them.
  * fields = 0: d_out holds ingot_rec records; 1: ingot_fields blocks (EINVAL
  * for GENEVE_OVER_V6); 2: ingot_geneve_fields blocks (GENEVE_OVER_V6 only).
+ * Staging: chunk 0 in a fixed 4-piece (64-B) window, whatever
+ * INGOT_TUNE_READ_PLAN says.
  */
 int ingot_gpu_parse_read_dense(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
                                const uint64_t* d_seg, const uint32_t* d_pkt_seg,

@@ -209,9 +209,13 @@ class Context:
 
     def _arg(self, name: str, t, dtypes, numel: Optional[int] = None,
              optional: bool = False) -> None:
-        """Validate one buffer before its raw pointer crosses the C ABI: the
-        kernels trust dtype (element size), contiguity and extent, so a
-        mismatch here would be an out-of-bounds access on the device."""
+        """Validate one buffer before its raw pointer crosses the C ABI:
+        dtype (element size), contiguity and element count.  Only the
+        buffers' shapes are checked here, not their contents: descriptor
+        values (off[i] + lens[i] inside the arena, pkt_seg non-decreasing and
+        inside the chunk table) are the caller's contract, as in the C ABI
+        (include/ingot_gpu.h), and a bad descriptor is an out-of-bounds
+        device read.  check_descriptors() verifies those values on demand."""
         if t is None:
             if optional:
                 return
@@ -308,6 +312,32 @@ class Context:
             self._h, _ptr(arena), int(stride), _ptr(lens), n, int(chain), _ptr(out),
             _stream(stream, self.device)), "ingot_gpu_parse_strided_compact")
         return out
+
+    def parse_ring(self, arenas, stride: int, n: int, chain: Chain, outs, record_bytes: int = 16,
+                   doorbell: "Optional[Doorbell]" = None, db_first: int = 0,
+                   timeout_ms: int = 10000, status=None, stream=None) -> None:
+        """ingot_gpu_parse_ring: one persistent launch parses len(arenas)
+        batches of n slots (batch b: arenas[b] -> outs[b], (n, record_bytes)
+        uint8).  doorbell=None: every batch is resident; else batch b starts
+        once the doorbell reaches db_first + b (a wave gives up after
+        timeout_ms and sets bit 0 of `status`, a zeroed int32 cuda tensor)."""
+        nb = len(arenas)
+        if len(outs) != nb:
+            raise ValueError("one record buffer per batch")
+        if nb > RING_MAX_BATCHES:
+            raise ValueError(f"at most {RING_MAX_BATCHES} batches per launch")
+        batches = (RingBatch * max(1, nb))()
+        for b, (a, o) in enumerate(zip(arenas, outs)):
+            self._frames(a, None, None, stride, n)
+            self._arg("out", o, _U8, n * record_bytes)
+            self._on_device(arena=a, out=o)
+            batches[b].d_arena, batches[b].d_out = _ptr(a), _ptr(o)
+        self._arg("status", status, _U32, 1, optional=True)
+        self._on_device(status=status)
+        _lib.check(self._lib.ingot_gpu_parse_ring(
+            self._h, ctypes.cast(batches, ctypes.c_void_p), nb, int(stride), int(n), int(chain),
+            int(record_bytes), doorbell._h if doorbell is not None else None, int(db_first),
+            int(timeout_ms), _ptr(status), _stream(stream, self.device)), "ingot_gpu_parse_ring")
 
     def fields(self, arena, off, lens, chain: Chain, stride: int = 0, n: Optional[int] = None,
                out=None, stream=None):
@@ -470,6 +500,48 @@ class Context:
         if not b:
             return None
         return _torch().empty(b, dtype=_torch().uint8, device=f"cuda:{self.device}")
+
+
+def check_descriptors(arena, off=None, lens=None, seg_off=None, seg_len=None, pkt_seg=None,
+                      seg=None) -> None:
+    """Check descriptor VALUES against the arena before a call (the calls
+    check only shapes and dtypes): every frame (off[i], lens[i]) and every
+    chunk (seg_off[k], seg_len[k]) — or dense entry seg[k] = offset << 16 |
+    length — lies inside the arena, and pkt_seg is non-decreasing from 0 and
+    ends inside the chunk table.  Raises ValueError; one reduction per array,
+    on the arrays' own device."""
+    size = int(arena.numel())
+
+    def inside(o, ln, what):
+        if o is None or o.numel() == 0:
+            return
+        end = o.to(_torch().int64) + ln.to(_torch().int64) if ln is not None else o
+        if int(o.min()) < 0 or int(end.max()) > size:
+            raise ValueError(f"{what} reach past the {size}-B arena")
+
+    if off is not None:
+        inside(off, lens.to(_torch().int32) & 0xFFFF, "frames (off + lens)")
+    if seg_off is not None:
+        inside(seg_off, seg_len.to(_torch().int32) & 0xFFFF, "chunks (seg_off + seg_len)")
+    nseg = seg_off.numel() if seg_off is not None else (seg.numel() if seg is not None else None)
+    if seg is not None:
+        inside(seg >> 16, seg & 0xFFFF, "dense chunks")
+    if pkt_seg is not None:
+        ps = pkt_seg.to(_torch().int64) & 0xFFFFFFFF
+        if ps.numel() == 0 or int(ps[0]) != 0:
+            raise ValueError("pkt_seg must start at 0")
+        if ps.numel() > 1 and bool((ps[1:] < ps[:-1]).any()):
+            raise ValueError("pkt_seg must be non-decreasing")
+        if nseg is not None and int(ps[-1]) > nseg:
+            raise ValueError(f"pkt_seg ends at {int(ps[-1])}, past the {nseg}-chunk table")
+
+
+RING_MAX_BATCHES = 64  # INGOT_RING_MAX_BATCHES
+
+
+class RingBatch(ctypes.Structure):
+    """ingot_ring_batch"""
+    _fields_ = [("d_arena", ctypes.c_void_p), ("d_out", ctypes.c_void_p)]
 
 
 class Doorbell:

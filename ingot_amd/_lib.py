@@ -53,6 +53,12 @@ SIGNATURES = {
         [ctypes.c_void_p, c_u8p, ctypes.c_uint32, c_u8p, c_u64, ctypes.c_int, c_u8p,
          ctypes.c_void_p],
     ),
+    "ingot_gpu_parse_ring": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, c_u64, ctypes.c_int,
+         ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, c_u8p,
+         ctypes.c_void_p],
+    ),
     "ingot_gpu_parse_compact": (
         ctypes.c_int,
         [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, c_u64, ctypes.c_int, c_u8p, ctypes.c_void_p],

@@ -81,6 +81,7 @@ TUNE_FLOW_TABLE = 8
 TUNE_SLOW_PATH = 9
 TUNE_READ_PLAN = 10
 TUNE_FLOW_KERNEL = 11
+TUNE_RING_GRID = 12
 
 
 class IngotRec(ctypes.Structure):

@@ -259,6 +259,7 @@ int ingot_gpu_host_unmap(ingot_gpu_ctx* ctx, void* host) {
 struct ingot_gpu_doorbell {
     int device;
     uint32_t* word;
+    uint32_t* dword = nullptr;  // the word's device address (ingot_gpu_parse_ring polls it)
 };
 
 int ingot_gpu_doorbell_create(ingot_gpu_ctx* ctx, ingot_gpu_doorbell** out,
@@ -275,7 +276,13 @@ int ingot_gpu_doorbell_create(ingot_gpu_ctx* ctx, ingot_gpu_doorbell** out,
     void* p = nullptr;
     if (hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
         return INGOT_GPU_EHIP;
-    ingot_gpu_doorbell* d = new (std::nothrow) ingot_gpu_doorbell{ctx->device, (uint32_t*)p};
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess) {
+        (void)hipHostFree(p);
+        return INGOT_GPU_EHIP;
+    }
+    ingot_gpu_doorbell* d =
+        new (std::nothrow) ingot_gpu_doorbell{ctx->device, (uint32_t*)p, (uint32_t*)dp};
     if (!d) {
         (void)hipHostFree(p);
         return INGOT_GPU_ENOMEM;
@@ -326,6 +333,7 @@ int ingot_gpu_ctx_set_tuning(ingot_gpu_ctx* ctx, int key, int value) {
     case INGOT_TUNE_SLOW_PATH: ctx->tuning.slow_path = value; break;
     case INGOT_TUNE_READ_PLAN: ctx->tuning.read_plan = value; break;
     case INGOT_TUNE_FLOW_KERNEL: ctx->tuning.flow_kernel = value; break;
+    case INGOT_TUNE_RING_GRID: ctx->tuning.ring_grid = value; break;
     default: ctx->tuning.max_blocks = (uint32_t)value; break;
     }
     return INGOT_GPU_SUCCESS;
@@ -345,6 +353,7 @@ int ingot_gpu_ctx_get_tuning(const ingot_gpu_ctx* ctx, int key) {
     case INGOT_TUNE_SLOW_PATH: return ctx->tuning.slow_path;
     case INGOT_TUNE_READ_PLAN: return ctx->tuning.read_plan;
     case INGOT_TUNE_FLOW_KERNEL: return ctx->tuning.flow_kernel;
+    case INGOT_TUNE_RING_GRID: return ctx->tuning.ring_grid;
     default: return INGOT_GPU_EINVAL;
     }
 }
@@ -361,6 +370,44 @@ int ingot_gpu_parse_strided(ingot_gpu_ctx* ctx, const uint8_t* d_arena, uint32_t
                             void* stream) {
     return parse_strided(ctx, d_arena, stride, d_len, n, chain, d_out, ingot_gpu::OUT_REC16,
                          stream);
+}
+
+int ingot_gpu_parse_ring(ingot_gpu_ctx* ctx, const ingot_ring_batch* batches, uint32_t nbatches,
+                         uint32_t stride, uint64_t n, int chain, uint32_t record_bytes,
+                         const ingot_gpu_doorbell* db, uint32_t db_first, uint32_t timeout_ms,
+                         uint32_t* d_status, void* stream) {
+    if (!ctx || !chain_ok(chain) || chain == INGOT_CHAIN_GENEVE_OVER_V6) return INGOT_GPU_EINVAL;
+    if (record_bytes != 16 && record_bytes != 8) return INGOT_GPU_EINVAL;
+    if (nbatches > INGOT_RING_MAX_BATCHES) return INGOT_GPU_ERANGE;
+    if (stride < 64u || stride % 16u != 0 || stride > 65535u) return INGOT_GPU_ERANGE;
+    if (db && (timeout_ms == 0 || timeout_ms > 60000u)) return INGOT_GPU_ERANGE;
+    if (nbatches == 0 || n == 0) return INGOT_GPU_SUCCESS;
+    if (!batches) return INGOT_GPU_EINVAL;
+    // the kernel's tile cursors are 32-bit
+    const uint64_t tiles = (n + 63u) / 64u;
+    if (tiles * nbatches >= (1ull << 31)) return INGOT_GPU_ERANGE;
+    ingot_gpu::RingArgs a{};
+    for (uint32_t b = 0; b < nbatches; ++b) {
+        const ingot_ring_batch& x = batches[b];
+        if (!x.d_arena || !x.d_out || ((uintptr_t)x.d_arena & 15u)) return INGOT_GPU_EINVAL;
+        a.b[b] = ingot_gpu::RingBatch{x.d_arena, x.d_out};
+    }
+    if (db && !ctx->wall_khz) return INGOT_GPU_ENODEV;
+    if (int e = enter(ctx)) return e;
+    a.n = n;
+    a.stride = stride;
+    a.nbatches = nbatches;
+    a.tiles_per_batch = (uint32_t)tiles;
+    a.published = db ? 0u : nbatches;
+    a.doorbell = db ? db->dword : nullptr;
+    a.db_first = db_first;
+    a.timeout_ticks = (uint64_t)timeout_ms * ctx->wall_khz;
+    a.status = d_status;
+    return from_hip(ingot_gpu::launch_ring(a, chain,
+                                           record_bytes == 8 ? ingot_gpu::OUT_REC8
+                                                             : ingot_gpu::OUT_REC16,
+                                           tuning_for(ctx, batches[0].d_arena),
+                                           (hipStream_t)stream));
 }
 
 int ingot_gpu_parse_compact(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,

@@ -76,6 +76,34 @@ struct ModifyArgs {
     uint32_t n_edits;
     Edit e[INGOT_MAX_EDITS];
 };
+// 3,824 B today (ParseArgs + key windows + the 16-bit table): the kernarg
+// segment is 4 KiB, and a larger FlowArgs would fail flow launches at run
+// time, not here.
+static_assert(sizeof(FlowArgs) <= 4096, "FlowArgs exceeds the 4 KiB kernel-argument limit");
+
+// Persistent ring consumer (ingot_gpu_parse_ring): one launch parses up to
+// INGOT_RING_MAX_BATCHES batches of n fixed slots, batch b from b.arena into
+// b.out; tiles of batch b are staged only once b is published (b < published,
+// or the doorbell word reaches db_first + b).
+struct RingBatch {
+    const uint8_t* arena;
+    void* out;
+};
+struct RingArgs {
+    uint64_t n;               // frames per batch
+    uint32_t stride;          // slot bytes (>= 64, multiple of 16)
+    uint32_t nbatches;
+    uint32_t policy;          // INGOT_TUNE_CACHE_POLICY bits
+    uint32_t published;       // batches known published at launch (no poll below)
+    const uint32_t* doorbell; // device address of the doorbell word, or NULL
+    uint32_t db_first;        // doorbell value that publishes batch 0
+    uint32_t tiles_per_batch;
+    uint64_t timeout_ticks;   // wall-clock ticks a wave waits for a batch
+    uint32_t* status;         // optional: |= 1 when a wave gave up waiting
+    RingBatch b[INGOT_RING_MAX_BATCHES];
+};
+static_assert(sizeof(RingArgs) <= 4096, "RingArgs exceeds the 4 KiB kernel-argument limit");
+
 // Histogram pass over flow bins (flow.hip).
 hipError_t launch_flow_hist(const uint32_t* flow, uint64_t n, uint32_t* hist, uint32_t bins,
                             void* work, size_t work_bytes, hipStream_t s);
@@ -103,7 +131,7 @@ size_t packed_workspace(uint64_t n);
 hipError_t launch_tile_bases(const uint16_t* len, uint64_t n, void* work, hipStream_t s);
 
 // One wave that holds its stream for `ticks` of the device's constant-rate
-// wall clock (ingot_gpu_stream_delay, packed.hip).
+// wall clock (ingot_gpu_stream_delay, stream.hip).
 hipError_t launch_delay(uint64_t ticks, hipStream_t s);
 
 // Per-context tuning (0 = measured default); see INGOT_TUNE_* in ingot_gpu.h.
@@ -120,6 +148,7 @@ struct Tuning {
     int read_plan = 0;     // parse_read: LDS pieces per staged chunk (see launch_parse)
     int flow_kernel = 0;   // flows: 0 = k_parse (16-bit table: one tile per wave), 1 = hash
                            // overlapped with the next tile (k_flows), 2 = k_parse persistent
+    int ring_grid = 0;     // ring consumer: blocks per CU (0 = measured default)
     uint32_t cus = 256;  // compute units of the context's device (grid shaping)
     bool host_arena = false;  // per call: the arena is host memory (ingot_gpu_host_map)
 };
@@ -128,6 +157,7 @@ hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, int mode
                         const Tuning& t, hipStream_t s);
 hipError_t launch_flows(const FlowArgs& a, int layout_kind, int chain, const Tuning& t,
                         hipStream_t s);
+hipError_t launch_ring(const RingArgs& a, int chain, int mode, const Tuning& t, hipStream_t s);
 hipError_t launch_modify(const ModifyArgs& a, int layout_kind, int chain, const Tuning& t,
                          hipStream_t s);
 bool tuning_valid(int key, int value);

@@ -1759,6 +1759,135 @@ __global__ __launch_bounds__(BLOCK) void k_parse_pipe(ParseArgs a) {
     }
 }
 
+// One 32-bit word read past every cache (system scope: a doorbell in pinned
+// host memory, written by the host while the kernel runs), made uniform.
+// A vector load in asm: the compiler would turn a uniform plain load into a
+// scalar one served from the scalar cache, and never see the new value.
+__device__ __forceinline__ uint32_t load_system_u32(const uint32_t* p) {
+    uint32_t v;
+    asm volatile("global_load_dword %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
+                 : "=v"(v)
+                 : "v"(p)
+                 : "memory");
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+// Persistent ring consumer (ingot_gpu_parse_ring): k_parse_pipe's staging and
+// walk over the tiles of up to INGOT_RING_MAX_BATCHES batches in one launch.
+// The batches' tiles are laid end to end and wave w of the W in the grid
+// takes tiles w, w + W, w + 2W, ..., so every wave crosses the batch
+// boundaries with its next tile's LDS-DMA already in flight: one grid ramp-up
+// and one drain per launch instead of one per batch (the per-launch cost the
+// two-stream schedule only half hides).  Tiles of batch b are
+// staged only once b is published: b < a.published (known at launch), else
+// the doorbell word >= db_first + b, polled by the wave that needs it.
+template <uint32_t NCH, uint32_t DEPTH, int CHAIN, int MODE>
+__global__ __launch_bounds__(BLOCK) void k_parse_ring(RingArgs a) {
+    constexpr uint32_t WIN = NCH * 16u;
+    constexpr uint32_t WAVE_DW = WAVE * NCH * 4u;
+    constexpr uint32_t IMG_DW = WAVES * WAVE_DW + 16u;
+    __shared__ __attribute__((aligned(16))) uint32_t s_img[DEPTH * IMG_DW];
+    const uint32_t lane = threadIdx.x & (WAVE - 1u);
+    const uint32_t wave = threadIdx.x / WAVE;
+    uint32_t* img0 = s_img + wave * WAVE_DW;
+    const uint32_t tpb = a.tiles_per_batch;
+    const uint32_t W = gridDim.x * WAVES;
+    const uint32_t total = tpb * a.nbatches;  // < 2^32 (api.cpp)
+    const uint32_t g0 = blockIdx.x * WAVES + wave;
+    if (g0 >= total) return;
+    const uint32_t J = (total - g0 + W - 1u) / W;  // this wave's tiles
+    const uint32_t take = a.stride < WIN ? a.stride : WIN;
+    uint32_t avail = a.published;  // batches [0, avail) are known published
+    bool live = true;              // false once this wave gave up waiting
+
+    // Batch b published?  Polls only past `avail`: one lane's system-scope
+    // load of the doorbell, sleeping between polls, until the word reaches
+    // db_first + b or the wave's wait exceeds timeout_ticks.  On success the
+    // wave's caches are invalidated (system-scope acquire) before it stages
+    // the new batch, so frames written after the launch started are seen.
+    auto ready = [&](uint32_t b) -> bool {
+        if (b < avail) return true;
+        if (!a.doorbell) return false;
+        const uint64_t t0 = wall_clock64();
+        for (;;) {
+            const uint32_t v = load_system_u32(a.doorbell);
+            if (v >= a.db_first + b) {
+                const uint32_t pub = v - a.db_first + 1u;
+                avail = pub < a.nbatches ? pub : a.nbatches;
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                return true;
+            }
+            if (wall_clock64() - t0 > a.timeout_ticks) {
+                if (a.status && lane == 0) atomicOr(a.status, 1u);
+                return false;
+            }
+            __builtin_amdgcn_s_sleep(32);
+        }
+    };
+    // (batch, tile) cursors of the next tile to stage and to parse
+    uint32_t sb = g0 / tpb, st = g0 - sb * tpb;
+    uint32_t pb = sb, pt = st;
+    auto adv = [&](uint32_t& b, uint32_t& t) {
+        t += W;
+        while (t >= tpb) {
+            t -= tpb;
+            ++b;
+        }
+    };
+    auto stage = [&](uint32_t b, uint32_t t, uint32_t* img) {
+        const uint8_t* arena = a.b[b].arena;
+#pragma unroll
+        for (uint32_t k = 0; k < NCH; ++k) {
+            const uint32_t q = k * WAVE + lane;
+            const uint32_t pp = q / NCH;
+            const uint32_t c = (q - pp * NCH) ^ swz<NCH>(pp);
+            uint64_t slot = (uint64_t)t * WAVE + pp;
+            if (slot >= a.n) slot = a.n - 1u;  // a valid address for the tail tile
+            stage16p(arena + slot * a.stride + 16u * c, img + k * WAVE * 4u, a.policy);
+        }
+    };
+    auto parse = [&](uint32_t b, uint32_t t, const uint32_t* img) {
+        const uint64_t i = (uint64_t)t * WAVE + lane;
+        Frame<NCH> fr{(const lds_u32*)img, lane, 0u, take, a.stride, a.b[b].arena + i * a.stride};
+        Rec r;
+        walk<CHAIN, false>(fr, r, nullptr, nullptr);
+        if (i < a.n) {
+            if constexpr (MODE == OUT_REC8)
+                store_rec(static_cast<uint2*>(a.b[b].out) + i, pack8(r), a.policy);
+            else
+                store_rec(static_cast<uint4*>(a.b[b].out) + i, pack(r), a.policy);
+        }
+    };
+    // stage the next tile when there is one and its batch is published
+    auto issue = [&](uint32_t& js) -> bool {
+        if (!live || js >= J) return false;
+        if (!ready(sb)) {
+            live = false;
+            return false;
+        }
+        stage(sb, st, img0 + (js % DEPTH) * IMG_DW);
+        ++js;
+        adv(sb, st);
+        return true;
+    };
+
+    uint32_t js = 0;  // tiles staged so far
+#pragma unroll
+    for (uint32_t d = 0; d + 1u < DEPTH; ++d) issue(js);
+    for (uint32_t j = 0; j < js; ++j) {
+        // tile j's loads have landed: only the DEPTH-1 younger tiles' loads
+        // may still be in flight (record stores count too: conservative)
+        if (issue(js) && js - j == DEPTH)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DEPTH - 1u) * NCH) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        parse(pb, pt, img0 + (j % DEPTH) * IMG_DW);
+        adv(pb, pt);
+        // every lane's reads of this image have returned before it is restaged
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+}
+
 // In-place rewrite on a slot ring (C2m: the reference's parse-and-decr-v4):
 // k_parse_pipe's multi-tile staging, then the setters edit the staged copy
 // (put_staged) and mark the write-back units they touch; the wave writes the
@@ -2317,8 +2446,56 @@ hipError_t launch_flows(const FlowArgs& a, int layout_kind, int chain, const Tun
                : launch_flows_mode<OUT_FLOWS>(a, layout_kind, chain, t, s);
 }
 
+template <uint32_t DEPTH, int MODE>
+hipError_t launch_ring_chain(const RingArgs& a, int chain, uint32_t grid, hipStream_t s) {
+    switch (chain) {
+    case INGOT_CHAIN_UDP_PARSER:
+        hipLaunchKernelGGL((k_parse_ring<4, DEPTH, INGOT_CHAIN_UDP_PARSER, MODE>), dim3(grid),
+                           dim3(BLOCK), 0, s, a);
+        break;
+    case INGOT_CHAIN_GENERIC_ULP:
+        hipLaunchKernelGGL((k_parse_ring<4, DEPTH, INGOT_CHAIN_GENERIC_ULP, MODE>), dim3(grid),
+                           dim3(BLOCK), 0, s, a);
+        break;
+    case INGOT_CHAIN_VLAN_ULP:
+        hipLaunchKernelGGL((k_parse_ring<4, DEPTH, INGOT_CHAIN_VLAN_ULP, MODE>), dim3(grid),
+                           dim3(BLOCK), 0, s, a);
+        break;
+    default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// The ring consumer's grid is persistent: blocks per CU x CUs (default 2,
+// like the single-batch ring kernel), capped at one tile per wave.  Cache
+// policy as k_parse_pipe's (nt staging loads; 16-B records stored sc1).
+hipError_t launch_ring(const RingArgs& args, int chain, int mode, const Tuning& t,
+                       hipStream_t s) {
+    RingArgs a = args;
+    if (a.nbatches == 0 || a.n == 0) return hipSuccess;
+    if (t.cache_policy == 0) a.policy = mode == OUT_REC16 ? 11u : 3u;
+    else a.policy = (uint32_t)t.cache_policy & 0x1fbu;
+    const uint64_t total = (uint64_t)a.tiles_per_batch * a.nbatches;
+    const uint64_t bpc = t.ring_grid ? (uint64_t)t.ring_grid : 2ull;
+    uint64_t blocks = (total + WAVES - 1) / WAVES;
+    if (blocks > bpc * t.cus) blocks = bpc * t.cus;
+    const uint32_t g = (uint32_t)(blocks ? blocks : 1);
+    const bool r8 = mode == OUT_REC8;
+    switch (t.pipe_depth) {
+    case 3: return r8 ? launch_ring_chain<3, OUT_REC8>(a, chain, g, s)
+                      : launch_ring_chain<3, OUT_REC16>(a, chain, g, s);
+    case 4: return r8 ? launch_ring_chain<4, OUT_REC8>(a, chain, g, s)
+                      : launch_ring_chain<4, OUT_REC16>(a, chain, g, s);
+    default: return r8 ? launch_ring_chain<2, OUT_REC8>(a, chain, g, s)
+                       : launch_ring_chain<2, OUT_REC16>(a, chain, g, s);
+    }
+}
+
 bool tuning_valid(int key, int value) {
     switch (key) {
+    case INGOT_TUNE_RING_GRID:
+        return value >= 0 && value <= 8;
     case INGOT_TUNE_WINDOW_INDEXED:  // 20 + k: line-completing, up to k chunks
         return value == 0 || (value >= 2 && value <= 6) || value == 8 || value == 9 ||
                value == 100 || (value >= 22 && value <= 26) || value == 28 || value == 29 ||

@@ -67,6 +67,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     lib.oracle_parse_read_batch.restype = ctypes.c_int
     lib.oracle_set_passes.argtypes = [ctypes.c_int]
     lib.oracle_set_passes.restype = None
+    lib.oracle_set_affinity.argtypes = [vp, ctypes.c_int]
+    lib.oracle_set_affinity.restype = None
     if path is None:
         _lib = lib
     return lib

@@ -12,9 +12,11 @@
  * ingot-examples/benches/packet.rs) and tests/test_oracle_golden.py checks
  * this file against every one of them.
  */
+#define _GNU_SOURCE
 #include "ingot_oracle.h"
 
 #include <pthread.h>
+#include <sched.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -930,6 +932,27 @@ static int g_passes = 1;
 
 void oracle_set_passes(int passes) { g_passes = passes < 1 ? 1 : passes; }
 
+/* CPUs the workers are pinned to (bench.py's CPU baseline: one thread per
+ * CPU the process may use, worker t on cpus[t % n]); none = unpinned. */
+static int* g_cpus = 0;
+static int g_ncpus = 0;
+
+void oracle_set_affinity(const int* cpus, int n) {
+    free(g_cpus);
+    g_cpus = 0;
+    g_ncpus = 0;
+    if (!cpus || n <= 0) return;
+    g_cpus = (int*)malloc((size_t)n * sizeof(int));
+    if (!g_cpus) return;
+    memcpy(g_cpus, cpus, (size_t)n * sizeof(int));
+    g_ncpus = n;
+}
+
+static void pin_set(int t, cpu_set_t* set) {
+    CPU_ZERO(set);
+    CPU_SET(g_cpus[t % g_ncpus], set);
+}
+
 static void* run_range(void* arg) {
     range_job_t* j = (range_job_t*)arg;
     for (int k = 0; k < g_passes; ++k) j->fn(j->ctx, j->lo, j->hi);
@@ -956,10 +979,29 @@ static int parallel_ranges(uint64_t n, int nthreads, range_fn fn, void* ctx) {
     }
     int started = 0;
     for (int t = 1; t < nthreads; ++t) {
-        if (pthread_create(&th[t], 0, run_range, &jobs[t]) != 0) break;
+        pthread_attr_t attr;
+        pthread_attr_t* ap = 0;
+        if (g_ncpus && pthread_attr_init(&attr) == 0) {
+            cpu_set_t set;
+            pin_set(t, &set);
+            pthread_attr_setaffinity_np(&attr, sizeof(set), &set);
+            ap = &attr;
+        }
+        const int rc = pthread_create(&th[t], ap, run_range, &jobs[t]);
+        if (ap) pthread_attr_destroy(ap);
+        if (rc != 0) break;
         started = t;
     }
+    /* worker 0 is the calling thread: pinned for the call, then restored */
+    cpu_set_t saved;
+    const int repin = g_ncpus && pthread_getaffinity_np(pthread_self(), sizeof(saved), &saved) == 0;
+    if (repin) {
+        cpu_set_t set;
+        pin_set(0, &set);
+        pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+    }
     run_range(&jobs[0]);
+    if (repin) pthread_setaffinity_np(pthread_self(), sizeof(saved), &saved);
     for (int t = 1; t <= started; ++t) pthread_join(th[t], 0);
     /* any range whose thread failed to start runs here */
     for (int t = started + 1; t < nthreads; ++t) run_range(&jobs[t]);

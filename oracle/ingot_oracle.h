@@ -57,6 +57,8 @@ int oracle_parse_batch(const uint8_t* arena, const uint64_t* off,
 /* Throughput measurement only: every batch worker repeats its range `passes`
  * times per call (thread start-up amortised over more work). */
 void oracle_set_passes(int passes);
+/* Pin batch worker t to cpus[t % n] (NULL / 0: unpinned); bench.py's CPU baseline. */
+void oracle_set_affinity(const int* cpus, int n);
 
 /* Generic big-endian bitfield getter (ingot-macros/src/packet/bitfield.rs
  * BE get paths): the n_bits (<= 64) starting at bit first_bit, MSB first. */

@@ -98,3 +98,33 @@ def test_host_tensors_are_rejected_after_shape_checks(ctx):
     arena, off, lens = _bufs()
     with pytest.raises(ValueError, match="must live on cuda:0"):
         ctx.parse(arena, off, lens, Chain.UdpParser, out=torch.empty((8, 16), dtype=torch.uint8))
+
+
+def test_check_descriptors_catches_out_of_arena_values():
+    """Descriptor values are the caller's contract; check_descriptors tests
+    them on demand (CPU tensors here)."""
+    import torch
+
+    import ingot_amd
+
+    arena = torch.zeros(1000, dtype=torch.uint8)
+    off = torch.tensor([0, 100, 900], dtype=torch.int64)
+    lens = torch.tensor([60, 64, 100], dtype=torch.int32).to(torch.uint16)
+    ingot_amd.check_descriptors(arena, off=off, lens=lens)
+    with pytest.raises(ValueError):
+        ingot_amd.check_descriptors(arena, off=off, lens=torch.tensor([60, 64, 101]).to(
+            torch.uint16))
+    seg_off = torch.tensor([0, 14, 34], dtype=torch.int64)
+    seg_len = torch.tensor([14, 20, 30], dtype=torch.int32).to(torch.uint16)
+    ps = torch.tensor([0, 2, 3], dtype=torch.int32)
+    ingot_amd.check_descriptors(arena, seg_off=seg_off, seg_len=seg_len, pkt_seg=ps)
+    with pytest.raises(ValueError):
+        ingot_amd.check_descriptors(arena, seg_off=seg_off, seg_len=seg_len,
+                                    pkt_seg=torch.tensor([0, 2, 4], dtype=torch.int32))
+    with pytest.raises(ValueError):
+        ingot_amd.check_descriptors(arena, seg_off=seg_off, seg_len=seg_len,
+                                    pkt_seg=torch.tensor([0, 2, 1], dtype=torch.int32))
+    dense = (seg_off << 16) | seg_len.to(torch.int64)
+    ingot_amd.check_descriptors(arena, seg=dense, pkt_seg=ps)
+    with pytest.raises(ValueError):
+        ingot_amd.check_descriptors(arena, seg=dense + (1000 << 16), pkt_seg=ps)

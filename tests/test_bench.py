@@ -245,3 +245,64 @@ def test_timed_region_spans_earliest_start_to_latest_end(monkeypatch):
     with pytest.raises(RuntimeError):
         bench._timed(_ClockTorch, [_ClockStream()], lambda k: -1, 3, gate=_Gate(log2))
     assert log2 == ["arm", "open"]
+
+
+def test_gate_policy():
+    """No collective behind an unrung doorbell: config 5 over RCCL at N > 1
+    holds launches only until its first collective; the gloo rehearsal
+    (host-side reduce) is not gated; everything else holds Gate.HOLD."""
+    assert bench.gate_policy(False, 1, "nccl", False) == "hold"
+    assert bench.gate_policy(True, 1, "nccl", False) == "hold"
+    assert bench.gate_policy(False, 8, "nccl", False) == "hold"
+    assert bench.gate_policy(True, 8, "nccl", False) == "until_collective"
+    assert bench.gate_policy(True, 2, "gloo", False) == "off"
+    assert bench.gate_policy(True, 8, "nccl", True) == "off"
+
+
+def test_flow_runner_rings_the_doorbell_before_every_collective():
+    """Under a gate, FlowRunner opens it before issuing the first all-reduce
+    of the region: every reduce in the log comes after an "open"."""
+    log = []
+    reps = 4
+
+    class _Buf:
+        def __init__(self, i):
+            self.i = i
+
+        def data_ptr(self):
+            return self.i
+
+    class _LogGate:
+        def arm(self, streams):
+            log.append(("arm",))
+
+        def open(self):
+            log.append(("open",))
+
+    def reduce_fn(h):
+        log.append(("reduce", h.i))
+        return _Work(log, h.i)
+
+    hists = [_Hist(log, i) for i in range(reps)]
+    r = bench.FlowRunner(_FakeTorch, _Lib(log), _Ctx(), Chain.VlanUlp, 8,
+                         [_Buf(i) for i in range(reps)], _Buf(0), _Buf(0), hists,
+                         [_Buf(0)] * reps, [_Stream(), _Stream()], reduce_fn)
+    r.run(6, gate=_LogGate())
+    ops = [e[0] for e in log]
+    assert ops[0] == "arm"
+    first_reduce = ops.index("reduce")
+    assert "open" in ops[:first_reduce]
+    assert ops.count("reduce") == 6
+    # and without a gate nothing is opened
+    log.clear()
+    r.run(2)
+    assert "open" not in [e[0] for e in log]
+
+
+def test_ring_group_divides_the_steps():
+    assert bench.ring_group(20) == 20
+    assert bench.ring_group(2000) == 50
+    assert bench.ring_group(64) == 64
+    assert bench.ring_group(67) == 1  # prime above the cap
+    assert bench.ring_group(200) == 50
+    assert bench.ring_group(1) == 1

@@ -86,6 +86,42 @@ def test_ring_releases_several_streams(env):
     db.close()
 
 
+def test_held_queue_blocks_its_streams(env):
+    """A doorbell wait holds its whole hardware queue (include/ingot_gpu.h):
+    with more streams than GPU_MAX_HW_QUEUES (4 on this image), streams that
+    HIP mapped onto the held stream's queue do not run until the ring, while
+    streams on other queues do.  A producer that published its frames from
+    such a stream and rang only after that work finished would deadlock; from
+    the host (as here) the ring releases everything."""
+    torch, ctx = env
+    db = ingot_amd.Doorbell(ctx)
+    arena, _, _ = ingot_amd.gen_frames(GenProfile.V4UDP64, 4096, stride=64)
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in range(9)]
+    watchdog = threading.Timer(5.0, lambda: db.ring(1))
+    watchdog.start()
+    try:
+        db.wait(1, streams[0])
+        evs = []
+        for s in streams[1:]:
+            ctx.parse_strided(arena, 64, 4096, Chain.UdpParser, stream=s)
+            e = torch.cuda.Event()
+            e.record(s)
+            evs.append(e)
+        time.sleep(0.3)
+        ran = [e.query() for e in evs]
+        db.ring(1)
+    finally:
+        watchdog.cancel()
+        db.ring(1)
+    torch.cuda.synchronize()
+    assert all(e.query() for e in evs)
+    assert any(ran), "no stream ran beside the held one"
+    assert not all(ran), ("every stream ran beside the held queue: more hardware queues than "
+                          "streams on this box?")
+    db.close()
+
+
 def test_stream_delay_holds_the_stream(env):
     """ingot_gpu_stream_delay: work enqueued after it starts `ns` later (device
     wall clock); 0 is a no-op; the parse behind it is unchanged."""

@@ -181,3 +181,38 @@ def test_protocol_constants_and_eh_classes_match_reference():
     for p in range(256):
         want = 1 if p in frag else 2 if p in r6564 else 0
         assert oracle.v6eh_class(p) == want, p
+
+
+PACKETS = Path("/root/reference/ingot-examples/src/packets.rs")
+MACRO = Path("/root/reference/ingot-macros/src/parse.rs")
+
+
+@pytest.mark.skipif(not PACKETS.exists(), reason="reference checkout not present")
+def test_chain_labels_are_the_reference_crstr_labels():
+    """ingot_chain_layer_label(chain, i) is the label the generated parser
+    attaches to a PacketParseError at layer i: the field name of the
+    `#[derive(Parse)]` struct, as `CRStr::new_unchecked("<field>\\0")`
+    (ingot-macros/src/parse.rs:36-50; ingot-examples/src/packets.rs:18-60).
+    A Rust binding keeps a static CRStr table equal to these strings
+    (INTEGRATION.md §2), indexed by the record's err_layer."""
+    from ingot_amd import _lib
+    from ingot_amd.abi import Chain
+
+    macro = MACRO.read_text()
+    # the label literal is the field name plus a NUL terminator
+    assert 'format!("{}\\0", self.fname)' in macro
+    assert "CRStr::new_unchecked(#fname_str)" in macro
+    text = PACKETS.read_text()
+    structs = {}
+    for m in re.finditer(r"#\[derive\(Parse\)\]\s*pub struct (\w+)<[^>]*>\s*\{(.*?)\n\}", text,
+                         re.S):
+        structs[m.group(1)] = re.findall(r"^\s*pub (\w+):", m.group(2), re.M)
+    assert set(structs) >= {"UdpParser", "GenericUlp", "GeneveOverV6Tunnel"}
+    lib = _lib.load()
+    for name, chain in (("UdpParser", Chain.UdpParser), ("GenericUlp", Chain.GenericUlp),
+                        ("GeneveOverV6Tunnel", Chain.GeneveOverV6Tunnel)):
+        fields = structs[name]
+        n = lib.ingot_chain_layer_count(int(chain))
+        assert n == len(fields), name
+        got = [lib.ingot_chain_layer_label(int(chain), i) + b"\0" for i in range(n)]
+        assert got == [f"{f}\0".encode() for f in fields], name

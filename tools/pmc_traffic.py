@@ -32,7 +32,7 @@ def run_pass(counter: str, config: str, outdir: Path, steps: int, extra=()) -> l
     cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", str(d), "-o", "run",
            "--", sys.executable, str(ROOT / "bench.py"), "--config", config, "--steps", str(steps),
            "--warmup", "2", "--streams", "1", "--no-cpu-baseline", "--no-variants", "--no-gate",
-           "--no-host-path",
+           "--no-host-path", "--no-sublines",
            *extra]
     env = dict(os.environ, TMPDIR="/tmp")
     r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=180)
@@ -72,12 +72,15 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--tag", default="r02")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--timing", default="launches", choices=("launches", "ring"),
+                    help="ring: profile k_parse_ring launches of bench.ring_group(steps) "
+                         "batches (bench.py --timing ring)")
     ap.add_argument("--tune", action="append", default=[],
                     help="bench.py --tune KEY=VALUE for a variant; its file is named "
                          "<tag>_pmc_<config>@<key>=<value>.json (never attached to a bench line)")
     args = ap.parse_args()
-    extra = [x for kv in args.tune for x in ("--tune", kv)]
-    suffix = "".join(f"@{kv}" for kv in args.tune)
+    extra = [x for kv in args.tune for x in ("--tune", kv)] + ["--timing", args.timing]
+    suffix = ("_ring" if args.timing == "ring" else "") + "".join(f"@{kv}" for kv in args.tune)
     out = ROOT / "gpurun_out" / f"pmc_{args.config}{suffix}"
     fetch = run_pass("FETCH_SIZE", args.config, out, args.steps, extra)
     write = run_pass("WRITE_SIZE", args.config, out, args.steps, extra)
@@ -88,13 +91,16 @@ def main():
     sys.path.insert(0, str(ROOT))
     import bench
 
+    group = bench.ring_group(args.steps) if args.timing == "ring" else 1
     if len(KERNELS) != 1:
         raise RuntimeError(f"the two passes profiled different kernels: {sorted(KERNELS)}")
     res = {
         "config": args.config,
         "kernel": sorted(KERNELS)[0],
         "sources_sha": bench.kernel_sources_sha(),
-        "frames_per_launch": bench.CONFIGS[args.config][1],
+        "frames_per_launch": bench.CONFIGS[args.config][1] * group,
+        "batches_per_launch": group,
+        "timing": args.timing,
         "dispatches": [len(fetch), len(write)],
         "FETCH_SIZE_KiB_median": f_kib,
         "WRITE_SIZE_KiB_median": w_kib,

@@ -1,0 +1,120 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of the C2 timed region as the driver runs it (K-step
+regions after a W-step warm-up, doorbell-gated): the per-batch launches on
+two staggered streams (round-2 headline) against the persistent ring
+consumer (ingot_gpu_parse_ring) over its grid / depth / cache-policy knobs.
+
+    python tools/ring_ab.py [--steps 20] [--warmup 5] [--reps 15] [--out F]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import statistics
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=15)
+    ap.add_argument("--variants", default="")
+    ap.add_argument("--out", default=str(ROOT / "gpurun_out" / "ring_ab.json"))
+    args = ap.parse_args()
+
+    import torch
+
+    import ingot_amd
+    from ingot_amd import Chain, GenProfile, abi
+
+    ctx = ingot_amd.Context(0)
+    lib = ingot_amd.load_library()
+    n, stride = 1 << 20, 64
+    arena, _, _ = ingot_amd.gen_frames(GenProfile.V4UDP64, n, stride=stride)
+    reps = 8
+    arenas = [arena] + [arena.clone() for _ in range(reps - 1)]
+    outs = [torch.empty((n, 16), dtype=torch.uint8, device="cuda") for _ in range(64)]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(3)]
+    gate = bench.Gate(ingot_amd, ctx, 6.0)
+    G = bench.ring_group(args.steps)
+
+    knobs = {"grid": abi.TUNE_RING_GRID, "depth": abi.TUNE_PIPE_DEPTH,
+             "pol": abi.TUNE_CACHE_POLICY}
+    variants = {
+        "pipe2": None,
+        "ring": {},
+        "ring_g1": {"grid": 1},
+        "ring_g3": {"grid": 3},
+        "ring_g4": {"grid": 4},
+        "ring_d3": {"depth": 3},
+        "ring_d4": {"depth": 4},
+        "ring_g4_d3": {"grid": 4, "depth": 3},
+        "ring_nt": {"pol": 3},
+        "ring_plain": {"pol": 4},
+    }
+    if args.variants:
+        keep = args.variants.split(",")
+        variants = {k: v for k, v in variants.items() if k in keep}
+
+    def set_knobs(kv):
+        for k, key in knobs.items():
+            ctx.set_tuning(key, (kv or {}).get(k, 0))
+
+    def runner(name):
+        if variants[name] is None:
+            return bench.Runner(torch, lib, ctx, Chain.UdpParser, n, stride, arenas, None, None,
+                                outs[:reps], streams[:2], 16)
+        return bench.RingRunner(torch, lib, ctx, Chain.UdpParser, n, stride, arenas, outs,
+                                streams[0], 16, G)
+
+    runners = {k: runner(k) for k in variants}
+    res = {k: [] for k in variants}
+    for r in range(args.reps):
+        for name, kv in variants.items():
+            set_knobs(kv)
+            rr = runners[name]
+            if isinstance(rr, bench.RingRunner):
+                rr.warm(args.warmup, gate)
+            else:
+                rr.run(args.warmup, gate)
+            torch.cuda.synchronize()
+            ms, _ = rr.run(args.steps, gate)
+            res[name].append(ms * 1e3 / args.steps)
+        print(f"rep {r}: " + " ".join(f"{k}={v[-1]:.3f}" for k, v in res.items()), flush=True)
+    set_knobs(None)
+    # steady state: 2,000-step regions
+    steady = {}
+    for name in ("pipe2", "ring"):
+        if name not in runners:
+            continue
+        rr = runners[name]
+        if isinstance(rr, bench.RingRunner):
+            rr = bench.RingRunner(torch, lib, ctx, Chain.UdpParser, n, stride, arenas, outs,
+                                  streams[0], 16, bench.ring_group(2000))
+        rr.run(200, gate)
+        ms, _ = rr.run(2000, gate)
+        steady[name] = ms * 1e3 / 2000
+    rd = 64 * n
+    summary = {k: {"median_us_per_step": round(statistics.median(v), 3),
+                   "min": round(min(v), 3), "max": round(max(v), 3),
+                   "Gpkt_s": round(n / statistics.median(v) / 1e3, 2),
+                   "read_frac": round(rd / (statistics.median(v) * 1e-6) / 8e12, 4)}
+               for k, v in res.items()}
+    out = {"steps": args.steps, "warmup": args.warmup, "reps": args.reps, "group": G,
+           "summary": summary, "steady_2000_us_per_step": steady, "raw": res}
+    Path(args.out).parent.mkdir(parents=True, exist_ok=True)
+    Path(args.out).write_text(json.dumps(out, indent=1))
+    print(json.dumps(summary, indent=1))
+    print("steady", steady)
+
+
+if __name__ == "__main__":
+    main()
