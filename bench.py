@@ -354,7 +354,7 @@ class RingRunner:
                 tables[key] = t
             return tables[key]
 
-        def launch(k, m):
+        def launch(k, m=1):
             return lib.ingot_gpu_parse_ring(h, ctypes.cast(table(k, m), ctypes.c_void_p), m,
                                             stride, n, c, record_bytes, None, 0, 0, None, sp)
 

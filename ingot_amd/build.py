@@ -20,7 +20,7 @@ ROOT = PKG.parent
 CSRC = PKG / "csrc"
 BUILD = PKG / "build"
 LIB = PKG / "lib" / "libingot_gpu.so"
-SOURCES = ["parse.hip", "flow.hip", "header.hip", "packed.hip", "pktgen.hip", "stream.hip", "api.cpp"]
+SOURCES = ["parse.hip", "read.hip", "ring.hip", "flow.hip", "header.hip", "packed.hip", "pktgen.hip", "stream.hip", "api.cpp"]
 ARCH = "gfx950"
 
 
@@ -69,7 +69,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
             jobs.append((src, obj))
     if jobs:
         try:
-            with cf.ThreadPoolExecutor(max_workers=min(len(jobs), 4)) as ex:
+            with cf.ThreadPoolExecutor(max_workers=min(len(jobs), 6)) as ex:
                 for f in [ex.submit(_compile, s, o) for s, o in jobs]:
                     f.result()
         except Exception:

@@ -158,6 +158,14 @@ hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, int mode
 hipError_t launch_flows(const FlowArgs& a, int layout_kind, int chain, const Tuning& t,
                         hipStream_t s);
 hipError_t launch_ring(const RingArgs& a, int chain, int mode, const Tuning& t, hipStream_t s);
+// launch_parse's branches in their own files: parse_read over chunk lists
+// (read.hip; `a` with its cache policy set, `g` the one-tile-per-wave grid)
+// and the slot-ring kernels (ring.hip).
+hipError_t launch_segmented(const ParseArgs& a, int chain, int mode, const Tuning& t, uint32_t g,
+                            hipStream_t s);
+hipError_t launch_slot_ring(const ParseArgs& a, int chain, int mode, const Tuning& t,
+                            hipStream_t s);
+hipError_t launch_modify_ring(const ModifyArgs& a, int chain, const Tuning& t, hipStream_t s);
 hipError_t launch_modify(const ModifyArgs& a, int layout_kind, int chain, const Tuning& t,
                          hipStream_t s);
 bool tuning_valid(int key, int value);

@@ -1,0 +1,309 @@
+// read.hip — parse_read over chunk lists (ingot_gpu_parse_read*,
+// ingot-macros/src/parse.rs:511-537): the k_parse_read kernel with the header
+// chunks staged in LDS (SegFrameP) and its launcher; DESIGN.md §1b.
+#include "walk.h"
+
+namespace ingot_gpu {
+namespace {
+
+// parse_read over chunk lists with the header chunks staged (SegFrameP): per
+// tile, the packets' chunk bounds and the first four chunks' descriptors are
+// loaded together (independent loads), chunk 0 is staged packet-major like a
+// frame window, the later non-final chunks plane by plane, then the walk —
+// no dependent descriptor or byte load for headers inside staged pieces.
+// One 64-packet tile per wave.
+//
+// PIPE (persistent grid, INGOT_TUNE_READ_PLAN 12-14): the chain pkt_seg ->
+// chunk-0 descriptor -> staging is three dependent HBM round trips per tile,
+// and one tile per wave left them exposed.  A persistent wave instead keeps
+// the next tiles' lookups in flight while it walks the current one: tile
+// t + W's chunk-0 descriptor and tile t + 2W's chunk bounds are issued right
+// after tile t's staging: the staging and the lookahead loads are in flight
+// together and the wave waits for both (one round trip instead of three).
+template <int CS0, int CS1, int CS2, int CS3, int CHAIN, int MODE, bool DENSE = false,
+          bool PIPE = false>
+__global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
+    using FR = SegFrameP<CS0, CS1, CS2, CS3, DENSE>;
+    constexpr uint32_t P = CS0 + CS1 + CS2 + CS3;
+    constexpr uint32_t WAVE_DW = WAVE * P * 4u;
+    constexpr bool TUN = CHAIN == INGOT_CHAIN_GENEVE_OVER_V6;
+    __shared__ __attribute__((aligned(16))) uint32_t s_win[WAVES * WAVE_DW + 16];
+    const uint32_t lane = threadIdx.x & (WAVE - 1u);
+    const uint32_t wave = threadIdx.x / WAVE;
+    uint32_t* wimg = s_win + wave * WAVE_DW;
+    const uint64_t ntiles = (a.n + WAVE - 1u) / WAVE;
+    const uint64_t W = (uint64_t)gridDim.x * WAVES;
+    uint64_t t = (uint64_t)blockIdx.x * WAVES + wave;
+    if (t >= ntiles) return;
+
+    // packet i's chunk bounds (clamped index: always one load pair)
+    auto load_pkt = [&](uint64_t tt, uint32_t& s0, uint32_t& ns) {
+        uint64_t i = tt * WAVE + lane;
+        const bool v = i < a.n;
+        if (!v) i = a.n - 1u;
+        const uint32_t b0 = a.pkt_seg[i], b1 = a.pkt_seg[i + 1];
+        s0 = v ? b0 : 0u;
+        ns = v ? b1 - b0 : 0u;
+    };
+    // chunk 0's descriptor (none for a packet without chunks)
+    auto load_d0 = [&](uint32_t s0, uint32_t ns, uint64_t& o0, uint32_t& l0) {
+        if constexpr (DENSE) {
+            const uint64_t v = ns ? a.off[s0] : 0u;
+            o0 = v >> 16;
+            l0 = (uint32_t)(v & 0xffffu);
+        } else {
+            o0 = ns ? a.off[s0] : 0u;
+            l0 = ns ? a.len[s0] : 0u;
+        }
+    };
+    uint32_t s0, nseg, s0n = 0, nsn = 0;
+    uint64_t o0;
+    uint32_t l0;
+    load_pkt(t, s0, nseg);
+    load_d0(s0, nseg, o0, l0);
+    if constexpr (PIPE) load_pkt(t + W < ntiles ? t + W : t, s0n, nsn);
+
+    for (;;) {
+        const uint64_t i = t * WAVE + lane;
+        const bool valid = i < a.n;
+        FR fr;
+        fr.o0 = o0;
+        fr.l0 = l0;
+        if constexpr (DENSE) {
+            // one 8-B entry per chunk: (offset << 16) | length; chunks 1..3
+            // only when not the packet's last (SegFrameP::advance)
+            const uint64_t v1 = nseg > 2 ? a.off[s0 + 1] : 0u;
+            const uint64_t v2 = nseg > 3 ? a.off[s0 + 2] : 0u;
+            const uint64_t v3 = nseg > 4 ? a.off[s0 + 3] : 0u;
+            fr.o1 = v1 >> 16;
+            fr.o2 = v2 >> 16;
+            fr.o3 = v3 >> 16;
+            fr.l1 = (uint32_t)(v1 & 0xffffu);
+            fr.l2 = (uint32_t)(v2 & 0xffffu);
+            fr.l3 = (uint32_t)(v3 & 0xffffu);
+        } else {
+            fr.o1 = nseg > 2 ? a.off[s0 + 1] : 0u;
+            fr.o2 = nseg > 3 ? a.off[s0 + 2] : 0u;
+            fr.o3 = nseg > 4 ? a.off[s0 + 3] : 0u;
+            fr.l1 = nseg > 2 ? a.len[s0 + 1] : 0u;
+            fr.l2 = nseg > 3 ? a.len[s0 + 2] : 0u;
+            fr.l3 = nseg > 4 ? a.len[s0 + 3] : 0u;
+        }
+        // chunk 0, packet-major: instruction k, lane L fills slot 64k + L =
+        // packet q / CS0, piece (q mod CS0) ^ swz (16-B aligned absolute
+        // addresses; pieces only below the chunk's end)
+        const uint32_t sh0 = (uint32_t)((uintptr_t)(a.arena + fr.o0) & 15u);
+        const int64_t base0 = (int64_t)fr.o0 - (int64_t)sh0;
+        // chunk 0's window: CS0 pieces, or (a.linewin = m) a line-completing
+        // window — at least m pieces, then to the end of that 128-B line
+        // (k_parse's windows), at most CS0
+        uint32_t want = CS0;
+        if (a.linewin) {
+            const uint32_t lp = (uint32_t)((uintptr_t)(a.arena + base0) >> 4) & 7u;
+            want = ((lp + a.linewin + 7u) & ~7u) - lp;
+            if (want > (uint32_t)CS0) want = CS0;
+        }
+        const uint32_t wlim = 16u * want;
+        uint32_t ext = nseg ? sh0 + (fr.l0 < wlim - sh0 ? fr.l0 : wlim - sh0) : 0u;
+        // a later non-last chunk without planes that starts inside chunk 0's
+        // window: stage the window's pieces up to its end (or the window's)
+        auto widen = [&](uint32_t e, uint64_t o, uint32_t l) {
+            const int64_t d = (int64_t)o - base0;
+            if (FR::cs(e) == 0 && e + 1 < nseg && d >= 0 && d < (int64_t)wlim) {
+                const uint32_t end = (uint32_t)d + l < wlim ? (uint32_t)d + l : wlim;
+                ext = end > ext ? end : ext;
+            }
+        };
+        widen(1, fr.o1, fr.l1);
+        widen(2, fr.o2, fr.l2);
+        widen(3, fr.o3, fr.l3);
+        const uint32_t n0 = (ext + 15u) >> 4;
+#pragma unroll
+        for (uint32_t k = 0; k < (uint32_t)CS0; ++k) {
+            const uint32_t q = k * WAVE + lane;
+            const uint32_t pp = q / CS0;
+            const uint32_t c = (q - pp * CS0) ^ swz<CS0>(pp);
+            const uint32_t np = (uint32_t)__shfl((int)n0, (int)pp);
+            const int64_t bp = (int64_t)__shfl((long long)base0, (int)pp);
+            if (c < np) stage16(a.arena + bp + 16u * c, wimg + k * WAVE * 4u, false);
+        }
+        // chunks 1..3 unless last: piece j of chunk e into plane CS0 + pb(e) + j
+        auto stage_chunk = [&](uint32_t e, uint64_t o, uint32_t l) {
+            const uint32_t sh = (uint32_t)((uintptr_t)(a.arena + o) & 15u);
+            const uint32_t c = FR::staged(e, nseg);
+            for (uint32_t j = 0; j < FR::cs(e); ++j)
+                if (j < c && 16u * j < sh + l)
+                    stage16(a.arena + o - sh + 16u * j,
+                            wimg + (CS0 + FR::pb(e) + j) * WAVE * 4u, false);
+        };
+        if constexpr (CS1 > 0) stage_chunk(1, fr.o1, fr.l1);
+        if constexpr (CS2 > 0) stage_chunk(2, fr.o2, fr.l2);
+        if constexpr (CS3 > 0) stage_chunk(3, fr.o3, fr.l3);
+        uint32_t s0nn = 0, nsnn = 0;
+        uint64_t o0n = 0;
+        uint32_t l0n = 0;
+        if constexpr (PIPE) {
+            // lookahead, issued behind the staging (the compiler may not
+            // hoist loads across the barrier): tile t+W's chunk-0
+            // descriptor, tile t+2W's bounds
+            asm volatile("" ::: "memory");
+            load_d0(s0n, nsn, o0n, l0n);
+            const uint64_t t2 = t + 2u * W;
+            load_pkt(t2 < ntiles ? t2 : t, s0nn, nsnn);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+        fr.win = (const lds_u32*)wimg;
+        fr.p = lane;
+        fr.arena = a.arena;
+        fr.seg_off = a.off;
+        fr.seg_len = a.len;
+        fr.s0 = s0;
+        fr.k = 0;
+        fr.nseg = nseg;
+        fr.L = 0;
+        fr.b0 = base0;
+        fr.span0 = 16u * n0;
+        fr.enter(fr.o0, fr.l0, 0u, nseg ? want : 0u);
+        Rec r;
+        if constexpr (MODE == OUT_FIELDS) {
+            using OutT = typename std::conditional<TUN, ingot_geneve_fields, ingot_fields>::type;
+            OutT* G = static_cast<OutT*>(a.out) + (valid ? i : 0);
+            if (valid) {
+                uint4* z = reinterpret_cast<uint4*>(G);
+#pragma unroll
+                for (int k = 0; k < (int)(sizeof(OutT) / 16); ++k) z[k] = make_uint4(0, 0, 0, 0);
+                ingot_fields* F;
+                ingot_tunnel_fields* T = nullptr;
+                if constexpr (TUN) {
+                    F = &G->inner;
+                    T = &G->outer;
+                } else {
+                    F = G;
+                }
+                walk<CHAIN, true>(fr, r, F, T);
+                reinterpret_cast<uint4*>(F)[0] = pack(r);
+            }
+        } else {
+            walk<CHAIN, false>(fr, r, nullptr, nullptr);
+            if (valid) store_rec(static_cast<uint4*>(a.out) + i, pack(r), a.policy);
+        }
+        if (valid && a.chunk) a.chunk[i] = (uint16_t)fr.k;
+        // the next tile's LDS-DMA overwrites this image: every lane's reads
+        // above have returned (their values were consumed by the stores)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        t += W;
+        if (t >= ntiles) break;
+        if constexpr (PIPE) {
+            s0 = s0n;
+            nseg = nsn;
+            o0 = o0n;
+            l0 = l0n;
+            s0n = s0nn;
+            nsn = nsnn;
+        } else {
+            load_pkt(t, s0, nseg);
+            load_d0(s0, nseg, o0, l0);
+        }
+    }
+}
+
+// persist_cus != 0 (the PIPE kernels): a persistent grid of the blocks the
+// device holds at once.
+template <int CS0, int CS1, int CS2, int CS3, int MODE, bool DENSE = false, bool PIPE = false>
+hipError_t launch_read(const ParseArgs& a, int chain, uint32_t grid, hipStream_t s,
+                       uint32_t persist_cus = 0) {
+    auto go = [&](auto kernel) {
+        uint32_t g = grid;
+        if (persist_cus) {
+            const uint32_t cap = persist_cus * resident_per_cu(kernel);
+            if (g > cap) g = cap;
+        }
+        hipLaunchKernelGGL(kernel, dim3(g), dim3(BLOCK), 0, s, a);
+    };
+    switch (chain) {
+    case INGOT_CHAIN_UDP_PARSER:
+        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_UDP_PARSER, MODE, DENSE, PIPE>);
+        break;
+    case INGOT_CHAIN_GENERIC_ULP:
+        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENERIC_ULP, MODE, DENSE, PIPE>);
+        break;
+    case INGOT_CHAIN_VLAN_ULP:
+        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_VLAN_ULP, MODE, DENSE, PIPE>);
+        break;
+    default:
+        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENEVE_OVER_V6, MODE, DENSE, PIPE>);
+        break;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace
+
+// parse_read over chunk lists: chunk 0 staged in a 4-chunk (64-B) window
+// (first mblk-style chunks are short header blocks), the rest from L2/HBM.
+hipError_t launch_segmented(const ParseArgs& a, int chain, int mode, const Tuning& t,
+                            uint32_t g, hipStream_t s) {
+    if (mode != OUT_FIELDS && mode != OUT_REC16) return hipErrorInvalidValue;
+    // dense chunk table (ingot_gpu_parse_read_dense): no length array,
+    // one (offset << 16) | length entry per chunk
+    if (!a.len) {
+        if (mode == OUT_REC16 && t.read_plan >= 12)
+            return launch_read<4, 0, 0, 0, OUT_REC16, true, true>(a, chain, g, s, t.cus);
+        return mode == OUT_FIELDS ? launch_read<4, 0, 0, 0, OUT_FIELDS, true>(a, chain, g, s)
+                                  : launch_read<4, 0, 0, 0, OUT_REC16, true>(a, chain, g, s);
+    }
+    // INGOT_TUNE_READ_PLAN: 16-B pieces staged per chunk of the first four.
+    // Measured (tools/abtune.py, us per launch): the
+    // reference's one-header-per-chunk shape (c2r, 1 M) 33.3 on demand
+    // (9) / 25.1 {4,0,0,0} / 24.2 {2,2,2,0} / 27.0 {4,2,2,0}; header +
+    // payload chunks (c3r, 16.7 M) 651 / 667 / 681 / 769 — extra planes
+    // cost occupancy on the gather-bound shape.  Default (round 2): chunk
+    // 0 in a line-completing window of 3 to 5 pieces (to the end of the
+    // 128-B line its third piece lies in; k_parse's windows, DESIGN.md
+    // §4): c3r 676 -> 651 us, c2r 23.05 -> 23.24; 3 to 8 pieces reads 15%
+    // fewer bytes but loses occupancy (724 us).  1 = the round-1 {4,0,0,0}.
+    // (9, the round-1 kernel without descriptor prefetch, is k_parse over
+    // SegFrame: launch_parse runs it.)
+    if (mode == OUT_FIELDS) return launch_read<4, 0, 0, 0, OUT_FIELDS>(a, chain, g, s);
+    // chunk pools in mapped host memory keep the round-1 window (every
+    // staged piece is a PCIe read there)
+    switch (t.read_plan ? t.read_plan : t.host_arena ? 1 : 11) {
+    case 2: return launch_read<2, 2, 2, 0, OUT_REC16>(a, chain, g, s);
+    case 3: return launch_read<4, 2, 2, 0, OUT_REC16>(a, chain, g, s);
+    case 4: return launch_read<4, 1, 1, 0, OUT_REC16>(a, chain, g, s);
+    case 5: return launch_read<3, 0, 0, 0, OUT_REC16>(a, chain, g, s);
+    case 6: return launch_read<2, 0, 0, 0, OUT_REC16>(a, chain, g, s);
+    case 7:  // line-completing chunk-0 windows of 2 / 4 to 8 pieces
+    case 8: {
+        ParseArgs b = a;
+        b.linewin = t.read_plan == 7 ? 2u : 4u;
+        return launch_read<8, 0, 0, 0, OUT_REC16>(b, chain, g, s);
+    }
+    case 10: {  // ... of 2 to 5 pieces (11, the default: 3 to 5)
+        ParseArgs b = a;
+        b.linewin = 2u;
+        return launch_read<5, 0, 0, 0, OUT_REC16>(b, chain, g, s);
+    }
+    case 1: return launch_read<4, 0, 0, 0, OUT_REC16>(a, chain, g, s);
+    // 12-14: the persistent kernel with the descriptor lookahead (PIPE)
+    case 12: {
+        ParseArgs b = a;
+        b.linewin = 3u;
+        return launch_read<5, 0, 0, 0, OUT_REC16, false, true>(b, chain, g, s, t.cus);
+    }
+    case 13: return launch_read<4, 0, 0, 0, OUT_REC16, false, true>(a, chain, g, s, t.cus);
+    case 14: {
+        ParseArgs b = a;
+        b.linewin = 2u;
+        return launch_read<5, 0, 0, 0, OUT_REC16, false, true>(b, chain, g, s, t.cus);
+    }
+    default: {  // 11
+        ParseArgs b = a;
+        b.linewin = 3u;
+        return launch_read<5, 0, 0, 0, OUT_REC16>(b, chain, g, s);
+    }
+    }
+}
+
+}  // namespace ingot_gpu

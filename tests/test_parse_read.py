@@ -163,7 +163,7 @@ def split_many(frames, seed):
     return out
 
 
-@pytest.mark.parametrize("plan", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("plan", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
 def test_every_read_plan_is_bit_exact(torch, plan):
     """INGOT_TUNE_READ_PLAN: how many 16-B pieces of each of the first four
     chunks are staged in LDS never changes a record, a field block or the
@@ -231,6 +231,15 @@ def test_dense_chunk_table_matches(ctx, torch, chain):
     assert np.array_equal(c2.cpu().numpy().view(np.uint16), chunk)
     w_rec, _, w_chunk = oracle.parse_read_batch(*segs, chain)
     assert recs.tobytes() == w_rec.tobytes() and np.array_equal(chunk, w_chunk)
+    # the persistent lookahead kernel over the dense table (READ_PLAN >= 12)
+    from ingot_amd.abi import TUNE_READ_PLAN
+
+    c = ingot_amd.Context(0)
+    c.set_tuning(TUNE_READ_PLAN, 12)
+    r3, c3 = c.parse_read_dense(*d, chain)
+    torch.cuda.synchronize()
+    assert r3.cpu().numpy().tobytes() == recs.tobytes()
+    assert np.array_equal(c3.cpu().numpy().view(np.uint16), chunk)
 
 
 def scatter(packets, seed):
@@ -266,7 +275,7 @@ def scatter(packets, seed):
             np.array(pkt, dtype=np.uint32))
 
 
-@pytest.mark.parametrize("plan", [0, 1, 2, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("plan", [0, 1, 2, 5, 6, 7, 8, 9, 12, 13])
 def test_scattered_and_aliased_chunks(torch, plan):
     """Chunks out of memory order, with gaps, partly inside chunk 0's staged
     window and partly outside, and repeated chunks: the staged reads of later

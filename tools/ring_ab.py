@@ -50,6 +50,11 @@ def main():
              "pol": abi.TUNE_CACHE_POLICY}
     variants = {
         "pipe2": None,
+        "pipe1": None,
+        "ring_G1": {"G": 1},
+        "ring_G1_o8": {"G": 1, "outs": 8},
+        "ring_o8": {"outs": 8},
+        "pipe1_o64": None,
         "ring": {},
         "ring_g1": {"grid": 1},
         "ring_g3": {"grid": 3},
@@ -65,15 +70,20 @@ def main():
         variants = {k: v for k, v in variants.items() if k in keep}
 
     def set_knobs(kv):
+        kv = {k: v for k, v in (kv or {}).items() if k in knobs}
         for k, key in knobs.items():
             ctx.set_tuning(key, (kv or {}).get(k, 0))
 
     def runner(name):
         if variants[name] is None:
-            return bench.Runner(torch, lib, ctx, Chain.UdpParser, n, stride, arenas, None, None,
-                                outs[:reps], streams[:2], 16)
-        return bench.RingRunner(torch, lib, ctx, Chain.UdpParser, n, stride, arenas, outs,
-                                streams[0], 16, G)
+            ns = 1 if name.startswith("pipe1") else 2
+            o = outs if name.endswith("_o64") else outs[:reps]
+            a = arenas * (len(o) // reps)  # same arena rotation, one record buffer per step
+            return bench.Runner(torch, lib, ctx, Chain.UdpParser, n, stride, a, None, None,
+                                o, streams[:ns], 16)
+        kv = variants[name]
+        return bench.RingRunner(torch, lib, ctx, Chain.UdpParser, n, stride, arenas,
+                                outs[:kv.get("outs", 64)], streams[0], 16, kv.get("G", G))
 
     runners = {k: runner(k) for k in variants}
     res = {k: [] for k in variants}
