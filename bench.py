@@ -326,37 +326,98 @@ def ring_group(steps: int, cap: int = 64) -> int:
     return max(d for d in range(1, min(cap, steps) + 1) if steps % d == 0)
 
 
+class HalfOffsetRunner:
+    """Per-batch launches over two streams without a stagger wait: stream 0
+    parses batches 0, 2, 4, ...; stream 1 opens with the first half of batch
+    1, parses 3, 5, ..., and closes with batch 1's second half.  Both streams
+    start at once yet run half a launch apart (stream 1's first kernel is half
+    as long), and both end together (each carries 10 batches of a 20-step
+    region) — no stretch where one stream runs alone, which the staggered
+    start pays at both ends of the region.  Every step is still one batch's
+    full pass (batch 1's as two half launches); batch k reads arena k % R and
+    writes record buffer k % R."""
+
+    def __init__(self, torch, lib, ctx, chain, n, stride, arenas, outs, streams, record_bytes):
+        self.torch, self.streams = torch, list(streams[:2])
+        assert len(self.streams) == 2
+        self.reps = len(arenas)
+        h, c = ctx._h, int(chain)
+        fn = lib.ingot_gpu_parse_strided if record_bytes == 16 else \
+            lib.ingot_gpu_parse_strided_compact
+        aptrs = [a.data_ptr() for a in arenas]
+        optrs = [o.data_ptr() for o in outs]
+        sps = [st.cuda_stream for st in self.streams]
+        half = n // 2
+        self._go = lambda s, b, lo, cnt: fn(h, aptrs[b % self.reps] + lo * stride, stride, None,
+                                             cnt, c, optrs[b % self.reps] + lo * record_bytes,
+                                             sps[s])
+        self.n, self.half = n, half
+
+    def plan(self, steps):
+        """[(stream, batch, first frame, frames)] in enqueue order."""
+        if steps < 2:
+            return [(0, b, 0, self.n) for b in range(steps)]
+        even = list(range(0, steps, 2))
+        odd = list(range(3, steps, 2))
+        s1 = [(1, 1, 0, self.half)] + [(1, b, 0, self.n) for b in odd] + \
+            [(1, 1, self.half, self.n - self.half)]
+        s0 = [(0, b, 0, self.n) for b in even]
+        out = []
+        for i in range(max(len(s0), len(s1))):
+            if i < len(s1):
+                out.append(s1[i])
+            if i < len(s0):
+                out.append(s0[i])
+        return out
+
+    def run(self, steps, gate=None):
+        pl = self.plan(steps)
+        return _timed(self.torch, self.streams, lambda i: self._go(*pl[i]), len(pl), gate=gate)
+
+
 class RingRunner:
     """The persistent ring consumer (ingot_gpu_parse_ring): steps k .. k+G-1
-    are one launch of G batches, batch k reading arena k % R and writing its
-    own record buffer k % len(outs) (every batch's records are stored inside
-    the region).  One stream; launches back to back."""
+    are one launch per stream, stream s taking batches k+s, k+s+S, ... of the
+    group; batch k reads arena k % R and writes its own record buffer
+    k % len(outs) (every batch's records are stored inside the region)."""
 
-    def __init__(self, torch, lib, ctx, chain, n, stride, arenas, outs, stream, record_bytes,
+    def __init__(self, torch, lib, ctx, chain, n, stride, arenas, outs, streams, record_bytes,
                  group):
         import ctypes
 
         import ingot_amd
 
-        self.torch, self.streams, self.group = torch, [stream], group
+        if not isinstance(streams, (list, tuple)):
+            streams = [streams]
+        self.torch, self.streams, self.group = torch, list(streams), group
         reps, nout = len(arenas), len(outs)
-        h, c, sp = ctx._h, int(chain), stream.cuda_stream
+        h, c = ctx._h, int(chain)
+        sps = [st.cuda_stream for st in self.streams]
+        S = len(sps)
         aptrs = [a.data_ptr() for a in arenas]
         optrs = [o.data_ptr() for o in outs]
         tables = {}
 
-        def table(k, m):
-            key = (k % (reps * nout), m)
+        def table(first, m):
+            """batches first, first+S, ... below the group's end"""
+            key = (first % (reps * nout), m)
             if key not in tables:
                 t = (ingot_amd.RingBatch * m)()
                 for j in range(m):
-                    t[j].d_arena, t[j].d_out = aptrs[(k + j) % reps], optrs[(k + j) % nout]
+                    b = first + j * S
+                    t[j].d_arena, t[j].d_out = aptrs[b % reps], optrs[b % nout]
                 tables[key] = t
             return tables[key]
 
         def launch(k, m=1):
-            return lib.ingot_gpu_parse_ring(h, ctypes.cast(table(k, m), ctypes.c_void_p), m,
-                                            stride, n, c, record_bytes, None, 0, 0, None, sp)
+            for s in range(min(S, m)):
+                cnt = len(range(s, m, S))
+                rc = lib.ingot_gpu_parse_ring(h, ctypes.cast(table(k + s, cnt), ctypes.c_void_p),
+                                              cnt, stride, n, c, record_bytes, None, 0, 0, None,
+                                              sps[s])
+                if rc:
+                    return rc
+            return 0
 
         self.launch = launch
 
@@ -789,11 +850,12 @@ def main():
     ap.add_argument("--streams", type=int, default=0,
                     help="streams the steps alternate over (0 = the config's measured best)")
     ap.add_argument("--record", type=int, default=16, choices=(16, 8))
-    ap.add_argument("--timing", default="auto", choices=("auto", "ring", "launches"),
-                    help="ring: the persistent ring consumer (ingot_gpu_parse_ring, one launch "
-                         "per group of up to 64 batches); launches: one launch per batch over "
-                         "the config's streams; auto: ring where the ring kernel serves the "
-                         "config (fixed slots, no length array: c2)")
+    ap.add_argument("--timing", default="launches", choices=("ring", "launches"),
+                    help="launches (default): one launch per batch over the config's streams "
+                         "(c2: 2 streams, the second started 6 us late); ring: the persistent "
+                         "ring consumer (ingot_gpu_parse_ring), one launch per group of up to 64 "
+                         "batches — measured slower on C2 (DESIGN.md §5: one long-lived launch "
+                         "sustains ~5.5 TB/s, two overlapped per-batch launches ~7 TB/s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true")
     ap.add_argument("--no-host-path", action="store_true",
@@ -868,7 +930,7 @@ def main():
     # timed by the same rules, with its own roofline and CPU baseline.
     if args.config == "c2" and not args.no_sublines and not args.tune:
         sub = argparse.Namespace(**vars(args))
-        sub.config, sub.streams, sub.record, sub.timing = "c3", STREAMS["c3"], 16, "auto"
+        sub.config, sub.streams, sub.record, sub.timing = "c3", STREAMS["c3"], 16, "launches"
         sub.no_variants, sub.no_host_path = True, True
         sub.stagger_us = None
         r3 = run_config(sub, "c3", env)
@@ -896,7 +958,7 @@ def run_config(args, config, env):
     # (the ring kernel's layout), 16- or 8-B records, not the tunnel chain
     ring_ok = (mode == "parse" and stride is not None and stride >= 64 and prof_name == "V4UDP64"
                and chain != Chain.GeneveOverV6Tunnel)
-    use_ring = args.timing == "ring" or (args.timing == "auto" and ring_ok)
+    use_ring = args.timing == "ring"
     if use_ring and not ring_ok:
         raise SystemExit(f"--timing ring: {config} is not a slot ring without lengths")
     streams_n = 1 if use_ring else args.streams
@@ -1095,6 +1157,8 @@ def run_config(args, config, env):
     if not no_variants:
         vsteps = min(args.steps, 1000)
         combos = [(1, 16), (2, 8), (1, 8), (4, 16)]
+        if ring_ok and not use_ring:  # the persistent ring consumer over the same batches
+            combos += [("ring", 16)]
         if use_ring:  # the per-batch launches the ring replaces, and 8-B ring records
             combos = [(2, 16), (1, 16), (2, 8), ("ring", 8)]
         for ns, rb in combos:
@@ -1105,9 +1169,12 @@ def run_config(args, config, env):
             if rb == 8 and (chain == Chain.GeneveOverV6Tunnel or mode != "parse"):
                 continue
             if ns == "ring":
-                if outs8 is None:
+                if rb == 8 and outs8 is None:
                     outs8 = [torch.empty((n, 8), dtype=torch.uint8, device=dev)
                              for _ in range(max(G, reps))]
+                if rb == 16 and ring_outs is None:
+                    ring_outs = outs + [torch.empty((n, 16), dtype=torch.uint8, device=dev)
+                                        for _ in range(max(0, G - reps))]
                 r = runner(1, rb, ring=True)
                 r.warm(min(args.warmup, 50), gate)
                 name = f"ring_rec{rb}"

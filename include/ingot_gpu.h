@@ -519,6 +519,10 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              CU (1..8; 0 = measured default).  The ring's
  *                              tiles in flight per wave follow
  *                              INGOT_TUNE_PIPE_DEPTH
+ *   INGOT_TUNE_RING_GROUPS     ingot_gpu_parse_ring: batches in flight at
+ *                              once (1, 2 or 4; 0 = measured default): the
+ *                              grid is cut into that many block groups, group
+ *                              q consuming batches q, q+G, ...
  */
 #define INGOT_TUNE_WINDOW_INDEXED 1
 #define INGOT_TUNE_WINDOW_STRIDED 2
@@ -532,6 +536,7 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
 #define INGOT_TUNE_READ_PLAN 10
 #define INGOT_TUNE_FLOW_KERNEL 11
 #define INGOT_TUNE_RING_GRID 12
+#define INGOT_TUNE_RING_GROUPS 13
 int ingot_gpu_ctx_set_tuning(ingot_gpu_ctx* ctx, int key, int value);
 int ingot_gpu_ctx_get_tuning(const ingot_gpu_ctx* ctx, int key);
 

@@ -82,6 +82,7 @@ TUNE_SLOW_PATH = 9
 TUNE_READ_PLAN = 10
 TUNE_FLOW_KERNEL = 11
 TUNE_RING_GRID = 12
+TUNE_RING_GROUPS = 13
 
 
 class IngotRec(ctypes.Structure):

@@ -100,6 +100,7 @@ struct RingArgs {
     uint32_t tiles_per_batch;
     uint64_t timeout_ticks;   // wall-clock ticks a wave waits for a batch
     uint32_t* status;         // optional: |= 1 when a wave gave up waiting
+    uint32_t groups = 1;      // batch groups in flight at once (launch_ring)
     RingBatch b[INGOT_RING_MAX_BATCHES];
 };
 static_assert(sizeof(RingArgs) <= 4096, "RingArgs exceeds the 4 KiB kernel-argument limit");
@@ -149,6 +150,7 @@ struct Tuning {
     int flow_kernel = 0;   // flows: 0 = k_parse (16-bit table: one tile per wave), 1 = hash
                            // overlapped with the next tile (k_flows), 2 = k_parse persistent
     int ring_grid = 0;     // ring consumer: blocks per CU (0 = measured default)
+    int ring_groups = 0;   // ring consumer: batches in flight at once (0 = measured default)
     uint32_t cus = 256;  // compute units of the context's device (grid shaping)
     bool host_arena = false;  // per call: the arena is host memory (ingot_gpu_host_map)
 };

@@ -57,9 +57,16 @@ __global__ __launch_bounds__(BLOCK) void k_parse_pipe(ParseArgs a) {
         const uint64_t tn = t + (DEPTH - 1u) * step;
         if (tn < ntiles) {
             stage(tn, img0 + ((j + DEPTH - 1u) % DEPTH) * IMG_DW);
-            // everything but the youngest DEPTH-1 tiles' loads has landed
-            // (record stores count too, so this is conservative)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DEPTH - 1u) * NCH) : "memory");
+            // tile j's loads have landed (vector-memory ops retire in issue
+            // order, stores and LDS-DMA alike): younger than them are the
+            // DEPTH-1 later tiles' loads and, once the pipeline is full, the
+            // DEPTH-1 record stores of the tiles before j — which need not
+            // have completed (counting them out left every tile waiting for
+            // the previous record's write-through)
+            if (j + 1u >= DEPTH)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DEPTH - 1u) * (NCH + 1u)) : "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DEPTH - 1u) * NCH) : "memory");
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -104,9 +111,18 @@ __global__ __launch_bounds__(BLOCK) void k_parse_ring(RingArgs a) {
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
     uint32_t* img0 = s_img + wave * WAVE_DW;
     const uint32_t tpb = a.tiles_per_batch;
-    const uint32_t W = gridDim.x * WAVES;
-    const uint32_t total = tpb * a.nbatches;  // < 2^32 (api.cpp)
-    const uint32_t g0 = blockIdx.x * WAVES + wave;
+    // Batch groups (RingArgs::groups = G): the grid is cut into G groups of
+    // blocks (8 consecutive blocks, one per XCD, per group in turn), group q
+    // consuming batches q, q+G, q+2G, ... — G batches in flight at once, as G
+    // streams of per-batch launches would have (launch_ring: G divides the
+    // grid into whole 8-block rows).
+    const uint32_t G = a.groups;
+    const uint32_t grp = (blockIdx.x / 8u) % G;
+    const uint32_t gblk = (blockIdx.x / (8u * G)) * 8u + blockIdx.x % 8u;
+    const uint32_t W = (gridDim.x / G) * WAVES;  // waves of the group
+    const uint32_t nbg = (a.nbatches - grp + G - 1u) / G;
+    const uint32_t total = tpb * nbg;  // the group's tiles (< 2^32, api.cpp)
+    const uint32_t g0 = gblk * WAVES + wave;
     if (g0 >= total) return;
     const uint32_t J = (total - g0 + W - 1u) / W;  // this wave's tiles
     // the fields the loop uses, held in SGPRs: left as kernel-argument
@@ -163,13 +179,12 @@ __global__ __launch_bounds__(BLOCK) void k_parse_ring(RingArgs a) {
         if (c.t >= tpb) {
             do {
                 c.t -= tpb;
-                ++c.b;
+                c.b += G;
             } while (c.t >= tpb);
             setb(c);
         }
     };
-    Cur sc{g0 / tpb, 0u, nullptr, nullptr};
-    sc.t = g0 - sc.b * tpb;
+    Cur sc{grp + (g0 / tpb) * G, g0 % tpb, nullptr, nullptr};
     setb(sc);
     Cur pc = sc;
     auto stage = [&](const Cur& c, uint32_t* img) {
@@ -212,12 +227,17 @@ __global__ __launch_bounds__(BLOCK) void k_parse_ring(RingArgs a) {
 #pragma unroll
     for (uint32_t d = 0; d + 1u < DEPTH; ++d) issue(js);
     for (uint32_t j = 0; j < js; ++j) {
-        // tile j's loads have landed: only the DEPTH-1 younger tiles' loads
-        // may still be in flight (record stores count too: conservative)
-        if (issue(js) && js - j == DEPTH)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DEPTH - 1u) * NCH) : "memory");
-        else
+        // tile j's loads have landed: younger than them are the DEPTH-1 later
+        // tiles' loads and (pipeline full) the DEPTH-1 earlier tiles' record
+        // stores, which may still be in flight (k_parse_pipe)
+        if (issue(js) && js - j == DEPTH) {
+            if (j + 1u >= DEPTH)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DEPTH - 1u) * (NCH + 1u)) : "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DEPTH - 1u) * NCH) : "memory");
+        } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         // the image is restaged only after every lane's reads of it have
         // returned: the record store consumes them (as in k_parse_pipe)
         parse(pc, img0 + (j % DEPTH) * IMG_DW);
@@ -476,6 +496,9 @@ hipError_t launch_ring(const RingArgs& args, int chain, int mode, const Tuning& 
     uint64_t blocks = (total + WAVES - 1) / WAVES;
     if (blocks > bpc * t.cus) blocks = bpc * t.cus;
     const uint32_t g = (uint32_t)(blocks ? blocks : 1);
+    // batch groups only on a grid of whole 8-block rows per group
+    a.groups = t.ring_groups > 1 ? (uint32_t)t.ring_groups : 1u;
+    if (g % (8u * a.groups) != 0 || a.groups > a.nbatches) a.groups = 1;
     const bool r8 = mode == OUT_REC8;
     switch (t.pipe_depth) {
     case 3: return r8 ? launch_ring_chain<3, OUT_REC8>(a, chain, g, s)

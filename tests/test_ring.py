@@ -17,7 +17,7 @@ import pytest
 import ingot_amd
 import oracle
 from ingot_amd import Chain, GenProfile
-from ingot_amd.abi import TUNE_CACHE_POLICY, TUNE_PIPE_DEPTH, TUNE_RING_GRID
+from ingot_amd.abi import TUNE_CACHE_POLICY, TUNE_PIPE_DEPTH, TUNE_RING_GRID, TUNE_RING_GROUPS
 
 pytestmark = pytest.mark.gpu
 
@@ -40,13 +40,15 @@ def _want(arena, chain, stride, n):
                               nthreads=8)
 
 
-@pytest.mark.parametrize("grid,depth,pol", [(0, 0, 0), (1, 0, 0), (4, 0, 0), (8, 0, 0),
-                                            (0, 3, 0), (0, 4, 0), (2, 3, 1), (0, 0, 4),
-                                            (0, 0, 3), (3, 4, 75)])
+@pytest.mark.parametrize("grid,depth,pol,groups", [
+    (0, 0, 0, 0), (1, 0, 0, 0), (4, 0, 0, 0), (8, 0, 0, 0), (0, 3, 0, 0), (0, 4, 0, 0),
+    (2, 3, 1, 0), (0, 0, 4, 0), (0, 0, 3, 0), (3, 4, 75, 0), (0, 0, 0, 2), (4, 0, 0, 4),
+    (3, 3, 0, 2), (1, 0, 0, 4)])
 @pytest.mark.parametrize("n", [1, 63, 65, 4097, 100_003])
-def test_ring_bit_exact(torch, grid, depth, pol, n):
+def test_ring_bit_exact(torch, grid, depth, pol, groups, n):
     ctx = ingot_amd.Context(0)
     ctx.set_tuning(TUNE_RING_GRID, grid)
+    ctx.set_tuning(TUNE_RING_GROUPS, groups)
     ctx.set_tuning(TUNE_PIPE_DEPTH, depth)
     ctx.set_tuning(TUNE_CACHE_POLICY, pol)
     for prof, stride, k in ((GenProfile.V4UDP64, 64, 5), (GenProfile.ADVERSARIAL, 64, 3),
