@@ -173,11 +173,13 @@ def test_protocol_constants_and_eh_classes_match_reference():
     r6564_src = cls.split("FragmentHeader),", 1)[1]
     r6564 = {pp[n] for n in re.findall(r"Self::(\w+)", r6564_src)}
     assert frag == {44} and 0 in r6564 and len(r6564) == 8
-    kernel = (LAYOUTS.parent / "parse.hip").read_text()
-    body = re.search(r"uint32_t eh_class\(uint32_t h\) \{(.*?)\n\}", kernel, re.S).group(1)
-    k_frag = {int(x) for x in re.findall(r"h == (\d+)u\) return EH_FRAGMENT", body)}
-    k_6564 = {int(x) for x in re.findall(r"h == (\d+)u", body)} - k_frag
-    assert k_frag == frag and k_6564 == r6564
+    # the chain walk (walk.h) and the single-header parsers (header.hip)
+    for src in ("walk.h", "header.hip"):
+        kernel = (LAYOUTS.parent / src).read_text()
+        body = re.search(r"uint32_t eh_class\(uint32_t h\) \{(.*?)\n\}", kernel, re.S).group(1)
+        k_frag = {int(x) for x in re.findall(r"h == (\d+)u\) return EH_FRAGMENT", body)}
+        k_6564 = {int(x) for x in re.findall(r"h == (\d+)u", body)} - k_frag
+        assert k_frag == frag and k_6564 == r6564, src
     for p in range(256):
         want = 1 if p in frag else 2 if p in r6564 else 0
         assert oracle.v6eh_class(p) == want, p
