@@ -12,9 +12,14 @@ namespace {
 // each wave walks several tiles and keeps the next DEPTH-1 tiles' LDS-DMA in
 // flight while it parses the current one (DEPTH LDS images per wave, used
 // round robin).  Requires stride >= 16*NCH.
-template <uint32_t NCH, uint32_t DEPTH, int CHAIN, int MODE>
+// POL != 0: the cache-policy word fixed at compile time (the launcher's
+// defaults), so the staging loads and record stores carry their cache bits
+// directly instead of the runtime policy switch around every instruction
+// (a tree of scalar branches per chunk); 0 = a.policy at run time.
+template <uint32_t NCH, uint32_t DEPTH, int CHAIN, int MODE, uint32_t POL = 0>
 __global__ __launch_bounds__(BLOCK) void k_parse_pipe(ParseArgs a) {
     constexpr uint32_t WIN = NCH * 16u;
+    const uint32_t pol = POL ? POL : a.policy;
     constexpr uint32_t WAVE_DW = WAVE * NCH * 4u;
     constexpr uint32_t IMG_DW = WAVES * WAVE_DW + 16u;
     __shared__ __attribute__((aligned(16))) uint32_t s_img[DEPTH * IMG_DW];
@@ -33,7 +38,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse_pipe(ParseArgs a) {
             const uint32_t c = (q - pp * NCH) ^ swz<NCH>(pp);
             uint64_t slot = tt * WAVE + pp;
             if (slot >= a.n) slot = a.n - 1u;  // a valid address for the tail tile
-            stage16p(a.arena + slot * a.stride + 16u * c, img + k * WAVE * 4u, a.policy);
+            stage16p(a.arena + slot * a.stride + 16u * c, img + k * WAVE * 4u, pol);
         }
     };
     auto parse = [&](uint64_t tt, const uint32_t* img) {
@@ -42,8 +47,8 @@ __global__ __launch_bounds__(BLOCK) void k_parse_pipe(ParseArgs a) {
         Rec r;
         walk<CHAIN, false>(fr, r, nullptr, nullptr);
         if (i < a.n) {
-            if constexpr (MODE == OUT_REC8) store_rec(static_cast<uint2*>(a.out) + i, pack8(r), a.policy);
-            else store_rec(static_cast<uint4*>(a.out) + i, pack(r), a.policy);
+            if constexpr (MODE == OUT_REC8) store_rec(static_cast<uint2*>(a.out) + i, pack8(r), pol);
+            else store_rec(static_cast<uint4*>(a.out) + i, pack(r), pol);
         }
     };
 
@@ -382,20 +387,20 @@ hipError_t launch_modify_pipe(const ModifyArgs& a, int chain, uint32_t grid, hip
     return hipGetLastError();
 }
 
-template <uint32_t NCH, uint32_t DEPTH, int MODE>
+template <uint32_t NCH, uint32_t DEPTH, int MODE, uint32_t POL = 0>
 hipError_t launch_pipe(const ParseArgs& a, int chain, uint32_t grid, hipStream_t s) {
     switch (chain) {
     case INGOT_CHAIN_UDP_PARSER:
-        hipLaunchKernelGGL((k_parse_pipe<NCH, DEPTH, INGOT_CHAIN_UDP_PARSER, MODE>), dim3(grid),
-                           dim3(BLOCK), 0, s, a);
+        hipLaunchKernelGGL((k_parse_pipe<NCH, DEPTH, INGOT_CHAIN_UDP_PARSER, MODE, POL>),
+                           dim3(grid), dim3(BLOCK), 0, s, a);
         break;
     case INGOT_CHAIN_GENERIC_ULP:
-        hipLaunchKernelGGL((k_parse_pipe<NCH, DEPTH, INGOT_CHAIN_GENERIC_ULP, MODE>), dim3(grid),
-                           dim3(BLOCK), 0, s, a);
+        hipLaunchKernelGGL((k_parse_pipe<NCH, DEPTH, INGOT_CHAIN_GENERIC_ULP, MODE, POL>),
+                           dim3(grid), dim3(BLOCK), 0, s, a);
         break;
     case INGOT_CHAIN_VLAN_ULP:
-        hipLaunchKernelGGL((k_parse_pipe<NCH, DEPTH, INGOT_CHAIN_VLAN_ULP, MODE>), dim3(grid),
-                           dim3(BLOCK), 0, s, a);
+        hipLaunchKernelGGL((k_parse_pipe<NCH, DEPTH, INGOT_CHAIN_VLAN_ULP, MODE, POL>),
+                           dim3(grid), dim3(BLOCK), 0, s, a);
         break;
     default:
         return hipErrorInvalidValue;
@@ -434,6 +439,10 @@ hipError_t launch_slot_ring(const ParseArgs& a, int chain, int mode, const Tunin
     if (t.pipe_depth == 4)
         return mode == OUT_REC8 ? launch_pipe<4, 4, OUT_REC8>(a, chain, pg, s)
                                 : launch_pipe<4, 4, OUT_REC16>(a, chain, pg, s);
+    // the default policies (launch_parse: 16-B records 11, 8-B records 3)
+    // with their cache bits compiled in
+    if (mode == OUT_REC16 && a.policy == 11u) return launch_pipe<4, 2, OUT_REC16, 11u>(a, chain, pg, s);
+    if (mode == OUT_REC8 && a.policy == 3u) return launch_pipe<4, 2, OUT_REC8, 3u>(a, chain, pg, s);
     return mode == OUT_REC8 ? launch_pipe<4, 2, OUT_REC8>(a, chain, pg, s)
                             : launch_pipe<4, 2, OUT_REC16>(a, chain, pg, s);
 }
