@@ -514,7 +514,9 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              table, a persistent grid with the 32-bit one);
  *                              1 = the next tile's staging issued before the
  *                              hash of this one (persistent); 2 = the default
- *                              kernel on a persistent grid
+ *                              kernel on a persistent grid; 3 = the default
+ *                              kernel with the address block's source (LDS
+ *                              window or L2) chosen per lane, not per wave
  *   INGOT_TUNE_RING_GRID       ingot_gpu_parse_ring: 256-thread blocks per
  *                              CU (1..8; 0 = measured default).  The ring's
  *                              tiles in flight per wave follow

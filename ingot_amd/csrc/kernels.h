@@ -57,6 +57,7 @@ struct FlowArgs {
     ParseArgs p;
     uint32_t* flow;  // per-packet bin or INGOT_FLOW_NONE
     uint32_t bin_mask;
+    uint32_t addr_lanes;  // 1: address block read per lane (INGOT_TUNE_FLOW_KERNEL 3)
     uint32_t* hash;  // optional
     uint32_t w[FLOW_INPUT_BITS];
     alignas(16) uint32_t tab16[FLOW_TAB16_DW];  // entry (p, v) at half-word 16p + v

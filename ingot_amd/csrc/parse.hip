@@ -226,7 +226,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
         } else if constexpr (FLOWS) {
             walk<CHAIN, false>(fr, r, nullptr, nullptr);
             uint32_t h;
-            const bool counted = valid && flow_hash<H16>(fr, r, s_tab, h);
+            const bool counted = valid && flow_hash<H16>(fr, r, s_tab, h, args.addr_lanes != 0u);
             if (valid) {
                 args.flow[i] = counted ? (h & args.bin_mask) : INGOT_FLOW_NONE;
                 if (args.hash) args.hash[i] = h;
@@ -576,7 +576,8 @@ hipError_t launch_flows_mode(const FlowArgs& a, int layout_kind, int chain, cons
     // built per block (1,152 entries from the key windows), so its grid is
     // persistent; INGOT_TUNE_FLOW_KERNEL = 2 makes the 16-bit one persistent
     // too.  Fixed max_blocks: grid-stride over that many blocks.
-    const uint32_t pc = t.max_blocks || (H16 && t.flow_kernel == 0) ? 0u : t.cus;
+    const uint32_t pc =
+        t.max_blocks || (H16 && (t.flow_kernel == 0 || t.flow_kernel == 3)) ? 0u : t.cus;
     // INGOT_TUNE_FLOW_KERNEL = 1: the hash-overlapped kernel (k_flows) at the
     // default windows.  Measured on C5 (tools/abtune.py, us per step incl.
     // the histogram): 360.7 vs 363.6 on one stream, 350.2 vs
@@ -620,9 +621,11 @@ hipError_t launch_flows_mode(const FlowArgs& a, int layout_kind, int chain, cons
     }
 }
 
-hipError_t launch_flows(const FlowArgs& a, int layout_kind, int chain, const Tuning& t,
+hipError_t launch_flows(const FlowArgs& args, int layout_kind, int chain, const Tuning& t,
                         hipStream_t s) {
-    if (a.p.n == 0) return hipSuccess;
+    if (args.p.n == 0) return hipSuccess;
+    FlowArgs a = args;
+    a.addr_lanes = t.flow_kernel == 3 ? 1u : 0u;
     // With a table built per block, the grid is persistent: exactly the
     // blocks the device holds at once (resident_per_cu, per kernel instance),
     // each wave walking tiles.  Measured on C5 (round 1, 32-bit table built
@@ -670,7 +673,7 @@ bool tuning_valid(int key, int value) {
     case INGOT_TUNE_READ_PLAN:
         return (value >= 0 && value <= 14);
     case INGOT_TUNE_FLOW_KERNEL:
-        return value >= 0 && value <= 2;
+        return value >= 0 && value <= 3;
     default:
         return false;
     }

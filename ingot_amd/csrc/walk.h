@@ -1020,8 +1020,14 @@ struct FlowWords {
 // holding it from L2 — instead of a bounds check, two reads and a wait (or 4
 // byte loads) per word.  The port word: LDS, or aligned dwords past the
 // window (IPv6 EH chains).
+// lanes (INGOT_TUNE_FLOW_KERNEL 3): the path is chosen per lane — a lane
+// whose block lies past its window reads it from L2 while the others read
+// LDS (a split wave runs both paths, each under its lanes' mask) — so that a
+// window ending before some lanes' IPv6 addresses does not send every lane
+// of the wave to L2.
 template <class FR>
-__device__ __forceinline__ bool flow_words(const FR& f, const Rec& r, FlowWords& x) {
+__device__ __forceinline__ bool flow_words(const FR& f, const Rec& r, FlowWords& x,
+                                           bool lanes = false) {
 #pragma unroll
     for (uint32_t k = 0; k < 9; ++k) x.w[k] = 0;
     if (r.status != INGOT_OK || r.l3_kind == INGOT_L3_NONE) return false;
@@ -1032,7 +1038,8 @@ __device__ __forceinline__ bool flow_words(const FR& f, const Rec& r, FlowWords&
     const uint32_t naddr = v6 ? 8u : 2u;                            // address words
     uint32_t w[8];
     // one path per wave: a wave split between the two runs both
-    if (__all(a + 4u * naddr <= f.avail)) f.template be_words<8>(a, w);
+    const bool in = a + 4u * naddr <= f.avail;
+    if (lanes ? in : __all(in)) f.template be_words<8>(a, w);
     else f.be_words_global8(a, naddr, w);
 #pragma unroll
     for (uint32_t k = 0; k < 9; ++k) {
@@ -1105,9 +1112,9 @@ __device__ __forceinline__ uint32_t toeplitz9_16(const FlowWords& x, const uint3
 
 template <bool H16, class FR>
 __device__ __forceinline__ bool flow_hash(const FR& f, const Rec& r, const uint32_t* tab,
-                                          uint32_t& h) {
+                                          uint32_t& h, bool lanes = false) {
     FlowWords x;
-    const bool ok = flow_words(f, r, x);
+    const bool ok = flow_words(f, r, x, lanes);
     if constexpr (H16) h = ok ? toeplitz9_16(x, tab) : 0u;
     else h = ok ? toeplitz9(x, tab) : 0u;
     return ok;

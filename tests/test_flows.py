@@ -119,7 +119,8 @@ def test_flow_hist_bit_exact(profile, chain, stride):
                                   {"fk": 1, "blocks": 3}, {"fk": 2}, {"fk": 2, "win": 4},
                                   {"fk": 2, "blocks": 3}, {"win": 25}, {"win": 26}, {"win": 28},
                                   {"fk": 2, "win": 25}, {"win": 25, "blocks": 3}, {"win": 1045},
-                                  {"win": 1058}])
+                                  {"win": 1058}, {"fk": 3}, {"fk": 3, "win": 1025},
+                                  {"fk": 3, "win": 1035}, {"fk": 3, "win": 3}])
 @pytest.mark.parametrize("profile,chain,stride", [
     ("FLOWS", "VlanUlp", None), ("ADVERSARIAL", "GenericUlp", None),
     ("GENEVE_ADVERSARIAL", "GeneveOverV6Tunnel", None), ("VLAN_V6EH", "VlanUlp", 256),
@@ -164,7 +165,7 @@ def test_flow_kernels_every_setting(tune, profile, chain, stride):
 @pytest.mark.gpu
 @pytest.mark.parametrize("table", [0, 32])
 @pytest.mark.parametrize("tune", [{}, {"win": 3}, {"win": 4}, {"win": 8}, {"blocks": 5},
-                                  {"fk": 1}, {"fk": 2}, {"win": 25}])
+                                  {"fk": 1}, {"fk": 2}, {"win": 25}, {"fk": 3, "win": 1025}])
 @pytest.mark.parametrize("bins", [1 << 16, 1024])
 @pytest.mark.parametrize("profile,chain,stride", [
     ("FLOWS", "VlanUlp", None), ("ADVERSARIAL", "GenericUlp", None),
@@ -267,7 +268,7 @@ def test_flow_hist_many_slices():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fk", [0, 1, 2])
+@pytest.mark.parametrize("fk", [0, 1, 2, 3])
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 4097, 262_145])
 def test_flow_ids_ragged_batches(n, fk):
     """Ragged batch sizes on every flows grid (one tile per wave, the
