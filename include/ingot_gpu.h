@@ -504,7 +504,11 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              5 = {3,0,0,0}, 6 = {2,0,0,0}, 7 / 8 / 10 =
  *                              line-completing 2-8 / 4-8 / 2-5; 9 = no descriptor
  *                              prefetch: chunk 0 staged, later chunks'
- *                              descriptors and bytes read on demand.  Chunk
+ *                              descriptors and bytes read on demand;
+ *                              12-14 = persistent grids with a descriptor
+ *                              lookahead; 15 / 16 = the default window with
+ *                              only chunk 1's / no later chunk's descriptor
+ *                              loaded up front (fewer VGPRs).  Chunk
  *                              pools in mapped host memory (ingot_gpu_host_map)
  *                              default to 1, and ingot_gpu_parse_read_dense
  *                              always stages {4,0,0,0} (the knob is ignored)

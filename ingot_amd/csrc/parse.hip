@@ -671,7 +671,7 @@ bool tuning_valid(int key, int value) {
     case INGOT_TUNE_SLOW_PATH:
         return value == 0 || value == 1;
     case INGOT_TUNE_READ_PLAN:
-        return (value >= 0 && value <= 14);
+        return (value >= 0 && value <= 16);
     case INGOT_TUNE_FLOW_KERNEL:
         return value >= 0 && value <= 3;
     default:

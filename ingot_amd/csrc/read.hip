@@ -20,10 +20,17 @@ namespace {
 // t + W's chunk-0 descriptor and tile t + 2W's chunk bounds are issued right
 // after tile t's staging: the staging and the lookahead loads are in flight
 // together and the wave waits for both (one round trip instead of three).
+//
+// NPRE (0..3): descriptors of chunks 1..NPRE loaded with chunk 0's (when not
+// the packet's last); later chunks are looked up when the walk reaches them.
+// Each prefetched descriptor holds 3 VGPRs through the walk: NPRE 3 is 68
+// VGPRs (7 waves per SIMD), NPRE 1 is 63 and NPRE 0 is 59 (8 waves).
 template <int CS0, int CS1, int CS2, int CS3, int CHAIN, int MODE, bool DENSE = false,
-          bool PIPE = false>
+          bool PIPE = false, int NPRE = 3>
 __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
-    using FR = SegFrameP<CS0, CS1, CS2, CS3, DENSE>;
+    using FR = SegFrameP<CS0, CS1, CS2, CS3, DENSE, NPRE>;
+    static_assert((CS1 == 0 || NPRE >= 1) && (CS2 == 0 || NPRE >= 2) && (CS3 == 0 || NPRE >= 3),
+                  "a chunk staged in planes needs its descriptor up front");
     constexpr uint32_t P = CS0 + CS1 + CS2 + CS3;
     constexpr uint32_t WAVE_DW = WAVE * P * 4u;
     constexpr bool TUN = CHAIN == INGOT_CHAIN_GENEVE_OVER_V6;
@@ -82,12 +89,12 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
             fr.l2 = (uint32_t)(v2 & 0xffffu);
             fr.l3 = (uint32_t)(v3 & 0xffffu);
         } else {
-            fr.o1 = nseg > 2 ? a.off[s0 + 1] : 0u;
-            fr.o2 = nseg > 3 ? a.off[s0 + 2] : 0u;
-            fr.o3 = nseg > 4 ? a.off[s0 + 3] : 0u;
-            fr.l1 = nseg > 2 ? a.len[s0 + 1] : 0u;
-            fr.l2 = nseg > 3 ? a.len[s0 + 2] : 0u;
-            fr.l3 = nseg > 4 ? a.len[s0 + 3] : 0u;
+            fr.o1 = NPRE >= 1 && nseg > 2 ? a.off[s0 + 1] : 0u;
+            fr.o2 = NPRE >= 2 && nseg > 3 ? a.off[s0 + 2] : 0u;
+            fr.o3 = NPRE >= 3 && nseg > 4 ? a.off[s0 + 3] : 0u;
+            fr.l1 = NPRE >= 1 && nseg > 2 ? a.len[s0 + 1] : 0u;
+            fr.l2 = NPRE >= 2 && nseg > 3 ? a.len[s0 + 2] : 0u;
+            fr.l3 = NPRE >= 3 && nseg > 4 ? a.len[s0 + 3] : 0u;
         }
         // chunk 0, packet-major: instruction k, lane L fills slot 64k + L =
         // packet q / CS0, piece (q mod CS0) ^ swz (16-B aligned absolute
@@ -114,9 +121,9 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
                 ext = end > ext ? end : ext;
             }
         };
-        widen(1, fr.o1, fr.l1);
-        widen(2, fr.o2, fr.l2);
-        widen(3, fr.o3, fr.l3);
+        if constexpr (NPRE >= 1) widen(1, fr.o1, fr.l1);
+        if constexpr (NPRE >= 2) widen(2, fr.o2, fr.l2);
+        if constexpr (NPRE >= 3) widen(3, fr.o3, fr.l3);
         const uint32_t n0 = (ext + 15u) >> 4;
 #pragma unroll
         for (uint32_t k = 0; k < (uint32_t)CS0; ++k) {
@@ -210,7 +217,8 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
 
 // persist_cus != 0 (the PIPE kernels): a persistent grid of the blocks the
 // device holds at once.
-template <int CS0, int CS1, int CS2, int CS3, int MODE, bool DENSE = false, bool PIPE = false>
+template <int CS0, int CS1, int CS2, int CS3, int MODE, bool DENSE = false, bool PIPE = false,
+          int NPRE = 3>
 hipError_t launch_read(const ParseArgs& a, int chain, uint32_t grid, hipStream_t s,
                        uint32_t persist_cus = 0) {
     auto go = [&](auto kernel) {
@@ -223,16 +231,16 @@ hipError_t launch_read(const ParseArgs& a, int chain, uint32_t grid, hipStream_t
     };
     switch (chain) {
     case INGOT_CHAIN_UDP_PARSER:
-        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_UDP_PARSER, MODE, DENSE, PIPE>);
+        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_UDP_PARSER, MODE, DENSE, PIPE, NPRE>);
         break;
     case INGOT_CHAIN_GENERIC_ULP:
-        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENERIC_ULP, MODE, DENSE, PIPE>);
+        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENERIC_ULP, MODE, DENSE, PIPE, NPRE>);
         break;
     case INGOT_CHAIN_VLAN_ULP:
-        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_VLAN_ULP, MODE, DENSE, PIPE>);
+        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_VLAN_ULP, MODE, DENSE, PIPE, NPRE>);
         break;
     default:
-        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENEVE_OVER_V6, MODE, DENSE, PIPE>);
+        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENEVE_OVER_V6, MODE, DENSE, PIPE, NPRE>);
         break;
     }
     return hipGetLastError();
@@ -297,6 +305,16 @@ hipError_t launch_segmented(const ParseArgs& a, int chain, int mode, const Tunin
         ParseArgs b = a;
         b.linewin = 2u;
         return launch_read<5, 0, 0, 0, OUT_REC16, false, true>(b, chain, g, s, t.cus);
+    }
+    // 15 / 16: the default window with only chunk 1's / no later descriptor
+    // prefetched (NPRE 1 / 0: 63 / 59 VGPRs, 8 waves per SIMD)
+    case 15:
+    case 16: {
+        ParseArgs b = a;
+        b.linewin = 3u;
+        return t.read_plan == 15
+                   ? launch_read<5, 0, 0, 0, OUT_REC16, false, false, 1>(b, chain, g, s)
+                   : launch_read<5, 0, 0, 0, OUT_REC16, false, false, 0>(b, chain, g, s);
     }
     default: {  // 11
         ParseArgs b = a;

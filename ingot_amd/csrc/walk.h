@@ -276,7 +276,7 @@ struct SegFrame : Frame<NCH> {
 // cut from one buffer, like the reference bench's one chunk per header) is
 // staged with chunk 0's pieces and read from there.
 // Offsets are logical as in SegFrame; `len` is the current chunk's end.
-template <int CS0, int CS1, int CS2, int CS3, bool DENSE = false>
+template <int CS0, int CS1, int CS2, int CS3, bool DENSE = false, int NPRE = 3>
 struct SegFrameP {
     static constexpr bool kRead = true;
     static constexpr bool kProbe = false;
@@ -348,12 +348,12 @@ struct SegFrameP {
     __device__ __forceinline__ void advance() {
         ++k;
         L = len;
-        // chunks 1..3 that are not the packet's last had their descriptors
-        // loaded with chunk 0's; the last chunk (the payload) and chunks past
-        // the fourth are looked up when the walk reaches them
-        if (k + 1 < nseg && k == 1) enter(o1, l1, pb(1), staged(1, nseg));
-        else if (k + 1 < nseg && k == 2) enter(o2, l2, pb(2), staged(2, nseg));
-        else if (k + 1 < nseg && k == 3) enter(o3, l3, pb(3), staged(3, nseg));
+        // chunks 1..NPRE that are not the packet's last had their
+        // descriptors loaded with chunk 0's; the last chunk (the payload) and
+        // the others are looked up when the walk reaches them
+        if (NPRE >= 1 && k + 1 < nseg && k == 1) enter(o1, l1, pb(1), staged(1, nseg));
+        else if (NPRE >= 2 && k + 1 < nseg && k == 2) enter(o2, l2, pb(2), staged(2, nseg));
+        else if (NPRE >= 3 && k + 1 < nseg && k == 3) enter(o3, l3, pb(3), staged(3, nseg));
         else if constexpr (DENSE) {
             const uint64_t v = seg_off[s0 + k];  // (offset << 16) | length
             enter(v >> 16, (uint32_t)(v & 0xffffu), 0u, 0u);

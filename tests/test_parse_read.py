@@ -163,7 +163,7 @@ def split_many(frames, seed):
     return out
 
 
-@pytest.mark.parametrize("plan", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
+@pytest.mark.parametrize("plan", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16])
 def test_every_read_plan_is_bit_exact(torch, plan):
     """INGOT_TUNE_READ_PLAN: how many 16-B pieces of each of the first four
     chunks are staged in LDS never changes a record, a field block or the
@@ -275,7 +275,7 @@ def scatter(packets, seed):
             np.array(pkt, dtype=np.uint32))
 
 
-@pytest.mark.parametrize("plan", [0, 1, 2, 5, 6, 7, 8, 9, 12, 13])
+@pytest.mark.parametrize("plan", [0, 1, 2, 5, 6, 7, 8, 9, 12, 13, 15, 16])
 def test_scattered_and_aliased_chunks(torch, plan):
     """Chunks out of memory order, with gaps, partly inside chunk 0's staged
     window and partly outside, and repeated chunks: the staged reads of later
