@@ -62,7 +62,10 @@ def main():
             prof_line = line
         rows = list(csv.DictReader(open(sp)))
         parse = [r for r in rows if "k_parse" in r["Name"] or "k_modify" in r["Name"]]
-        dom = max(parse, key=lambda r: int(r["Calls"]))
+        # the line names its kernel (and a C2 run's summary also holds the
+        # C3 sub-line's k_parse): match it; else the most-called parse kernel
+        named = [r for r in parse if r["Name"] == prof_line["roofline"].get("kernel")]
+        dom = named[0] if named else max(parse, key=lambda r: int(r["Calls"]))
         mean_us = float(dom["AverageNs"]) / 1e3
         for extra in EXTRA.get(cfg, ()):
             mean_us += sum(float(r["AverageNs"]) / 1e3 for r in rows if extra in r["Name"])
