@@ -288,7 +288,7 @@ def _cpu_model():
 
 
 class Runner:
-    """Launches step k (arena k % R -> records k % R) on stream k % S."""
+    """Launches step k (arena k % R -> records k % len(outs)) on stream k % S."""
 
     def __init__(self, torch, lib, ctx, chain, n, stride, arenas, off, lens, outs, streams,
                  record_bytes):
@@ -306,11 +306,11 @@ class Runner:
             fn = lib.ingot_gpu_parse_strided if record_bytes == 16 else \
                 lib.ingot_gpu_parse_strided_compact
             self.launch = lambda k: fn(h, aptrs[k % reps], stride, lptr, n, c,
-                                       outptrs[k % reps], sps[k % ns])
+                                       outptrs[k % len(outptrs)], sps[k % ns])
         else:
             fn = lib.ingot_gpu_parse if record_bytes == 16 else lib.ingot_gpu_parse_compact
             self.launch = lambda k: fn(h, aptrs[k % reps], optr, lptr, n, c,
-                                       outptrs[k % reps], sps[k % ns])
+                                       outptrs[k % len(outptrs)], sps[k % ns])
 
     def run(self, steps, gate=None):
         """Time `steps` launches (see _timed)."""
@@ -1190,6 +1190,23 @@ def run_config(args, config, env):
                 "hbm_GBps": round(bpl / (ms / vsteps / 1e3) / 1e9, 1),
                 "read_frac": round(rd / (ms / vsteps / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             }
+        if stride == 64 and mode == "parse" and not use_ring and args.record == 16:
+            # the headline schedule with 64 record buffers rotated (1 GiB):
+            # the default's R buffers (R x 16 MiB) fit the 256 MiB Infinity
+            # Cache, so their stores need not reach HBM inside the region;
+            # 1 GiB of them cannot stay there (tools/record_footprint.py)
+            outs64 = outs + [torch.empty((n, 16), dtype=torch.uint8, device=dev)
+                             for _ in range(max(0, 64 - len(outs)))]
+            r = Runner(torch, lib, ctx, chain, n, stride, arenas, off, lens, outs64,
+                       streams[:args.streams], 16)
+            r.run(min(args.warmup, 50), gate)
+            ms, _ = r.run(vsteps, gate)
+            variants[f"streams{args.streams}_rec16_records64"] = {
+                "value": round(n * vsteps / (ms / 1e3) / 1e6, 2),
+                "us_per_step": round(ms * 1e3 / vsteps, 3),
+                "read_frac": round(rd / (ms / vsteps / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                "record_buffers_rotated": len(outs64)}
+            del outs64, r
         if mode == "read":  # the same chunks as one dense 8-B entry each
             r = runner(args.streams, 16, dense=True)
             r.run(min(args.warmup, 50))
@@ -1269,6 +1286,7 @@ def run_config(args, config, env):
             "record_bytes": args.record,
             "streams": streams_n,
             "arena_copies_rotated": reps,
+            "record_buffers_rotated": (G if use_ring else reps),
             "parallelism": (f"{args.scaling} scaling, contiguous share per GPU x{world}" +
                             (f"; {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} "
                              f"all-reduce (sum) of the {FLOW_BINS} x u32 flow "
