@@ -34,7 +34,10 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
     constexpr uint32_t P = CS0 + CS1 + CS2 + CS3;
     constexpr uint32_t WAVE_DW = WAVE * P * 4u;
     constexpr bool TUN = CHAIN == INGOT_CHAIN_GENEVE_OVER_V6;
-    __shared__ __attribute__((aligned(16))) uint32_t s_win[WAVES * WAVE_DW + 16];
+    // no slack past the last image: SegFrameP::be clamps the second dword of
+    // a pair to the current chunk's staged pieces (a 5-piece image is then
+    // exactly 20 KiB per block)
+    __shared__ __attribute__((aligned(16))) uint32_t s_win[WAVES * WAVE_DW];
     const uint32_t lane = threadIdx.x & (WAVE - 1u);
     const uint32_t wave = threadIdx.x / WAVE;
     uint32_t* wimg = s_win + wave * WAVE_DW;

@@ -314,7 +314,12 @@ struct SegFrameP {
             const uint32_t b = sh + x0;
             const uint32_t a = b & ~3u;
             const uint32_t d0 = dw(a);
-            const uint32_t d1 = ((b & 3u) + n > 4u) ? dw(a + 4u) : 0u;
+            // the second dword only when the bytes straddle it (then it lies
+            // in the current chunk's staged pieces); clamped to them so that
+            // a speculated read stays inside this packet's slots / planes
+            const uint32_t lim = k == 0 || plane == kW0 ? 16u * CS0 : 16u * cs(k);
+            const uint32_t a1 = a + 4u < lim ? a + 4u : a;
+            const uint32_t d1 = ((b & 3u) + n > 4u) ? dw(a1) : 0u;
             return __builtin_bswap32(__builtin_amdgcn_alignbyte(d1, d0, b & 3u)) >> (32u - 8u * n);
         }
         uint32_t v = 0;
