@@ -104,7 +104,7 @@ def main():
         d_so = torch.from_numpy(seg_off).cuda()
         d_sl = torch.from_numpy(seg_len.view(np.int16)).cuda()
         d_ps = torch.from_numpy(pkt_seg.view(np.int32)).cuda()
-        for plan in (0, 1, 2, 3, 7, 8, 9, 10):
+        for plan in (0, 1, 2, 3, 7, 8, 9, 10, 15, 16):
             c2 = ingot_amd.Context(0)
             c2.set_tuning(TUNE_READ_PLAN, plan)
             r, ch = c2.parse_read(arena, d_so, d_sl, d_ps, chain)
@@ -132,6 +132,42 @@ def main():
         "flow_mismatches": int((flow.cpu().numpy().view(np.uint32) != w_flow).sum()),
         "flow16_mismatches": int((flow16.cpu().numpy().view(np.uint32) != w_flow).sum())}
     print("flows", res["flows/VlanUlp"], flush=True)
+    # round 3: flow bins with the address block read per lane (FLOW_KERNEL 3)
+    # at the 2-to-5-chunk window; the C2 ring kernel (64-B slots, no lengths:
+    # k_parse_pipe with its cache policy compiled in) over adversarial bytes,
+    # 16- and 8-B records
+    from ingot_amd.abi import TUNE_FLOW_KERNEL, TUNE_WINDOW_INDEXED
+
+    c3 = ingot_amd.Context(0)
+    c3.set_tuning(TUNE_FLOW_KERNEL, 3)
+    c3.set_tuning(TUNE_WINDOW_INDEXED, 1025)
+    f3 = c3.flow_hist(arena, off, lens, Chain.VlanUlp)
+    torch.cuda.synchronize()
+    res["flows/VlanUlp/lane_addr_1025"] = {
+        "flow_mismatches": int((f3.cpu().numpy().view(np.uint32) != w_flow).sum())}
+    print("flows fk3", res["flows/VlanUlp/lane_addr_1025"], flush=True)
+    del arena, off, lens
+    torch.cuda.empty_cache()
+    for chain in (Chain.UdpParser, Chain.GenericUlp, Chain.VlanUlp):
+        arena, _, _ = ingot_amd.gen_frames(GenProfile.ADVERSARIAL, n, seed=args.seed + 20 +
+                                           int(chain), stride=64)
+        w_rec = oracle.parse_batch(arena.cpu().numpy(), None, None, chain, stride=64, n=n,
+                                   nthreads=16)
+        g16 = ctx.parse_strided(arena, 64, n, chain)
+        g8 = ctx.parse_strided_compact(arena, 64, n, chain)
+        torch.cuda.synchronize()
+        bad16 = int((g16.cpu().numpy().reshape(n, -1) != w_rec.view(np.uint8).reshape(n, -1))
+                    .any(axis=1).sum())
+        from ingot_amd.abi import rec16_to_rec8
+
+        w8 = rec16_to_rec8(w_rec)
+        r = {"record_mismatches": bad16,
+             "rec8_mismatches": int((g8.cpu().numpy().reshape(n, -1) !=
+                                     w8.view(np.uint8).reshape(n, -1)).any(axis=1).sum())}
+        res[f"{chain.name}/ring64"] = r
+        print(chain.name, "ring64", r, flush=True)
+        del arena, g16, g8
+        torch.cuda.empty_cache()
     out = {"frames_per_case": n, "seed": args.seed, "wall_s": round(time.time() - t0, 1),
            "cases": res,
            "all_zero": all(v == 0 for c in res.values() for k, v in c.items() if "mismatch" in k)}
