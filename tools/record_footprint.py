@@ -34,7 +34,7 @@ def main():
     import torch
 
     import ingot_amd
-    from ingot_amd import Chain, GenProfile
+    from ingot_amd import Chain, GenProfile, abi
 
     ctx = ingot_amd.Context(0)
     lib = ingot_amd.load_library()
@@ -64,9 +64,18 @@ def main():
     for R in (8, 20, 64):
         runners[f"ring_R{R}"] = (bench.RingRunner(torch, lib, ctx, Chain.UdpParser, n, 64, arenas,
                                                   outs[:R], streams[:1], 16, 20), gate0)
+    # the ring consumer at its best-known shape with the small record ring:
+    # 3 / 4 blocks per CU (INGOT_TUNE_RING_GRID), 8 buffers
+    grids = {}
+    for gsz in (3, 4):
+        runners[f"ring_R8_grid{gsz}"] = (bench.RingRunner(torch, lib, ctx, Chain.UdpParser, n,
+                                                          64, arenas, outs[:8], streams[:1], 16,
+                                                          20), gate0)
+        grids[f"ring_R8_grid{gsz}"] = gsz
     res = {k: [] for k in runners}
     for r in range(args.reps):
         for name, (rr, g) in runners.items():
+            ctx.set_tuning(abi.TUNE_RING_GRID, grids.get(name, 0))
             if isinstance(rr, bench.RingRunner):
                 rr.warm(5, g)
             else:
@@ -75,6 +84,7 @@ def main():
             ms, _ = rr.run(20, g)
             res[name].append(ms * 1e3 / 20)
         print(f"rep {r}: " + " ".join(f"{k}={v[-1]:.3f}" for k, v in res.items()), flush=True)
+    ctx.set_tuning(abi.TUNE_RING_GRID, 0)
     steady = {}
     for name in ("launches_R8", "launches_R64"):
         rr, g = runners[name]
