@@ -306,3 +306,42 @@ def test_ring_group_divides_the_steps():
     assert bench.ring_group(67) == 1  # prime above the cap
     assert bench.ring_group(200) == 50
     assert bench.ring_group(1) == 1
+
+
+class _Buf:
+    def __init__(self, p):
+        self.p = p
+
+    def data_ptr(self):
+        return self.p
+
+
+class _S:
+    def __init__(self, i):
+        self.cuda_stream = i
+
+
+def test_runner_rotates_arenas_and_records_independently():
+    """bench.Runner: step k reads arena k % len(arenas) and writes record
+    buffer k % len(outs) on stream k % len(streams) — so the 64-record-buffer
+    variant of the C2 line keeps the default's 8-arena rotation
+    (config.record_buffers_rotated)."""
+    calls = []
+
+    class Lib:
+        def ingot_gpu_parse_strided(self, h, arena, stride, lens, n, chain, out, stream):
+            calls.append((arena, out, stream))
+            return 0
+
+    class Ctx:
+        _h = 0
+
+    arenas = [_Buf(1000 + i) for i in range(8)]
+    outs = [_Buf(5000 + i) for i in range(64)]
+    r = bench.Runner(None, Lib(), Ctx(), Chain.UdpParser, 16, 64, arenas, None, None, outs,
+                     [_S(0), _S(1)], 16)
+    for k in range(70):
+        assert r.launch(k) == 0
+    assert [a for a, _, _ in calls] == [1000 + k % 8 for k in range(70)]
+    assert [o for _, o, _ in calls] == [5000 + k % 64 for k in range(70)]
+    assert [s for _, _, s in calls] == [k % 2 for k in range(70)]
