@@ -486,7 +486,7 @@ class ReadRunner:
     ingot_gpu_parse_read_dense)."""
 
     def __init__(self, torch, lib, ctx, chain, n, arenas, seg_off, seg_len, pkt_seg, outs,
-                 streams, dense=False):
+                 streams, dense=False, first=False):
         self.torch, self.streams = torch, streams
         reps, h, c = len(arenas), ctx._h, int(chain)
         aptrs = [a.data_ptr() for a in arenas]
@@ -499,6 +499,14 @@ class ReadRunner:
             sd = self.seg.data_ptr()
             self.launch = lambda k: lib.ingot_gpu_parse_read_dense(
                 h, aptrs[k % reps], sd, ps, n, c, 0, outptrs[k % reps], None, sps[k % ns])
+            return
+        if first:  # chunk 0 per packet (ingot_gpu_parse_read_first)
+            import ingot_amd
+
+            self.first = ingot_amd.first_chunks(seg_off, seg_len, pkt_seg)
+            fp = self.first.data_ptr()
+            self.launch = lambda k: lib.ingot_gpu_parse_read_first(
+                h, aptrs[k % reps], so, sl, ps, fp, n, c, outptrs[k % reps], None, sps[k % ns])
             return
         self.launch = lambda k: lib.ingot_gpu_parse_read(h, aptrs[k % reps], so, sl, ps, n, c,
                                                          outptrs[k % reps], None, sps[k % ns])
@@ -1008,7 +1016,8 @@ def run_config(args, config, env):
         seg_off, seg_len, pkt_seg, head_chunks = read_chunks(
             torch, off, stride, rlens.to(torch.int32), recs0, READ_CHUNKS[config], dev)
 
-    def runner(nstreams, record, flows_only=False, dense=False, ring=False, group=G):
+    def runner(nstreams, record, flows_only=False, dense=False, ring=False, group=G,
+               first=False):
         if ring:
             return RingRunner(torch, lib, ctx, chain, n, stride, arenas,
                               ring_outs if record == 16 else outs8, streams[0], record, group)
@@ -1023,7 +1032,7 @@ def run_config(args, config, env):
                                 streams[:nstreams])
         if mode == "read":
             return ReadRunner(torch, lib, ctx, chain, n, arenas, seg_off, seg_len, pkt_seg,
-                              outs, streams[:nstreams], dense)
+                              outs, streams[:nstreams], dense, first)
         return Runner(torch, lib, ctx, chain, n, stride, arenas, off, lens, outs,
                       streams[:nstreams], record)
 
@@ -1214,6 +1223,14 @@ def run_config(args, config, env):
             variants[f"streams{args.streams}_dense_table"] = {
                 "value": round(n * vsteps / (ms / 1e3) / 1e6, 2),
                 "us_per_step": round(ms * 1e3 / vsteps, 3)}
+            # chunk 0's descriptor per packet (ingot_gpu_parse_read_first)
+            r = runner(args.streams, 16, first=True)
+            r.run(min(args.warmup, 50))
+            ms, _ = r.run(vsteps, gate)
+            variants[f"streams{args.streams}_first_chunk_inline"] = {
+                "value": round(n * vsteps / (ms / 1e3) / 1e6, 2),
+                "us_per_step": round(ms * 1e3 / vsteps, 3)}
+            del r
 
     if flows and not args.tune:
         # the plain parse (16-B records) of the same frames, one stream, as

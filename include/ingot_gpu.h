@@ -657,6 +657,23 @@ int ingot_gpu_parse_read_dense(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
                                uint64_t n, int chain, int fields, void* d_out,
                                uint16_t* d_chunk, void* stream);
 
+/*
+ * ingot_gpu_parse_read with chunk 0 of every packet also given per packet:
+ * d_first[i] = (seg_off[pkt_seg[i]] << 16) | seg_len[pkt_seg[i]] (0 for a
+ * packet without chunks; offsets < 2^48).  An mblk chain's packet pointer is
+ * its first chunk, so a ring of packets naturally carries this; the kernel
+ * then loads chunk 0's descriptor beside the packet's chunk bounds instead of
+ * after them (one HBM round trip before the staging, not two).  The chunk
+ * table is still read for chunks >= 1.  Records and chunk indices are those
+ * of ingot_gpu_parse_read over the same chunks (the caller keeps d_first
+ * consistent with the table).  16-B records; INGOT_TUNE_READ_PLAN is not
+ * consulted (chunk 0 in the default line-completing 3-5-piece window).
+ */
+int ingot_gpu_parse_read_first(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
+                               const uint64_t* d_seg_off, const uint16_t* d_seg_len,
+                               const uint32_t* d_pkt_seg, const uint64_t* d_first, uint64_t n,
+                               int chain, ingot_rec* d_out, uint16_t* d_chunk, void* stream);
+
 /* ---------------------------------------------------------------------------
  * In-place header rewrite: ingot's generated setters (packet/mod.rs:2097-2255;
  * BE bitfield set paths, bitfield.rs:188-315) after the parse, e.g. the

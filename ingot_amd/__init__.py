@@ -56,7 +56,7 @@ __all__ = [
     "Chain", "Context", "GenProfile", "PacketParseError", "ParseError", "UdpParser",
     "GenericUlp", "VlanUlp", "GeneveOverV6Tunnel", "gen_frames", "gen_lengths", "records_to_numpy",
     "fields_to_numpy", "load_library", "Parsed", "chunk_tables", "HeaderKind", "parse_header",
-    "HeaderParseError",
+    "HeaderParseError", "first_chunks",
 ]
 
 
@@ -376,13 +376,16 @@ class Context:
         return out
 
     def parse_read(self, arena, seg_off, seg_len, pkt_seg, chain: Chain, out=None, chunk=None,
-                   fields: Optional[str] = None, stream=None):
+                   fields: Optional[str] = None, stream=None, first=None):
         """Batched `<chain>::parse_read` over multi-chunk packets (packet i =
         chunks pkt_seg[i]..pkt_seg[i+1] of (seg_off int64, seg_len uint16);
         pkt_seg int32/uint32 with n+1 entries).  Returns (out, chunk): records
         (fields=None), ingot_fields blocks (fields="fields") or
         ingot_geneve_fields blocks (fields="geneve"), and per packet the index
-        of the chunk holding the remainder (uint16 stored in an int16 tensor)."""
+        of the chunk holding the remainder (uint16 stored in an int16 tensor).
+        `first` (records only; int64/uint64, n entries, see first_chunks()):
+        chunk 0 of every packet as (offset << 16) | length, which
+        ingot_gpu_parse_read_first loads beside the chunk bounds."""
         torch = _torch()
         n = pkt_seg.numel() - 1
         width = {None: REC_BYTES, "fields": FIELDS_BYTES,
@@ -401,6 +404,15 @@ class Context:
                         chunk=chunk)
         st = _stream(stream, self.device)
         args = (self._h, _ptr(arena), _ptr(seg_off), _ptr(seg_len), _ptr(pkt_seg), n)
+        if first is not None:
+            if fields is not None:
+                raise ValueError("first= is for 16-B records (ingot_gpu_parse_read_first)")
+            self._arg("first", first, _U64, n)
+            self._on_device(first=first)
+            rc = self._lib.ingot_gpu_parse_read_first(*args[:5], _ptr(first), n, int(chain),
+                                                      _ptr(out), _ptr(chunk), st)
+            _lib.check(rc, "ingot_gpu_parse_read_first")
+            return out, chunk
         if fields is None:
             rc = self._lib.ingot_gpu_parse_read(*args, int(chain), _ptr(out), _ptr(chunk), st)
         elif fields == "fields":
@@ -500,6 +512,22 @@ class Context:
         if not b:
             return None
         return _torch().empty(b, dtype=_torch().uint8, device=f"cuda:{self.device}")
+
+
+def first_chunks(seg_off, seg_len, pkt_seg):
+    """ingot_gpu_parse_read_first's per-packet array from a chunk table:
+    first[i] = (seg_off[pkt_seg[i]] << 16) | seg_len[pkt_seg[i]], 0 for a
+    packet without chunks (int64 tensor on the tables' device)."""
+    torch = _torch()
+    ps = pkt_seg.to(torch.int64) & 0xFFFFFFFF
+    lo, hi = ps[:-1], ps[1:]
+    has = hi > lo
+    idx = torch.where(has, lo, torch.zeros_like(lo))
+    if seg_off.numel() == 0:
+        return torch.zeros(lo.numel(), dtype=torch.int64, device=pkt_seg.device)
+    o = seg_off.to(torch.int64)[idx]
+    ln = seg_len.to(torch.int64)[idx] & 0xFFFF
+    return torch.where(has, (o << 16) | ln, torch.zeros_like(o))
 
 
 def check_descriptors(arena, off=None, lens=None, seg_off=None, seg_len=None, pkt_seg=None,

@@ -82,6 +82,11 @@ SIGNATURES = {
         [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, c_u8p, c_u64, ctypes.c_int, c_u8p, c_u8p,
          ctypes.c_void_p],
     ),
+    "ingot_gpu_parse_read_first": (
+        ctypes.c_int,
+        [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, c_u8p, c_u8p, c_u64, ctypes.c_int, c_u8p, c_u8p,
+         ctypes.c_void_p],
+    ),
     "ingot_gpu_fields_read": (
         ctypes.c_int,
         [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, c_u8p, c_u64, ctypes.c_int, c_u8p, c_u8p,

@@ -457,6 +457,22 @@ int ingot_gpu_parse_read(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint6
                            d_chunk, ingot_gpu::OUT_REC16, stream);
 }
 
+int ingot_gpu_parse_read_first(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
+                               const uint64_t* d_seg_off, const uint16_t* d_seg_len,
+                               const uint32_t* d_pkt_seg, const uint64_t* d_first, uint64_t n,
+                               int chain, ingot_rec* d_out, uint16_t* d_chunk, void* stream) {
+    if (!ctx || !chain_ok(chain)) return INGOT_GPU_EINVAL;
+    if (n == 0) return INGOT_GPU_SUCCESS;
+    if (!d_arena || !d_seg_off || !d_seg_len || !d_pkt_seg || !d_first || !d_out)
+        return INGOT_GPU_EINVAL;
+    if (int e = enter(ctx)) return e;
+    ingot_gpu::ParseArgs a{d_arena, d_seg_off, d_seg_len, 0, n, d_out, d_pkt_seg, d_chunk};
+    a.first = d_first;
+    return from_hip(ingot_gpu::launch_parse(a, ingot_gpu::LAYOUT_SEGMENTED, chain,
+                                            ingot_gpu::OUT_REC16, tuning_for(ctx, d_arena),
+                                            (hipStream_t)stream));
+}
+
 int ingot_gpu_fields_read(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_seg_off,
                           const uint16_t* d_seg_len, const uint32_t* d_pkt_seg, uint64_t n,
                           int chain, ingot_fields* d_out, uint16_t* d_chunk, void* stream) {

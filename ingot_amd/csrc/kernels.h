@@ -51,6 +51,9 @@ struct ParseArgs {
     const uint32_t* tile_local = nullptr;  // LAYOUT_PACKED: tile prefix within its group
     uint32_t policy = 0;                // INGOT_TUNE_CACHE_POLICY bits (launch_parse sets it)
     uint32_t linewin = 0;  // windows from byte 12: >= linewin chunks, then to the line end
+    // LAYOUT_SEGMENTED, optional (ingot_gpu_parse_read_first): per packet,
+    // chunk 0's (offset << 16) | length, indexed like pkt_seg
+    const uint64_t* first = nullptr;
 };
 
 struct FlowArgs {

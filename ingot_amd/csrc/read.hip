@@ -25,9 +25,15 @@ namespace {
 // the packet's last); later chunks are looked up when the walk reaches them.
 // Each prefetched descriptor holds 3 VGPRs through the walk: NPRE 3 is 68
 // VGPRs (7 waves per SIMD), NPRE 1 is 63 and NPRE 0 is 59 (8 waves).
+//
+// FIRST (ingot_gpu_parse_read_first): chunk 0's descriptor comes from the
+// per-packet array a.first, indexed by the packet like pkt_seg, so it is
+// loaded together with the chunk bounds — one HBM round trip before the
+// staging instead of two (pkt_seg, then the chunk table at pkt_seg[i]).
 template <int CS0, int CS1, int CS2, int CS3, int CHAIN, int MODE, bool DENSE = false,
-          bool PIPE = false, int NPRE = 3>
+          bool PIPE = false, int NPRE = 3, bool FIRST = false>
 __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
+    static_assert(!(FIRST && PIPE), "the lookahead kernel loads chunk 0 from the table");
     using FR = SegFrameP<CS0, CS1, CS2, CS3, DENSE, NPRE>;
     static_assert((CS1 == 0 || NPRE >= 1) && (CS2 == 0 || NPRE >= 2) && (CS3 == 0 || NPRE >= 3),
                   "a chunk staged in planes needs its descriptor up front");
@@ -66,11 +72,21 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
             l0 = ns ? a.len[s0] : 0u;
         }
     };
+    // FIRST: chunk 0's (offset << 16) | length of packet tt's lane, loaded
+    // beside its bounds (clamped index: always one load)
+    auto load_first = [&](uint64_t tt, uint32_t ns, uint64_t& o, uint32_t& l) {
+        uint64_t i = tt * WAVE + lane;
+        if (i >= a.n) i = a.n - 1u;
+        const uint64_t v = a.first[i];
+        o = ns ? v >> 16 : 0u;
+        l = ns ? (uint32_t)(v & 0xffffu) : 0u;
+    };
     uint32_t s0, nseg, s0n = 0, nsn = 0;
     uint64_t o0;
     uint32_t l0;
     load_pkt(t, s0, nseg);
-    load_d0(s0, nseg, o0, l0);
+    if constexpr (FIRST) load_first(t, nseg, o0, l0);
+    else load_d0(s0, nseg, o0, l0);
     if constexpr (PIPE) load_pkt(t + W < ntiles ? t + W : t, s0n, nsn);
 
     for (;;) {
@@ -213,7 +229,8 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
             nsn = nsnn;
         } else {
             load_pkt(t, s0, nseg);
-            load_d0(s0, nseg, o0, l0);
+            if constexpr (FIRST) load_first(t, nseg, o0, l0);
+            else load_d0(s0, nseg, o0, l0);
         }
     }
 }
@@ -221,7 +238,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
 // persist_cus != 0 (the PIPE kernels): a persistent grid of the blocks the
 // device holds at once.
 template <int CS0, int CS1, int CS2, int CS3, int MODE, bool DENSE = false, bool PIPE = false,
-          int NPRE = 3>
+          int NPRE = 3, bool FIRST = false>
 hipError_t launch_read(const ParseArgs& a, int chain, uint32_t grid, hipStream_t s,
                        uint32_t persist_cus = 0) {
     auto go = [&](auto kernel) {
@@ -234,16 +251,16 @@ hipError_t launch_read(const ParseArgs& a, int chain, uint32_t grid, hipStream_t
     };
     switch (chain) {
     case INGOT_CHAIN_UDP_PARSER:
-        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_UDP_PARSER, MODE, DENSE, PIPE, NPRE>);
+        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_UDP_PARSER, MODE, DENSE, PIPE, NPRE, FIRST>);
         break;
     case INGOT_CHAIN_GENERIC_ULP:
-        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENERIC_ULP, MODE, DENSE, PIPE, NPRE>);
+        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENERIC_ULP, MODE, DENSE, PIPE, NPRE, FIRST>);
         break;
     case INGOT_CHAIN_VLAN_ULP:
-        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_VLAN_ULP, MODE, DENSE, PIPE, NPRE>);
+        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_VLAN_ULP, MODE, DENSE, PIPE, NPRE, FIRST>);
         break;
     default:
-        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENEVE_OVER_V6, MODE, DENSE, PIPE, NPRE>);
+        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENEVE_OVER_V6, MODE, DENSE, PIPE, NPRE, FIRST>);
         break;
     }
     return hipGetLastError();
@@ -276,6 +293,19 @@ hipError_t launch_segmented(const ParseArgs& a, int chain, int mode, const Tunin
     // fewer bytes but loses occupancy (724 us).  1 = the round-1 {4,0,0,0}.
     // (9, the round-1 kernel without descriptor prefetch, is k_parse over
     // SegFrame: launch_parse runs it.)
+    // chunk 0's descriptor per packet (ingot_gpu_parse_read_first): the
+    // default window (3-5 pieces, line-completing; fields: 4 pieces; host
+    // pools: 4) with chunk 0 loaded beside the bounds; the staging plans of
+    // INGOT_TUNE_READ_PLAN other than these do not apply
+    if (a.first) {
+        if (mode == OUT_FIELDS)
+            return launch_read<4, 0, 0, 0, OUT_FIELDS, false, false, 3, true>(a, chain, g, s);
+        if (t.host_arena)
+            return launch_read<4, 0, 0, 0, OUT_REC16, false, false, 3, true>(a, chain, g, s);
+        ParseArgs b = a;
+        b.linewin = 3u;
+        return launch_read<5, 0, 0, 0, OUT_REC16, false, false, 3, true>(b, chain, g, s);
+    }
     if (mode == OUT_FIELDS) return launch_read<4, 0, 0, 0, OUT_FIELDS>(a, chain, g, s);
     // chunk pools in mapped host memory keep the round-1 window (every
     // staged piece is a PCIe read there)

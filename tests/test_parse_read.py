@@ -302,3 +302,38 @@ def test_scattered_and_aliased_chunks(torch, plan):
         bad = np.nonzero((r.reshape(n, 16) != w_rec.view(np.uint8).reshape(n, 16)).any(1))[0]
         assert bad.size == 0, (chain, bad[:5])
         assert np.array_equal(chunk.cpu().numpy().view(np.uint16), w_chunk)
+
+
+@pytest.mark.parametrize("chain", list(Chain))
+def test_first_chunk_descriptor_path_is_bit_exact(ctx, torch, chain):
+    """ingot_gpu_parse_read_first: chunk 0's descriptor per packet, loaded
+    beside the chunk bounds.  Records and the remainder's chunk index equal
+    the oracle's (and so ingot_gpu_parse_read's) over 1-8 chunks per packet,
+    empty chunks and packets without chunks, including the read KATs."""
+    prof = GenProfile.GENEVE_ADVERSARIAL if chain == TUN else GenProfile.ADVERSARIAL
+    frames = frames_of(prof, 30_000, seed=71 + int(chain))
+    frames += frames_of(GenProfile.GENEVE if chain == TUN else GenProfile.MIXED, 10_000, seed=73)
+    packets = split_many(frames, seed=11 + int(chain)) + [[]] * 3 + [[b""], [b"", b""]]
+    arena, seg_off, seg_len, pkt_seg = oracle.segments(packets)
+    dev = lambda x, dt: torch.from_numpy(x.view(dt)).cuda()  # noqa: E731
+    d = (dev(arena, np.uint8), dev(seg_off, np.int64), dev(seg_len, np.int16),
+         dev(pkt_seg, np.int32))
+    first = ingot_amd.first_chunks(d[1], d[2], d[3])
+    recs, chunk = ctx.parse_read(*d, chain, first=first)
+    torch.cuda.synchronize()
+    w_rec, _, w_chunk = oracle.parse_read_batch(arena, seg_off, seg_len, pkt_seg, chain)
+    n = len(packets)
+    got = recs.cpu().numpy().reshape(n, 16)
+    bad = np.nonzero((got != w_rec.view(np.uint8).reshape(n, 16)).any(1))[0]
+    assert bad.size == 0, (chain, bad[:5], [len(x) for x in packets[bad[0]]])
+    assert np.array_equal(chunk.cpu().numpy().view(np.uint16), w_chunk)
+
+
+def test_first_chunks_helper(torch):
+    """first_chunks(): (offset << 16) | length of each packet's chunk 0, 0
+    for a packet without chunks."""
+    so = torch.tensor([100, 7, 3000, 5], dtype=torch.int64)
+    sl = torch.tensor([14, 20, 65535, 1], dtype=torch.int16)
+    ps = torch.tensor([0, 2, 2, 3, 4], dtype=torch.int32)
+    f = ingot_amd.first_chunks(so, sl, ps).tolist()
+    assert f == [(100 << 16) | 14, 0, (3000 << 16) | 65535, (5 << 16) | 1]
