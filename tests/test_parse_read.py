@@ -333,7 +333,7 @@ def test_first_chunks_helper(torch):
     """first_chunks(): (offset << 16) | length of each packet's chunk 0, 0
     for a packet without chunks."""
     so = torch.tensor([100, 7, 3000, 5], dtype=torch.int64)
-    sl = torch.tensor([14, 20, 65535, 1], dtype=torch.int16)
+    sl = torch.tensor([14, 20, -1, 1], dtype=torch.int16)  # -1: a 65,535-B chunk
     ps = torch.tensor([0, 2, 2, 3, 4], dtype=torch.int32)
     f = ingot_amd.first_chunks(so, sl, ps).tolist()
     assert f == [(100 << 16) | 14, 0, (3000 << 16) | 65535, (5 << 16) | 1]
