@@ -465,7 +465,12 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              array, 16- or 8-B records: the multi-tile kernel
  *                              that stages the next tile while parsing one
  *                              (double-buffered LDS).  0 = on, 2 blocks per CU
- *                              (default); 1 = off; k >= 2 = k tiles per wave
+ *                              (default); 1 = off; k >= 2 = k tiles per wave.
+ *                              Frames addressed by offset (16-B records, device
+ *                              arenas, default windows, not the tunnel): k >= 2
+ *                              = k tiles per wave with the next tile's
+ *                              descriptors loaded a tile ahead (default 0: one
+ *                              tile per wave)
  *   INGOT_TUNE_CACHE_POLICY    0 = measured default (non-temporal record
  *                              stores; the ring kernel: non-temporal staging
  *                              loads and, for 16-B records, device-scope

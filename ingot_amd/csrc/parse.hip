@@ -32,8 +32,15 @@
 namespace ingot_gpu {
 namespace {
 
-template <uint32_t NCH, int LAYOUT, int CHAIN, int MODE, class ARGS, int SLOW = 0>
+// PF (INGOT_TUNE_PIPELINE >= 2 on frames addressed by offset, 16-B records):
+// a grid of fewer waves, each walking several tiles, with the next tile's
+// descriptors loaded while this tile is walked — its (offset, length) are
+// in registers when the next staging starts, one HBM round trip fewer per
+// tile after the first.
+template <uint32_t NCH, int LAYOUT, int CHAIN, int MODE, class ARGS, int SLOW = 0,
+          bool PF = false>
 __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
+    static_assert(!PF || LAYOUT == LAYOUT_INDEXED, "descriptor prefetch: offset-addressed frames");
     const ParseArgs& a = base_args(args);
     constexpr bool TUN = CHAIN == INGOT_CHAIN_GENEVE_OVER_V6;
     constexpr uint32_t WIN = NCH * 16u;
@@ -71,8 +78,17 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
                                                                                   : 0u;
     static_assert(SKIP <= 12u, "the walk reads the ethertype at frame byte 12");
 
-    for (uint64_t t = (uint64_t)blockIdx.x * WAVES + wave; t < ntiles;
-         t += (uint64_t)gridDim.x * WAVES) {
+    const uint64_t tstep = (uint64_t)gridDim.x * WAVES;
+    uint64_t pf_off = 0;  // PF: the next tile's descriptors, loaded a tile ahead
+    uint32_t pf_len = 0;
+    if constexpr (PF) {
+        const uint64_t i0 = ((uint64_t)blockIdx.x * WAVES + wave) * WAVE + lane;
+        if (i0 < a.n) {
+            pf_off = a.off[i0];
+            pf_len = (uint32_t)a.len[i0];
+        }
+    }
+    for (uint64_t t = (uint64_t)blockIdx.x * WAVES + wave; t < ntiles; t += tstep) {
         const uint64_t i = t * WAVE + lane;
         const bool valid = i < a.n;
         uint64_t off;
@@ -100,6 +116,9 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
             }
             off = a.off[t / PACKED_GROUP] + a.tile_local[t] + (x - len);
             if (valid && a.off_out) a.off_out[i] = off;
+        } else if constexpr (PF) {
+            off = pf_off;  // zero for a lane past the batch
+            len = pf_len;
         } else {
             off = valid ? a.off[i] : 0u;
             len = valid ? (uint32_t)a.len[i] : 0u;
@@ -156,6 +175,16 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
             if (c < np) stage16p(a.arena + bp + 16u * c, wimg + k * WAVE * 4u, a.policy);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (PF) {
+            // behind the staging wait: in flight during this tile's walk
+            const uint64_t in = (t + tstep) * WAVE + lane;
+            pf_off = 0u;
+            pf_len = 0u;
+            if (in < a.n) {
+                pf_off = a.off[in];
+                pf_len = (uint32_t)a.len[in];
+            }
+        }
 
         static_assert(!SLOW || (LAYOUT == LAYOUT_INDEXED && MODE == OUT_REC16),
                       "the compacted slow path is built for indexed 16-B records");
@@ -364,7 +393,7 @@ __global__ __launch_bounds__(BLOCK) void k_flows(FlowArgs args) {
 
 // persist_cus != 0: a persistent grid, capped at the blocks the device holds
 // at once (cus x resident_per_cu), so no CU runs a second partial round.
-template <uint32_t NCH, int LAYOUT, int MODE, class ARGS, int SLOW = 0>
+template <uint32_t NCH, int LAYOUT, int MODE, class ARGS, int SLOW = 0, bool PF = false>
 hipError_t launch_chain(const ARGS& a, int chain, uint32_t grid, hipStream_t s,
                         uint32_t persist_cus = 0) {
     auto go = [&](auto kernel) {
@@ -377,19 +406,19 @@ hipError_t launch_chain(const ARGS& a, int chain, uint32_t grid, hipStream_t s,
     };
     switch (chain) {
     case INGOT_CHAIN_UDP_PARSER:
-        go(k_parse<NCH, LAYOUT, INGOT_CHAIN_UDP_PARSER, MODE, ARGS, SLOW>);
+        go(k_parse<NCH, LAYOUT, INGOT_CHAIN_UDP_PARSER, MODE, ARGS, SLOW, PF>);
         break;
     case INGOT_CHAIN_GENERIC_ULP:
-        go(k_parse<NCH, LAYOUT, INGOT_CHAIN_GENERIC_ULP, MODE, ARGS, SLOW>);
+        go(k_parse<NCH, LAYOUT, INGOT_CHAIN_GENERIC_ULP, MODE, ARGS, SLOW, PF>);
         break;
     case INGOT_CHAIN_VLAN_ULP:
-        go(k_parse<NCH, LAYOUT, INGOT_CHAIN_VLAN_ULP, MODE, ARGS, SLOW>);
+        go(k_parse<NCH, LAYOUT, INGOT_CHAIN_VLAN_ULP, MODE, ARGS, SLOW, PF>);
         break;
     default:
         if constexpr (MODE == OUT_REC8) {
             return hipErrorInvalidValue;  // not offered for the tunnel (api.cpp)
         } else {
-            go(k_parse<NCH, LAYOUT, INGOT_CHAIN_GENEVE_OVER_V6, MODE, ARGS, SLOW>);
+            go(k_parse<NCH, LAYOUT, INGOT_CHAIN_GENEVE_OVER_V6, MODE, ARGS, SLOW, PF>);
         }
         break;
     }
@@ -499,6 +528,17 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
         case 8: return launch_mode<8, LAYOUT_PACKED>(a, chain, mode, g, s);
         default: return launch_mode<5, LAYOUT_PACKED>(a, chain, mode, g, s);
         }
+    }
+    // INGOT_TUNE_PIPELINE = k >= 2 (16-B records, device arenas, default
+    // windows, not the tunnel): k tiles per wave with the next tile's
+    // descriptors prefetched (k_parse<..., PF>)
+    if (t.pipeline >= 2 && mode == OUT_REC16 && !host && !t.window_indexed && !tun &&
+        t.slow_path != 1 && layout_kind == LAYOUT_INDEXED) {
+        const uint64_t tiles = (a.n + WAVE - 1) / WAVE;
+        const uint64_t waves = (tiles + (uint64_t)t.pipeline - 1) / (uint64_t)t.pipeline;
+        const uint64_t blocks = (waves + WAVES - 1) / WAVES;
+        return launch_chain<5, LAYOUT_INDEXED, OUT_REC16, ParseArgs, 0, true>(
+            a, chain, (uint32_t)(blocks ? blocks : 1), s);
     }
     // The compacted slow path (INGOT_TUNE_SLOW_PATH = 1, 16-B records,
     // device arenas): default windows only.

@@ -40,3 +40,26 @@ def test_pipelined_ring_bit_exact(tpw, depth, pol, n):
                                       nthreads=8)
             assert got.cpu().numpy().tobytes() == want.tobytes(), (prof, chain)
             assert got8.cpu().numpy().tobytes() == ingot_amd.rec16_to_rec8(want).tobytes()
+
+
+@pytest.mark.parametrize("tpw", [0, 1, 2, 3, 8])
+@pytest.mark.parametrize("n", [1, 63, 65, 100_003])
+def test_prefetching_indexed_kernel_bit_exact(tpw, n):
+    """INGOT_TUNE_PIPELINE >= 2 on frames addressed by offset (16-B records):
+    several tiles per wave with the next tile's descriptors loaded a tile
+    ahead (k_parse<..., PF>).  Records equal the oracle's on adversarial and
+    mixed / VLAN-EH frames, every non-tunnel chain, ragged sizes."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ctx = ingot_amd.Context(0)
+    ctx.set_tuning(TUNE_PIPELINE, tpw)
+    for prof in (GenProfile.ADVERSARIAL, GenProfile.MIXED, GenProfile.VLAN_V6EH):
+        arena, off, lens = ingot_amd.gen_frames(prof, n, seed=n + 3 * tpw)
+        a, o, ln = arena.cpu().numpy(), off.cpu().numpy(), lens.cpu().numpy()
+        for chain in (Chain.UdpParser, Chain.GenericUlp, Chain.VlanUlp):
+            got = ctx.parse(arena, off, lens, chain)
+            torch.cuda.synchronize()
+            want = oracle.parse_batch(a, o, ln, chain, nthreads=8)
+            assert got.cpu().numpy().tobytes() == want.tobytes(), (prof, chain)
