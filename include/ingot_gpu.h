@@ -530,6 +530,11 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              CU (1..8; 0 = measured default).  The ring's
  *                              tiles in flight per wave follow
  *                              INGOT_TUNE_PIPE_DEPTH
+ *   INGOT_TUNE_XCD_REMAP       slot-ring kernel (k_parse_pipe): 1 = blocks
+ *                              renumbered XCD-major (block b runs on XCD b % 8;
+ *                              logical block (b % 8) * G/8 + b / 8), so each
+ *                              XCD walks a contiguous eighth of every round of
+ *                              tiles; 0 = hardware order (default)
  *   INGOT_TUNE_RING_GROUPS     ingot_gpu_parse_ring: batches in flight at
  *                              once (1, 2 or 4; 0 = measured default): the
  *                              grid is cut into that many block groups, group
@@ -548,6 +553,7 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
 #define INGOT_TUNE_FLOW_KERNEL 11
 #define INGOT_TUNE_RING_GRID 12
 #define INGOT_TUNE_RING_GROUPS 13
+#define INGOT_TUNE_XCD_REMAP 14
 int ingot_gpu_ctx_set_tuning(ingot_gpu_ctx* ctx, int key, int value);
 int ingot_gpu_ctx_get_tuning(const ingot_gpu_ctx* ctx, int key);
 

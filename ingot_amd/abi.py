@@ -83,6 +83,7 @@ TUNE_READ_PLAN = 10
 TUNE_FLOW_KERNEL = 11
 TUNE_RING_GRID = 12
 TUNE_RING_GROUPS = 13
+TUNE_XCD_REMAP = 14
 
 
 class IngotRec(ctypes.Structure):

@@ -335,6 +335,7 @@ int ingot_gpu_ctx_set_tuning(ingot_gpu_ctx* ctx, int key, int value) {
     case INGOT_TUNE_FLOW_KERNEL: ctx->tuning.flow_kernel = value; break;
     case INGOT_TUNE_RING_GRID: ctx->tuning.ring_grid = value; break;
     case INGOT_TUNE_RING_GROUPS: ctx->tuning.ring_groups = value; break;
+    case INGOT_TUNE_XCD_REMAP: ctx->tuning.xcd_remap = value; break;
     default: ctx->tuning.max_blocks = (uint32_t)value; break;
     }
     return INGOT_GPU_SUCCESS;
@@ -356,6 +357,7 @@ int ingot_gpu_ctx_get_tuning(const ingot_gpu_ctx* ctx, int key) {
     case INGOT_TUNE_FLOW_KERNEL: return ctx->tuning.flow_kernel;
     case INGOT_TUNE_RING_GRID: return ctx->tuning.ring_grid;
     case INGOT_TUNE_RING_GROUPS: return ctx->tuning.ring_groups;
+    case INGOT_TUNE_XCD_REMAP: return ctx->tuning.xcd_remap;
     default: return INGOT_GPU_EINVAL;
     }
 }

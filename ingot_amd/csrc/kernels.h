@@ -54,6 +54,7 @@ struct ParseArgs {
     // LAYOUT_SEGMENTED, optional (ingot_gpu_parse_read_first): per packet,
     // chunk 0's (offset << 16) | length, indexed like pkt_seg
     const uint64_t* first = nullptr;
+    uint32_t xcd_remap = 0;  // k_parse_pipe: logical block = XCD-major (INGOT_TUNE_XCD_REMAP)
 };
 
 struct FlowArgs {
@@ -155,6 +156,7 @@ struct Tuning {
                            // overlapped with the next tile (k_flows), 2 = k_parse persistent
     int ring_grid = 0;     // ring consumer: blocks per CU (0 = measured default)
     int ring_groups = 0;   // ring consumer: batches in flight at once (0 = measured default)
+    int xcd_remap = 0;     // slot ring: 1 = each XCD's blocks take a contiguous share of tiles
     uint32_t cus = 256;  // compute units of the context's device (grid shaping)
     bool host_arena = false;  // per call: the arena is host memory (ingot_gpu_host_map)
 };

@@ -52,7 +52,12 @@ __global__ __launch_bounds__(BLOCK) void k_parse_pipe(ParseArgs a) {
         }
     };
 
-    uint64_t t = (uint64_t)blockIdx.x * WAVES + wave;
+    // XCD-major renumbering (INGOT_TUNE_XCD_REMAP): block b runs on XCD b % 8;
+    // as logical block (b % 8) * G/8 + b / 8 each XCD takes a contiguous
+    // eighth of every round of tiles instead of every eighth block's tiles
+    uint32_t bid = blockIdx.x;
+    if (a.xcd_remap && gridDim.x % 8u == 0u) bid = (bid % 8u) * (gridDim.x / 8u) + bid / 8u;
+    uint64_t t = (uint64_t)bid * WAVES + wave;
     if (t >= ntiles) return;
     // prologue: the first DEPTH-1 tiles
 #pragma unroll
@@ -420,8 +425,10 @@ constexpr uint32_t kModifyRingPolicy = 3;  // nt staging loads + nt write-back
 // 64 B, interleaved A/B): 16.6-16.7 vs 18.6-18.8 us per launch on one
 // stream, 13.5-13.6 vs 14.2-14.4 us per step on two; 6 or 12 tiles per
 // wave (uneven over the CUs) lose most of it.
-hipError_t launch_slot_ring(const ParseArgs& a, int chain, int mode, const Tuning& t,
+hipError_t launch_slot_ring(const ParseArgs& args, int chain, int mode, const Tuning& t,
                             hipStream_t s) {
+    ParseArgs a = args;
+    a.xcd_remap = t.xcd_remap ? 1u : 0u;
     const uint64_t tiles = (a.n + WAVE - 1) / WAVE;
     uint64_t blocks;
     if (t.pipeline > 1) {

@@ -63,3 +63,27 @@ def test_prefetching_indexed_kernel_bit_exact(tpw, n):
             torch.cuda.synchronize()
             want = oracle.parse_batch(a, o, ln, chain, nthreads=8)
             assert got.cpu().numpy().tobytes() == want.tobytes(), (prof, chain)
+
+
+@pytest.mark.parametrize("tpw", [0, 3])
+@pytest.mark.parametrize("n", [65, 100_003, 1 << 20])
+def test_xcd_remapped_ring_bit_exact(tpw, n):
+    """INGOT_TUNE_XCD_REMAP = 1: the slot-ring kernel's blocks renumbered
+    XCD-major cover every tile exactly once — records equal the oracle's."""
+    import torch
+
+    from ingot_amd.abi import TUNE_XCD_REMAP
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ctx = ingot_amd.Context(0)
+    ctx.set_tuning(TUNE_XCD_REMAP, 1)
+    ctx.set_tuning(TUNE_PIPELINE, tpw)
+    for prof in (GenProfile.V4UDP64, GenProfile.ADVERSARIAL):
+        arena, _, _ = ingot_amd.gen_frames(prof, n, seed=n + 5, stride=64)
+        for chain in (Chain.UdpParser, Chain.VlanUlp):
+            got = ctx.parse_strided(arena, 64, n, chain)
+            torch.cuda.synchronize()
+            want = oracle.parse_batch(arena.cpu().numpy(), None, None, chain, stride=64, n=n,
+                                      nthreads=8)
+            assert got.cpu().numpy().tobytes() == want.tobytes(), (prof, chain)

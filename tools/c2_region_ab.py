@@ -20,7 +20,7 @@ sys.path.insert(0, str(ROOT))
 
 import bench  # noqa: E402
 
-# name -> (streams, stagger us, tiles per wave (0 = default grid), policy (0 = default))
+# name -> (streams, stagger us, tiles per wave (0 = default grid), policy (0 = default)[, xcd remap])
 VARIANTS = {
     "s2_st6": (2, 6.0, 0, 0),
     "s2_st3": (2, 3.0, 0, 0),
@@ -37,6 +37,8 @@ VARIANTS = {
     "s2_pol27": (2, 6.0, 0, 27),
     "s2_pol3": (2, 6.0, 0, 3),
     "s1": (1, 0.0, 0, 0),
+    "s2_xcd": (2, 6.0, 0, 0, 1),
+    "s1_xcd": (1, 0.0, 0, 0, 1),
 }
 
 
@@ -73,6 +75,7 @@ def main():
     def knobs(v):
         ctx.set_tuning(abi.TUNE_PIPELINE, v[2])
         ctx.set_tuning(abi.TUNE_CACHE_POLICY, v[3])
+        ctx.set_tuning(abi.TUNE_XCD_REMAP, v[4] if len(v) > 4 else 0)
 
     res = {k: [] for k in variants}
     for r in range(args.reps):
@@ -99,7 +102,7 @@ def main():
                    "read_frac": round(rd / (statistics.median(v) * 1e-6) / 8e12, 4)}
                for k, v in res.items()}
     out = {"steps": args.steps, "warmup": args.warmup, "reps": args.reps,
-           "variants": {k: dict(zip(("streams", "stagger_us", "tiles_per_wave", "policy"), v))
+           "variants": {k: dict(zip(("streams", "stagger_us", "tiles_per_wave", "policy", "xcd"), v))
                         for k, v in variants.items()},
            "summary": summary, "steady_us_per_step": steady, "raw": res}
     Path(args.out).parent.mkdir(parents=True, exist_ok=True)
