@@ -530,11 +530,15 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              CU (1..8; 0 = measured default).  The ring's
  *                              tiles in flight per wave follow
  *                              INGOT_TUNE_PIPE_DEPTH
- *   INGOT_TUNE_XCD_REMAP       slot-ring kernel (k_parse_pipe): 1 = blocks
+ *   INGOT_TUNE_XCD_REMAP       slot-ring kernels (parse, rewrite) tile order:
+ *                              0 = measured default (= 1); 1 = blocks
  *                              renumbered XCD-major (block b runs on XCD b % 8;
  *                              logical block (b % 8) * G/8 + b / 8), so each
  *                              XCD walks a contiguous eighth of every round of
- *                              tiles; 0 = hardware order (default)
+ *                              tiles; 2 = each wave walks a contiguous run of
+ *                              tiles instead of striding by the grid; 3 = both;
+ *                              4 = hardware order, grid stride (parse ring: bit
+ *                              1 only applies to it)
  *   INGOT_TUNE_RING_GROUPS     ingot_gpu_parse_ring: batches in flight at
  *                              once (1, 2 or 4; 0 = measured default): the
  *                              grid is cut into that many block groups, group

@@ -27,7 +27,6 @@ __global__ __launch_bounds__(BLOCK) void k_parse_pipe(ParseArgs a) {
     const uint32_t wave = threadIdx.x / WAVE;
     uint32_t* img0 = s_img + wave * WAVE_DW;
     const uint64_t ntiles = (a.n + WAVE - 1u) / WAVE;
-    const uint64_t step = (uint64_t)gridDim.x * WAVES;
     const uint32_t take = a.stride < WIN ? a.stride : WIN;
 
     auto stage = [&](uint64_t tt, uint32_t* img) {
@@ -52,20 +51,35 @@ __global__ __launch_bounds__(BLOCK) void k_parse_pipe(ParseArgs a) {
         }
     };
 
-    // XCD-major renumbering (INGOT_TUNE_XCD_REMAP): block b runs on XCD b % 8;
-    // as logical block (b % 8) * G/8 + b / 8 each XCD takes a contiguous
-    // eighth of every round of tiles instead of every eighth block's tiles
+    // Tile order (INGOT_TUNE_XCD_REMAP).  Bit 0: block b runs on XCD b % 8;
+    // renumbered (b % 8) * G/8 + b / 8 ("XCD-major"), each XCD's blocks take
+    // a contiguous eighth of every round of G x WAVES tiles instead of every
+    // eighth block's tiles.  Bit 1: each wave walks a contiguous run of
+    // tiles (wave w: tiles w*J .. w*J + J-1) instead of striding by the grid.
     uint32_t bid = blockIdx.x;
-    if (a.xcd_remap && gridDim.x % 8u == 0u) bid = (bid % 8u) * (gridDim.x / 8u) + bid / 8u;
-    uint64_t t = (uint64_t)bid * WAVES + wave;
-    if (t >= ntiles) return;
+    if ((a.xcd_remap & 1u) && gridDim.x % 8u == 0u)
+        bid = (bid % 8u) * (gridDim.x / 8u) + bid / 8u;
+    const uint64_t gw = (uint64_t)bid * WAVES + wave;  // this wave's index in the grid
+    const uint64_t nw = (uint64_t)gridDim.x * WAVES;
+    uint64_t t, step, tend;
+    if (a.xcd_remap & 2u) {
+        const uint64_t J = (ntiles + nw - 1u) / nw;
+        t = gw * J;
+        tend = t + J < ntiles ? t + J : ntiles;
+        step = 1u;
+    } else {
+        t = gw;
+        tend = ntiles;
+        step = nw;
+    }
+    if (t >= tend) return;
     // prologue: the first DEPTH-1 tiles
 #pragma unroll
     for (uint32_t d = 0; d + 1u < DEPTH; ++d)
-        if (t + d * step < ntiles) stage(t + d * step, img0 + d * IMG_DW);
+        if (t + d * step < tend) stage(t + d * step, img0 + d * IMG_DW);
     for (uint32_t j = 0;; ++j) {
         const uint64_t tn = t + (DEPTH - 1u) * step;
-        if (tn < ntiles) {
+        if (tn < tend) {
             stage(tn, img0 + ((j + DEPTH - 1u) % DEPTH) * IMG_DW);
             // tile j's loads have landed (vector-memory ops retire in issue
             // order, stores and LDS-DMA alike): younger than them are the
@@ -82,7 +96,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse_pipe(ParseArgs a) {
         }
         parse(t, img0 + (j % DEPTH) * IMG_DW);
         t += step;
-        if (t >= ntiles) break;
+        if (t >= tend) break;
     }
 }
 
@@ -350,7 +364,11 @@ __global__ __launch_bounds__(BLOCK) void k_modify_pipe(ModifyArgs m) {
         }
     };
 
-    uint64_t t = (uint64_t)blockIdx.x * WAVES + wave;
+    // XCD-major block order (a.xcd_remap bit 0), as in k_parse_pipe
+    uint32_t bid = blockIdx.x;
+    if ((a.xcd_remap & 1u) && gridDim.x % 8u == 0u)
+        bid = (bid % 8u) * (gridDim.x / 8u) + bid / 8u;
+    uint64_t t = (uint64_t)bid * WAVES + wave;
     if (t >= ntiles) return;
 #pragma unroll
     for (uint32_t d = 0; d + 1u < DEPTH; ++d)
@@ -428,7 +446,10 @@ constexpr uint32_t kModifyRingPolicy = 3;  // nt staging loads + nt write-back
 hipError_t launch_slot_ring(const ParseArgs& args, int chain, int mode, const Tuning& t,
                             hipStream_t s) {
     ParseArgs a = args;
-    a.xcd_remap = t.xcd_remap ? 1u : 0u;
+    // tile order: XCD-major by default (measured, DESIGN.md §4.2: 2 streams
+    // 12.22 -> 12.03 us/step at 20 steps, 11.91 -> 11.74 at 2,000);
+    // INGOT_TUNE_XCD_REMAP 4 = hardware order
+    a.xcd_remap = t.xcd_remap == 0 ? 1u : t.xcd_remap == 4 ? 0u : (uint32_t)t.xcd_remap;
     const uint64_t tiles = (a.n + WAVE - 1) / WAVE;
     uint64_t blocks;
     if (t.pipeline > 1) {
@@ -460,6 +481,7 @@ hipError_t launch_slot_ring(const ParseArgs& args, int chain, int mode, const Tu
 hipError_t launch_modify_ring(const ModifyArgs& args, int chain, const Tuning& t,
                               hipStream_t s) {
     ModifyArgs a = args;
+    a.p.xcd_remap = t.xcd_remap == 0 ? 1u : t.xcd_remap == 4 ? 0u : ((uint32_t)t.xcd_remap & 1u);
     a.wb = t.writeback ? (uint32_t)t.writeback : kModifyRingWb;
     a.p.policy = t.cache_policy ? (uint32_t)t.cache_policy & 0x3bu : kModifyRingPolicy;
     const uint64_t tiles = (a.p.n + WAVE - 1) / WAVE;

@@ -65,9 +65,10 @@ def test_prefetching_indexed_kernel_bit_exact(tpw, n):
             assert got.cpu().numpy().tobytes() == want.tobytes(), (prof, chain)
 
 
+@pytest.mark.parametrize("remap", [1, 2, 3, 4])
 @pytest.mark.parametrize("tpw", [0, 3])
 @pytest.mark.parametrize("n", [65, 100_003, 1 << 20])
-def test_xcd_remapped_ring_bit_exact(tpw, n):
+def test_xcd_remapped_ring_bit_exact(remap, tpw, n):
     """INGOT_TUNE_XCD_REMAP = 1: the slot-ring kernel's blocks renumbered
     XCD-major cover every tile exactly once — records equal the oracle's."""
     import torch
@@ -77,7 +78,7 @@ def test_xcd_remapped_ring_bit_exact(tpw, n):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     ctx = ingot_amd.Context(0)
-    ctx.set_tuning(TUNE_XCD_REMAP, 1)
+    ctx.set_tuning(TUNE_XCD_REMAP, remap)
     ctx.set_tuning(TUNE_PIPELINE, tpw)
     for prof in (GenProfile.V4UDP64, GenProfile.ADVERSARIAL):
         arena, _, _ = ingot_amd.gen_frames(prof, n, seed=n + 5, stride=64)

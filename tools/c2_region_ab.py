@@ -23,6 +23,8 @@ import bench  # noqa: E402
 # name -> (streams, stagger us, tiles per wave (0 = default grid), policy (0 = default)[, xcd remap])
 VARIANTS = {
     "s2_st6": (2, 6.0, 0, 0),
+    "s2_hw": (2, 6.0, 0, 0, 4),
+    "s1_hw": (1, 0.0, 0, 0, 4),
     "s2_st3": (2, 3.0, 0, 0),
     "s2_st4.5": (2, 4.5, 0, 0),
     "s2_st7.5": (2, 7.5, 0, 0),
@@ -39,6 +41,9 @@ VARIANTS = {
     "s1": (1, 0.0, 0, 0),
     "s2_xcd": (2, 6.0, 0, 0, 1),
     "s1_xcd": (1, 0.0, 0, 0, 1),
+    "s2_run": (2, 6.0, 0, 0, 2),
+    "s2_xcd_run": (2, 6.0, 0, 0, 3),
+    "s1_run": (1, 0.0, 0, 0, 2),
 }
 
 
