@@ -537,8 +537,9 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              XCD walks a contiguous eighth of every round of
  *                              tiles; 2 = each wave walks a contiguous run of
  *                              tiles instead of striding by the grid; 3 = both;
- *                              4 = hardware order, grid stride (parse ring: bit
- *                              1 only applies to it)
+ *                              4 = hardware order, grid stride; 5 = the batch
+ *                              in 8 contiguous regions, one per XCD (parse ring
+ *                              only; the rewrite ring takes 0/1/4)
  *   INGOT_TUNE_RING_GROUPS     ingot_gpu_parse_ring: batches in flight at
  *                              once (1, 2 or 4; 0 = measured default): the
  *                              grid is cut into that many block groups, group

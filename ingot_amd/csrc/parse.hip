@@ -688,7 +688,7 @@ bool tuning_valid(int key, int value) {
     case INGOT_TUNE_RING_GROUPS:
         return value == 0 || value == 1 || value == 2 || value == 4;
     case INGOT_TUNE_XCD_REMAP:
-        return value >= 0 && value <= 4;
+        return value >= 0 && value <= 5;
     case INGOT_TUNE_WINDOW_INDEXED:  // 20 + k: line-completing, up to k chunks
         return value == 0 || (value >= 2 && value <= 6) || value == 8 || value == 9 ||
                value == 100 || (value >= 22 && value <= 26) || value == 28 || value == 29 ||

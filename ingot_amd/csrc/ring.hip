@@ -62,7 +62,16 @@ __global__ __launch_bounds__(BLOCK) void k_parse_pipe(ParseArgs a) {
     const uint64_t gw = (uint64_t)bid * WAVES + wave;  // this wave's index in the grid
     const uint64_t nw = (uint64_t)gridDim.x * WAVES;
     uint64_t t, step, tend;
-    if (a.xcd_remap & 2u) {
+    if ((a.xcd_remap & 4u) && gridDim.x % 8u == 0u) {
+        // bit 2: the batch in 8 contiguous regions, one per XCD, the XCD's
+        // waves striding through its region
+        const uint64_t x = blockIdx.x % 8u;
+        const uint64_t nwx = (uint64_t)(gridDim.x / 8u) * WAVES;
+        const uint64_t region = (ntiles + 7u) / 8u;
+        t = x * region + (uint64_t)(blockIdx.x / 8u) * WAVES + wave;
+        tend = (x + 1u) * region < ntiles ? (x + 1u) * region : ntiles;
+        step = nwx;
+    } else if (a.xcd_remap & 2u) {
         const uint64_t J = (ntiles + nw - 1u) / nw;
         t = gw * J;
         tend = t + J < ntiles ? t + J : ntiles;
@@ -449,7 +458,10 @@ hipError_t launch_slot_ring(const ParseArgs& args, int chain, int mode, const Tu
     // tile order: XCD-major by default (measured, DESIGN.md §4.2: 2 streams
     // 12.22 -> 12.03 us/step at 20 steps, 11.91 -> 11.74 at 2,000);
     // INGOT_TUNE_XCD_REMAP 4 = hardware order
-    a.xcd_remap = t.xcd_remap == 0 ? 1u : t.xcd_remap == 4 ? 0u : (uint32_t)t.xcd_remap;
+    a.xcd_remap = t.xcd_remap == 0   ? 1u
+                  : t.xcd_remap == 4 ? 0u
+                  : t.xcd_remap == 5 ? 4u
+                                     : (uint32_t)t.xcd_remap;
     const uint64_t tiles = (a.n + WAVE - 1) / WAVE;
     uint64_t blocks;
     if (t.pipeline > 1) {

@@ -65,7 +65,7 @@ def test_prefetching_indexed_kernel_bit_exact(tpw, n):
             assert got.cpu().numpy().tobytes() == want.tobytes(), (prof, chain)
 
 
-@pytest.mark.parametrize("remap", [1, 2, 3, 4])
+@pytest.mark.parametrize("remap", [1, 2, 3, 4, 5])
 @pytest.mark.parametrize("tpw", [0, 3])
 @pytest.mark.parametrize("n", [65, 100_003, 1 << 20])
 def test_xcd_remapped_ring_bit_exact(remap, tpw, n):

@@ -24,6 +24,8 @@ import bench  # noqa: E402
 VARIANTS = {
     "s2_st6": (2, 6.0, 0, 0),
     "s2_hw": (2, 6.0, 0, 0, 4),
+    "s2_regions": (2, 6.0, 0, 0, 5),
+    "s1_regions": (1, 0.0, 0, 0, 5),
     "s1_hw": (1, 0.0, 0, 0, 4),
     "s2_st3": (2, 3.0, 0, 0),
     "s2_st4.5": (2, 4.5, 0, 0),
