@@ -621,6 +621,65 @@ class Gate:
         self.db.ring(self.seq)
         self._timer.cancel()
 
+    # the region's timing events: HipEvent (no system fence) unless
+    # FENCED_EVENTS (bench.py --fenced-events: torch's default events)
+    FENCED_EVENTS = False
+
+    def event(self):
+        if self.FENCED_EVENTS:
+            import torch
+
+            return torch.cuda.Event(enable_timing=True)
+        return HipEvent()
+
+
+class HipEvent:
+    """A timing-only HIP event created with hipEventDisableSystemFence
+    (hip_runtime_api.h: for events "only being used to measure timing"; on
+    AMD GPUs it avoids the cache writeback + invalidation a default event's
+    record performs, and that work's delay of the launch that follows it).
+    Recorded on a torch stream; read after a device synchronize.  The work
+    between two such events is unchanged — only the measurement's own fence
+    at the region's edges goes."""
+
+    FLAGS = 0x20000000  # hipEventDisableSystemFence
+    _lib = None
+
+    @classmethod
+    def lib(cls):
+        if cls._lib is None:
+            import ctypes
+
+            cls._lib = ctypes.CDLL("libamdhip64.so")
+        return cls._lib
+
+    def __init__(self):
+        import ctypes
+
+        self._c = ctypes
+        self.h = ctypes.c_void_p()
+        rc = self.lib().hipEventCreateWithFlags(ctypes.byref(self.h), ctypes.c_uint(self.FLAGS))
+        if rc != 0:
+            raise RuntimeError(f"hipEventCreateWithFlags: {rc}")
+
+    def record(self, stream):
+        rc = self.lib().hipEventRecord(self.h, self._c.c_void_p(stream.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"hipEventRecord: {rc}")
+
+    def elapsed_time(self, other):
+        ms = self._c.c_float()
+        rc = self.lib().hipEventElapsedTime(self._c.byref(ms), self.h, other.h)
+        if rc != 0:
+            raise RuntimeError(f"hipEventElapsedTime: {rc}")
+        return ms.value
+
+    def __del__(self):
+        try:
+            self.lib().hipEventDestroy(self.h)
+        except Exception:
+            pass
+
 
 def _timed(torch, streams, launch, steps, finish=None, gate=None, group=1):
     """Run `steps` steps; returns (ms, wall s).  Every stream stamps a
@@ -633,6 +692,9 @@ def _timed(torch, streams, launch, steps, finish=None, gate=None, group=1):
     launch(k, m) runs steps k .. k+m-1 (the ring consumer)."""
     s0 = streams[0]
     w0 = time.perf_counter()
+    # gated regions: the gate's timing events (Gate.event: timing-only HIP
+    # events); ungated: torch's (the other streams wait on the start event)
+    mk_event = getattr(gate, "event", None) or (lambda: torch.cuda.Event(enable_timing=True))
     if gate is not None:
         gate.arm(streams)
     starts, ends = [], []
@@ -645,7 +707,7 @@ def _timed(torch, streams, launch, steps, finish=None, gate=None, group=1):
                 s.wait_event(e0)
         else:
             for s in streams:
-                e = torch.cuda.Event(enable_timing=True)
+                e = mk_event()
                 e.record(s)
                 starts.append(e)
         held = 0
@@ -659,7 +721,7 @@ def _timed(torch, streams, launch, steps, finish=None, gate=None, group=1):
         if finish is not None:
             finish()
         for s in streams:
-            e = torch.cuda.Event(enable_timing=True)
+            e = mk_event()
             e.record(s)
             ends.append(e)
     finally:
@@ -877,6 +939,9 @@ def main():
                          "stream 0 (default: the config's STAGGER_US, else 0)")
     ap.add_argument("--plan", action="store_true",
                     help="print the ranks' shares and exit without touching a GPU")
+    ap.add_argument("--fenced-events", action="store_true",
+                    help="time gated regions with torch's default (system-fenced) events "
+                         "instead of timing-only HIP events")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="INGOT_TUNE_* knob for this run, e.g. slow_path=1 (A/B and "
                          "profiling of variants; results never depend on it)")
@@ -952,6 +1017,7 @@ def main():
 
 
 def run_config(args, config, env):
+    Gate.FENCED_EVENTS = bool(getattr(args, "fenced_events", False))
     """One config's bench line (rank 0 returns the dict, other ranks None)."""
     torch, dist, ingot_amd, lib, ctx, world, rank, local, dev = env
     from ingot_amd import Chain, GenProfile
@@ -1053,7 +1119,9 @@ def run_config(args, config, env):
                        else STAGGER_US.get(config, 0.0))
             gate = Gate(ingot_amd, ctx, stagger)
             gate_note = (f"first {Gate.HOLD} launches held behind a doorbell "
-                         "(ingot_gpu_doorbell_wait); region from the first step's start")
+                         "(ingot_gpu_doorbell_wait); region from the first step's start" +
+                         ("" if Gate.FENCED_EVENTS else
+                          "; timing-only HIP events (hipEventDisableSystemFence)"))
             if policy == "until_collective":
                 gate_note = ("launches held behind a doorbell until the first RCCL collective "
                              "of the region, which is issued only after the ring")

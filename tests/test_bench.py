@@ -214,6 +214,9 @@ class _Gate:
     def open(self):
         self.log.append("open")
 
+    def event(self):  # the gated region's timing events (bench.HipEvent on a GPU)
+        return _ClockTorch.cuda.Event()
+
 
 def test_timed_region_spans_earliest_start_to_latest_end(monkeypatch):
     """_timed: every stream stamps its own start and end; the region is the
