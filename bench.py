@@ -650,7 +650,15 @@ class HipEvent:
         if cls._lib is None:
             import ctypes
 
-            cls._lib = ctypes.CDLL("libamdhip64.so")
+            # the HIP runtime torch already loaded (its streams are the ones
+            # recorded on), never a second copy from another path
+            path = "libamdhip64.so"
+            with open("/proc/self/maps") as f:
+                for line in f:
+                    if "libamdhip64.so" in line and "/" in line:
+                        path = line[line.index("/"):].strip()
+                        break
+            cls._lib = ctypes.CDLL(path)
         return cls._lib
 
     def __init__(self):
