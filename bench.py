@@ -211,14 +211,7 @@ def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode
     import oracle
     from ingot_amd import EditOp, Field
 
-    try:  # -march=native build for this host, into a scratch dir
-        d = Path(os.environ.get("TMPDIR", "/tmp")) / f"ingot_oracle_native_{os.getpid()}"
-        lib = oracle.load(oracle.build(out_dir=d, native=True))
-        arch = "native"
-    except Exception as e:  # noqa: BLE001
-        log(f"[bench] native oracle build failed ({e}); using the prebuilt x86-64-v3 one")
-        lib = oracle.load()
-        arch = "x86-64-v3"
+    lib, arch = _native_oracle(oracle)
 
     def one_call(t):
         if mode == "read":
@@ -275,6 +268,22 @@ def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode
         "cpu_model": _cpu_model(),
         **share,
     }
+
+
+_NATIVE_ORACLE = []
+
+
+def _native_oracle(oracle):
+    """The oracle built -march=native for this host (once per process, into a
+    scratch dir), or the prebuilt x86-64-v3 one if that build fails."""
+    if not _NATIVE_ORACLE:
+        try:
+            d = Path(os.environ.get("TMPDIR", "/tmp")) / f"ingot_oracle_native_{os.getpid()}"
+            _NATIVE_ORACLE.append((oracle.load(oracle.build(out_dir=d, native=True)), "native"))
+        except Exception as e:  # noqa: BLE001
+            log(f"[bench] native oracle build failed ({e}); using the prebuilt x86-64-v3 one")
+            _NATIVE_ORACLE.append((oracle.load(), "x86-64-v3"))
+    return _NATIVE_ORACLE[0]
 
 
 def _cpu_model():
@@ -526,9 +535,13 @@ class FlowRunner:
     every reduce has completed."""
 
     def __init__(self, torch, lib, ctx, chain, n, arenas, off, lens, hists, flows, streams,
-                 reduce_fn, flows_only=False):
+                 reduce_fn, flows_only=False, open_before_collective=False):
         """flows_only: launch the parse + hash kernel alone (no histogram, no
-        reduce) — the dominant kernel, timed for `roofline`."""
+        reduce) — the dominant kernel, timed for `roofline`.
+        open_before_collective: gate_policy "until_collective" (RCCL at
+        N > 1): ring the region's doorbell before the first all-reduce is
+        enqueued.  Otherwise ("hold") the gate opens after Gate.HOLD launches
+        as in every other config (_timed)."""
         self.torch, self.streams = torch, list(streams)
         reps, S = len(arenas), len(self.streams)
         assert reps >= 4
@@ -560,7 +573,7 @@ class FlowRunner:
                                                 wbytes, st.cuda_stream)
                 # never enqueue a collective behind an unrung doorbell
                 # (gate_policy "until_collective"): ring it first
-                if self._gate is not None:
+                if self._gate is not None and open_before_collective:
                     self._gate.open()
                 w = reduce_fn(hist)
             if w is not None:
@@ -916,6 +929,9 @@ def gate_policy(flows: bool, world: int, backend: str, no_gate: bool) -> str:
     return "hold"
 
 
+T_START = time.perf_counter()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -939,7 +955,9 @@ def main():
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the live host-inclusive (PCIe) measurement")
     ap.add_argument("--no-sublines", action="store_true",
-                    help="c2: skip the C3 (mixed 64-1500 B) sub-line")
+                    help="c2: skip the sub-lines (--sublines)")
+    ap.add_argument("--sublines", default="c3,c4,c5",
+                    help="c2: the configs carried as sub-lines of the default line")
     ap.add_argument("--no-gate", action="store_true",
                     help="time from host submission (no doorbell-held first launches)")
     ap.add_argument("--stagger-us", type=float, default=None,
@@ -963,6 +981,7 @@ def main():
         args.streams = STREAMS.get(args.config, 2)
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
+    subline_names(args)  # a bad --sublines fails before any GPU work
 
     # --- one process per GPU: under a launcher (WORLD_SIZE set) its world
     # must be --gpus; without one, start the ranks here (nothing has touched
@@ -1006,22 +1025,58 @@ def main():
         ctx.set_tuning(getattr(abi, f"TUNE_{k.upper()}"), int(v))
     env = (torch, dist, ingot_amd, ingot_amd.load_library(), ctx, world, rank, local, dev)
     result = run_config(args, args.config, env)
-    # The metric names 64-1500 B frames: the default (c2) line carries the
-    # mixed-frame config (BASELINE.json configs[2]) as a sub-line of its own,
-    # timed by the same rules, with its own roofline and CPU baseline.
-    if args.config == "c2" and not args.no_sublines and not args.tune:
-        sub = argparse.Namespace(**vars(args))
-        sub.config, sub.streams, sub.record, sub.timing = "c3", STREAMS["c3"], 16, "launches"
-        sub.no_variants, sub.no_host_path = True, True
-        sub.stagger_us = None
-        r3 = run_config(sub, "c3", env)
-        if result is not None:
-            result["sublines"] = {"c3": r3}
+    # The metric names 64-1500 B frames, and BASELINE.json names four configs
+    # past C2: the default (c2) line carries C3 (configs[2], mixed frames),
+    # C4 (configs[3], VLAN/QinQ + IPv6 EHs) and C5 (configs[4], flows +
+    # histogram + the RCCL all-reduce at N > 1) as sub-lines, each timed by
+    # the same rules with its own roofline and CPU baseline.  C4 and C5 are
+    # weak-scaled at 8,388,608 frames per GPU: at N = 8 exactly the 64 M-frame
+    # jobs BASELINE.json names.
+    subs = run_sublines(args, env, run_config, torch.cuda.empty_cache)
+    if result is not None and subs is not None:
+        result["sublines"] = subs
+        result["wall_s_command"] = round(time.perf_counter() - T_START, 2)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def subline_names(args) -> list:
+    """The configs the default line carries as sub-lines (none for other
+    configs, --no-sublines or a --tune run)."""
+    if args.config != "c2" or args.no_sublines or args.tune:
+        return []
+    names = [c for c in args.sublines.split(",") if c]
+    bad = [c for c in names if c not in CONFIGS or c == "c2"]
+    if bad:
+        raise SystemExit(f"--sublines: unknown config(s) {bad}")
+    return names
+
+
+def run_sublines(args, env, run, release=lambda: None):
+    """Each sub-line is `run(sub_args, name, env)` with the main line's steps
+    and warm-up, the config's own stream count, 16-B records and no variants
+    or host path; every rank runs them in the same order (their barriers and
+    collectives pair up).  Returns {name: line} on rank 0, None elsewhere or
+    when there are none."""
+    names = subline_names(args)
+    if not names:
+        return None
+    out = {}
+    for name in names:
+        sub = argparse.Namespace(**vars(args))
+        sub.config, sub.streams, sub.record, sub.timing = name, STREAMS[name], 16, "launches"
+        sub.no_variants, sub.no_host_path = True, True
+        sub.stagger_us = None
+        t0 = time.perf_counter()
+        line = run(sub, name, env)
+        if line is not None:
+            line["wall_s_subline"] = round(time.perf_counter() - t0, 2)
+        out[name] = line
+        release()
+    return out if env[6] == 0 else None
 
 
 def run_config(args, config, env):
@@ -1097,7 +1152,8 @@ def run_config(args, config, env):
                               ring_outs if record == 16 else outs8, streams[0], record, group)
         if flows:
             return FlowRunner(torch, lib, ctx, chain, n, arenas, off, lens, hists, flow_ids,
-                              streams[:nstreams], idist.reduce_histogram_async, flows_only)
+                              streams[:nstreams], idist.reduce_histogram_async, flows_only,
+                              open_before_collective=policy == "until_collective")
         if mode == "modify":
             return ModifyRunner(torch, lib, ctx, chain, n, stride, arenas, off, lens,
                                 streams[:nstreams])
@@ -1158,6 +1214,10 @@ def run_config(args, config, env):
     if world > 1:
         dist.barrier()
     t_sec = idist.max_over_ranks(ms_region / 1e3, device=dev)
+    region_ms_per_rank = idist.gather_over_ranks(ms_region, device=dev)
+    if flows:  # the last timed step's reduced histogram and this rank's flow ids
+        last = (args.steps - 1) % reps
+        hist_last, fid_last = hists[last].clone(), flow_ids[last].clone()
     # every rank's frames: weak = n per rank; strong = the job's total
     frames_all = n_total
     value = frames_all * args.steps / t_sec / 1e6
@@ -1221,6 +1281,12 @@ def run_config(args, config, env):
     bytes_launch = (rd + wr) * per_launch
     achieved = bytes_launch / (launch_ms / 1e3) / 1e9
     ok_frac = float((recs_np["status"] == 0).mean())
+    hist_check = None
+    if flows:
+        ok_l3 = int(((recs_np["status"] == 0) & (recs_np["l3_kind"] != 0)).sum())
+        hist_check = idist.flow_hist_check(hist_last, fid_last, ok_l3, FLOW_BINS)
+        hist_check["step"] = args.steps - 1
+        del hist_last, fid_last
     # the multi-tile ring kernels serve slot rings without a length array
     # (launch_parse / launch_modify in parse.hip); everything else is k_parse
     ring_k = (mode in ("parse", "modify") and stride is not None and stride >= 64
@@ -1416,6 +1482,14 @@ def run_config(args, config, env):
             "write_bytes_per_batch": wr,
             "read_frac": round(rd * per_launch / (launch_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             "frac_of_measured_copy_ceiling": round(achieved / HBM_MEASURED_GBS, 4),
+        },
+        "distributed": {
+            **idist.world_info(),
+            "region_ms_per_rank": [round(x, 5) for x in region_ms_per_rank],
+            "collective": (f"all_reduce SUM of the {FLOW_BINS} x u32 flow histogram every step "
+                           f"({'RCCL' if args.dist_backend == 'nccl' else 'gloo'})"
+                           if flows and world > 1 else None),
+            "flow_hist_check": hist_check,
         },
         "ms_per_step_ungated": ungated,
         "variants": variants,

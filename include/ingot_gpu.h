@@ -411,10 +411,16 @@ void ingot_gpu_doorbell_destroy(ingot_gpu_doorbell* db);
  *     not yet known published, then invalidates its caches (system-scope
  *     acquire), so frames written by the host, a copy engine or another
  *     kernel after the launch started are seen.  A wave that waits more than
- *     `timeout_ms` (1..60000) for a batch stops: the batches from there on
- *     keep whatever their record buffers held, and *d_status (optional,
- *     device memory, caller-zeroed) gets bit 0 set.  Every launch therefore
- *     ends, rung or not.
+ *     `timeout_ms` (1..60000) for a batch stops, and *d_status (optional,
+ *     device memory, caller-zeroed) gets bit 0 set.  Waves give up one by
+ *     one: a wave that reaches the ring later may still see a batch published
+ *     and parse its tiles.  So when bit 0 is set, the record buffers of
+ *     EVERY batch from the first one not published at launch onward are
+ *     undefined (some tiles written, some not); batches published before the
+ *     launch are complete.  Every launch ends, rung or not.  Doorbell values
+ *     must increase monotonically across ring launches, db_first + nbatches
+ *     must fit in 32 bits (else INGOT_GPU_ERANGE), and `db` must belong to
+ *     ctx's device (else INGOT_GPU_EINVAL).
  * The arenas are read-only for the launch; a batch buffer must not be
  * rewritten while the launch may still read it (a ring reuses a slot only
  * after the launch that consumes it has completed).  Unlike a

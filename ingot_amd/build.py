@@ -20,7 +20,7 @@ ROOT = PKG.parent
 CSRC = PKG / "csrc"
 BUILD = PKG / "build"
 LIB = PKG / "lib" / "libingot_gpu.so"
-SOURCES = ["parse.hip", "read.hip", "ring.hip", "flow.hip", "header.hip", "packed.hip", "pktgen.hip", "stream.hip", "api.cpp"]
+SOURCES = ["parse.hip", "read.hip", "ring.hip", "flow.hip", "tuple.hip", "header.hip", "packed.hip", "pktgen.hip", "stream.hip", "api.cpp"]
 ARCH = "gfx950"
 
 

@@ -166,6 +166,11 @@ hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, int mode
 hipError_t launch_flows(const FlowArgs& a, int layout_kind, int chain, const Tuning& t,
                         hipStream_t s);
 hipError_t launch_ring(const RingArgs& a, int chain, int mode, const Tuning& t, hipStream_t s);
+// Flow classification with the 5-tuple's chunks past the plain parse's
+// window fetched by a compacted LDS-DMA pass (tuple.hip): offset-addressed
+// device frames, 16-bit table, not the tunnel chain.
+hipError_t launch_flows_tuple(const FlowArgs& a, int chain, int variant, const Tuning& t,
+                              hipStream_t s);
 // launch_parse's branches in their own files: parse_read over chunk lists
 // (read.hip; `a` with its cache policy set, `g` the one-tile-per-wave grid)
 // and the slot-ring kernels (ring.hip).

@@ -616,6 +616,10 @@ hipError_t launch_flows_mode(const FlowArgs& a, int layout_kind, int chain, cons
     // built per block (1,152 entries from the key windows), so its grid is
     // persistent; INGOT_TUNE_FLOW_KERNEL = 2 makes the 16-bit one persistent
     // too.  Fixed max_blocks: grid-stride over that many blocks.
+    // INGOT_TUNE_FLOW_KERNEL 4..7: the compacted 5-tuple fetch (tuple.hip)
+    if (H16 && t.flow_kernel >= 4 && layout_kind == LAYOUT_INDEXED && !t.host_arena &&
+        !t.window_indexed && chain != INGOT_CHAIN_GENEVE_OVER_V6)
+        return launch_flows_tuple(a, chain, t.flow_kernel, t, s);
     const uint32_t pc =
         t.max_blocks || (H16 && (t.flow_kernel == 0 || t.flow_kernel == 3)) ? 0u : t.cus;
     // INGOT_TUNE_FLOW_KERNEL = 1: the hash-overlapped kernel (k_flows) at the
@@ -715,7 +719,7 @@ bool tuning_valid(int key, int value) {
     case INGOT_TUNE_READ_PLAN:
         return (value >= 0 && value <= 16);
     case INGOT_TUNE_FLOW_KERNEL:
-        return value >= 0 && value <= 3;
+        return value >= 0 && value <= 8;
     default:
         return false;
     }

@@ -117,9 +117,15 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
         }
         // chunk 0, packet-major: instruction k, lane L fills slot 64k + L =
         // packet q / CS0, piece (q mod CS0) ^ swz (16-B aligned absolute
-        // addresses; pieces only below the chunk's end)
-        const uint32_t sh0 = (uint32_t)((uintptr_t)(a.arena + fr.o0) & 15u);
-        const int64_t base0 = (int64_t)fr.o0 - (int64_t)sh0;
+        // addresses; pieces only below the chunk's end).  Records never read
+        // the MAC addresses (the walk reads Ethernet's ethertype only), so, as
+        // in k_parse, the window starts at the piece holding chunk 0's byte
+        // SKIP = 12: a frame starting in the last 12 bytes of a 128-B line
+        // does not fetch that line.  Staged byte sh0 + j is chunk-0 byte
+        // SKIP + j.
+        constexpr uint32_t SKIP = MODE == OUT_REC16 ? INGOT_REC_SKIP : 0u;
+        const uint32_t sh0 = (uint32_t)((uintptr_t)(a.arena + fr.o0 + SKIP) & 15u);
+        const int64_t base0 = (int64_t)fr.o0 + (int64_t)SKIP - (int64_t)sh0;
         // chunk 0's window: CS0 pieces, or (a.linewin = m) a line-completing
         // window — at least m pieces, then to the end of that 128-B line
         // (k_parse's windows), at most CS0
@@ -130,7 +136,10 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
             if (want > (uint32_t)CS0) want = CS0;
         }
         const uint32_t wlim = 16u * want;
-        uint32_t ext = nseg ? sh0 + (fr.l0 < wlim - sh0 ? fr.l0 : wlim - sh0) : 0u;
+        // the window's end in staged bytes: chunk 0's end, or the window's
+        // (nothing when chunk 0 ends before byte SKIP)
+        const int64_t e0 = (int64_t)sh0 + (int64_t)fr.l0 - (int64_t)SKIP;
+        uint32_t ext = nseg && e0 > 0 ? (e0 < (int64_t)wlim ? (uint32_t)e0 : wlim) : 0u;
         // a later non-last chunk without planes that starts inside chunk 0's
         // window: stage the window's pieces up to its end (or the window's)
         auto widen = [&](uint32_t e, uint64_t o, uint32_t l) {
@@ -191,6 +200,13 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
         fr.b0 = base0;
         fr.span0 = 16u * n0;
         fr.enter(fr.o0, fr.l0, 0u, nseg ? want : 0u);
+        if constexpr (SKIP != 0) {
+            // chunk-0 byte i >= SKIP is staged byte i + sh0 - SKIP (mod 2^32);
+            // bytes [0, avail) count as staged (those below SKIP are never read)
+            fr.sh = sh0 - SKIP;
+            const uint32_t w0 = 16u * want + SKIP - sh0;
+            fr.avail = nseg ? (fr.l0 < w0 ? fr.l0 : w0) : 0u;
+        }
         Rec r;
         if constexpr (MODE == OUT_FIELDS) {
             using OutT = typename std::conditional<TUN, ingot_geneve_fields, ingot_fields>::type;

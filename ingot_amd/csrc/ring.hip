@@ -168,8 +168,9 @@ __global__ __launch_bounds__(BLOCK) void k_parse_ring(RingArgs a) {
     uint32_t avail = a.published;  // batches [0, avail) are known published
     bool live = true;              // false once this wave gave up waiting
 
-    // Batch b published?  Polls only past `avail`: one lane's system-scope
-    // load of the doorbell, sleeping between polls, until the word reaches
+    // Batch b published?  Polls only past `avail`: one system-scope load of
+    // the doorbell per wave (one request; every lane gets the word), with
+    // backoff sleeps between polls, until the word reaches
     // db_first + b or the wave's wait exceeds timeout_ticks.  On success the
     // wave's caches are invalidated (system-scope acquire) before it stages
     // the new batch, so frames written after the launch started are seen.
@@ -177,6 +178,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse_ring(RingArgs a) {
         if (b < avail) return true;
         if (!a.doorbell) return false;
         const uint64_t t0 = wall_clock64();
+        uint32_t naps = 1;  // exponential backoff: 1, 2, 4, 8 sleeps between polls
         for (;;) {
             const uint32_t v = load_system_u32(a.doorbell);
             if (v >= a.db_first + b) {
@@ -189,7 +191,11 @@ __global__ __launch_bounds__(BLOCK) void k_parse_ring(RingArgs a) {
                 if (a.status && lane == 0) atomicOr(a.status, 1u);
                 return false;
             }
-            __builtin_amdgcn_s_sleep(32);
+            // ~1 us per nap: a waiting wave polls the host word at most
+            // every ~8 us once the wait is long, so thousands of waiting
+            // waves do not flood PCIe while a producer publishes
+            for (uint32_t z = 0; z < naps; ++z) __builtin_amdgcn_s_sleep(32);
+            naps = naps < 8u ? 2u * naps : 8u;
         }
     };
     // Cursors of the next tile to stage and to parse: (batch, tile) and that

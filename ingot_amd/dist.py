@@ -47,6 +47,74 @@ def max_over_ranks(value: float, device=None) -> float:
     return float(t.item())
 
 
+def gather_over_ranks(value: float, device=None) -> list:
+    """Every rank's `value`, in rank order (all-gather; [value] at world 1)."""
+    import torch
+    import torch.distributed as dist
+
+    if not _active():
+        return [float(value)]
+    dev = None if _gloo() else device
+    t = torch.tensor([float(value)], dtype=torch.float64, device=dev)
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(x.item()) for x in out]
+
+
+def sum_over_ranks(t):
+    """In-place SUM of an int64 tensor across ranks (through host memory on
+    gloo); returns it.  World 1: unchanged."""
+    import torch.distributed as dist
+
+    if not _active():
+        return t
+    if _gloo() and t.is_cuda:
+        host = t.cpu()
+        dist.all_reduce(host, op=dist.ReduceOp.SUM)
+        t.copy_(host)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t
+
+
+def world_info() -> dict:
+    """What the process group itself reports (not what the launcher asked
+    for): world size and backend; world 1 without a process group."""
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized():
+        return {"world_size": dist.get_world_size(), "backend": str(dist.get_backend()),
+                "process_group": True}
+    return {"world_size": 1, "backend": None, "process_group": False}
+
+
+def flow_hist_check(hist, flow_ids, ok_l3_local: int, bins: int) -> dict:
+    """Config 5's reduce, checked after the timed region on the buffers of one
+    step: `hist` holds that step's histogram after the all-reduce, `flow_ids`
+    this rank's per-packet bins of the same step (-1 = not counted).  Checks
+    (1) the reduced histogram equals the all-reduce of every rank's bincount
+    of its flow ids, bin for bin, and (2) its total equals the all-reduced
+    count of Ok packets with an L3 layer (the packets the flow kernel counts,
+    from this rank's parse records)."""
+    import torch
+
+    fid = flow_ids.to(torch.int64)
+    counted = fid[fid >= 0]
+    ref = torch.bincount(counted, minlength=bins)[:bins].to(torch.int64)
+    sum_over_ranks(ref)
+    exp = torch.tensor([int(ok_l3_local), int(counted.numel())], dtype=torch.int64,
+                       device=ref.device)
+    sum_over_ranks(exp)
+    got = hist.view(torch.int32).to(torch.int64)
+    total = int(got.sum().item())
+    bins_equal = bool(torch.equal(got, ref))
+    ok_l3, counted_all = (int(x) for x in exp.tolist())
+    return {"hist_total": total, "ok_l3_packets_all_ranks": ok_l3,
+            "flow_ids_counted_all_ranks": counted_all,
+            "bins_equal_allreduced_bincount": bins_equal,
+            "ok": bins_equal and total == ok_l3 == counted_all}
+
+
 def reduce_histogram(hist):
     """In-place SUM of a per-rank flow histogram across ranks (RCCL all-reduce
     over xGMI on GPUs: 65,536 x u32 = 256 KiB, one ring pass).  torch has no

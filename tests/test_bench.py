@@ -289,7 +289,8 @@ def test_flow_runner_rings_the_doorbell_before_every_collective():
     hists = [_Hist(log, i) for i in range(reps)]
     r = bench.FlowRunner(_FakeTorch, _Lib(log), _Ctx(), Chain.VlanUlp, 8,
                          [_Buf(i) for i in range(reps)], _Buf(0), _Buf(0), hists,
-                         [_Buf(0)] * reps, [_Stream(), _Stream()], reduce_fn)
+                         [_Buf(0)] * reps, [_Stream(), _Stream()], reduce_fn,
+                         open_before_collective=True)
     r.run(6, gate=_LogGate())
     ops = [e[0] for e in log]
     assert ops[0] == "arm"
@@ -348,3 +349,70 @@ def test_runner_rotates_arenas_and_records_independently():
     assert [a for a, _, _ in calls] == [1000 + k % 8 for k in range(70)]
     assert [o for _, o, _ in calls] == [5000 + k % 64 for k in range(70)]
     assert [s for _, _, s in calls] == [k % 2 for k in range(70)]
+
+
+def test_flow_runner_hold_policy_opens_only_at_hold(monkeypatch):
+    """gate_policy "hold" (one GPU: no collective in the region): the doorbell
+    is rung after Gate.HOLD launches or in _timed's finally, never by the
+    runner after the first step — the region holds HOLD launches, as
+    config.timing says."""
+    monkeypatch.setattr(bench.Gate, "HOLD", 5)
+    log = []
+    reps = 4
+
+    class _LogGate:
+        def arm(self, streams):
+            log.append(("arm",))
+
+        def open(self):
+            log.append(("open",))
+
+    hists = [_Hist(log, i) for i in range(reps)]
+    bufs = [_Buf(i) for i in range(reps)]
+    r = bench.FlowRunner(_FakeTorch, _Lib(log), _Ctx(), Chain.VlanUlp, 8, bufs, _Buf(0),
+                         _Buf(0), hists, [_Buf(0)] * reps, [_Stream(), _Stream()],
+                         lambda h: None)
+    r.run(8, gate=_LogGate())
+    ops = [e[0] for e in log]
+    kernels_before_open = ops[:ops.index("open")].count("kernel")
+    assert kernels_before_open == 5  # exactly Gate.HOLD launches held
+    # a run shorter than HOLD: the only open is the finally
+    log.clear()
+    r.run(3, gate=_LogGate())
+    ops = [e[0] for e in log]
+    assert ops.count("open") == 1 and ops[-1] == "open" and ops.count("kernel") == 3
+
+
+def test_sublines_carry_c3_c4_c5_in_order():
+    """The default line's sub-lines: C3, C4, C5 (BASELINE configs[2..4]),
+    each with the main line's steps / warm-up and its own stream count, no
+    variants; rank 0 returns them, other ranks None; other configs, --tune
+    and --no-sublines carry none; unknown names fail early."""
+    import argparse
+
+    args = argparse.Namespace(config="c2", no_sublines=False, tune=[], sublines="c3,c4,c5",
+                              steps=20, warmup=5, streams=2, record=16, timing="launches",
+                              no_variants=False, no_host_path=False, stagger_us=None)
+    seen, released = [], []
+
+    def run(sub, name, env):
+        seen.append((name, sub.config, sub.steps, sub.warmup, sub.streams, sub.no_variants,
+                     sub.no_host_path, sub.record))
+        return None if env[6] else {"config": name}
+
+    env0 = (None,) * 6 + (0,)
+    out = bench.run_sublines(args, env0, run, lambda: released.append(1))
+    assert list(out) == ["c3", "c4", "c5"]
+    assert [s[0] for s in seen] == ["c3", "c4", "c5"]
+    assert all(s[1] == s[0] and s[2:4] == (20, 5) and s[5] and s[6] and s[7] == 16
+               for s in seen)
+    assert [s[4] for s in seen] == [bench.STREAMS[c] for c in ("c3", "c4", "c5")]
+    assert all("wall_s_subline" in v for v in out.values()) and len(released) == 3
+    seen.clear()
+    assert bench.run_sublines(args, (None,) * 6 + (1,), run) is None
+    assert len(seen) == 3  # every rank runs them (their collectives pair up)
+    for kw in ({"config": "c3"}, {"no_sublines": True}, {"tune": ["x=1"]}):
+        a = argparse.Namespace(**{**vars(args), **kw})
+        assert bench.subline_names(a) == []
+    with pytest.raises(SystemExit):
+        bench.subline_names(argparse.Namespace(**{**vars(args), "sublines": "c3,c9"}))

@@ -11,7 +11,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import oracle
-from ingot_amd import Chain, dist as idist
+from ingot_amd import REC_DTYPE, Chain, dist as idist
 from tests.frames import build_frames, pack
 
 N_PER_RANK = 1500
@@ -75,3 +75,62 @@ def test_histogram_allreduce_gloo(world):
     want, _ = oracle.flow_hist(arena, off, lens, Chain.VlanUlp, bins=4096)
     assert (hist == want).all()
     assert slowest == 0.5 + (world - 1)
+
+
+def _check_worker(rank, world, port, q):
+    """bench.py's C5 checks at world 2: the per-rank region times, the
+    process group's own world size / backend, and the reduced histogram
+    against every rank's flow ids and Ok-with-L3 count."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        frames = build_frames(N_PER_RANK * world, seed=321)
+        first, n = idist.shard(rank, world, N_PER_RANK)
+        arena, off, lens = pack(frames[first:first + n])
+        bins = 4096
+        hist, _ = oracle.flow_hist(arena, off, lens, Chain.VlanUlp, bins=bins)
+        fids = torch.from_numpy(oracle.flow_hist.last_flows.view(np.int32).copy())
+        recs = oracle.parse_batch(arena, off, lens, Chain.VlanUlp).view(REC_DTYPE)
+        ok_l3 = int(((recs["status"] == 0) & (recs["l3_kind"] != 0)).sum())
+        h = torch.from_numpy(hist.astype(np.uint32).view(np.int32).copy())
+        idist.reduce_histogram(h)
+        good = idist.flow_hist_check(h, fids, ok_l3, bins)
+        bad_h = h.clone()
+        bad_h[7] += 1
+        bad = idist.flow_hist_check(bad_h, fids, ok_l3, bins)
+        times = idist.gather_over_ranks(1.0 + 0.25 * rank)
+        info = idist.world_info()
+        if rank == 0:
+            q.put((good, bad, times, info))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_flow_hist_check_and_rank_report_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_check_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    good, bad, times, info = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert good["ok"] and good["bins_equal_allreduced_bincount"]
+    assert good["hist_total"] == good["ok_l3_packets_all_ranks"] == \
+        good["flow_ids_counted_all_ranks"] > 0
+    assert not bad["ok"] and not bad["bins_equal_allreduced_bincount"]
+    assert times == [1.0, 1.25]
+    assert info == {"world_size": 2, "backend": "gloo", "process_group": True}
+
+
+def test_rank_report_world_one():
+    assert idist.gather_over_ranks(3.5) == [3.5]
+    assert idist.world_info()["world_size"] == 1
+    h = torch.tensor([2, 0, 1], dtype=torch.int32)
+    f = torch.tensor([0, -1, 0, 2], dtype=torch.int32)
+    r = idist.flow_hist_check(h, f, 3, 3)
+    assert r["ok"] and r["hist_total"] == 3

@@ -184,3 +184,19 @@ def test_ring_doorbell_timeout_ends_the_launch(torch):
         assert outs[b].cpu().numpy().tobytes() == _want(arenas[b], Chain.UdpParser, 64, n).tobytes()
     assert bool((outs[2] == 0xAB).all())
     db.close()
+
+
+def test_ring_doorbell_argument_checks(torch):
+    """db_first + nbatches must fit the kernel's 32-bit comparison (ERANGE);
+    nothing is launched."""
+    ctx = ingot_amd.Context(0)
+    n = 4096
+    arenas = _batches(torch, GenProfile.V4UDP64, n, 64, 2, seed=5)
+    outs = [torch.full((n, 16), 0xAB, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    db = ingot_amd.Doorbell(ctx)
+    with pytest.raises(RuntimeError, match=r"\(-?\d+\)"):
+        ctx.parse_ring(arenas, 64, n, Chain.UdpParser, outs, doorbell=db,
+                       db_first=0xFFFFFFFF, timeout_ms=100)
+    torch.cuda.synchronize()
+    assert all(bool((o == 0xAB).all()) for o in outs)
+    db.close()
