@@ -84,6 +84,12 @@ MODES = {"c5": "flows", "c2m": "modify", "c3r": "read", "c3p": "packed", "c2r": 
 # parse_read chunking: "split2" = header span | payload; "per_header" = one
 # chunk per parsed header, then the payload (the reference bench's shape)
 READ_CHUNKS = {"c3r": "split2", "c2r": "per_header"}
+# parse_read configs timed with chunk 0's descriptor per packet (the mblk
+# chain's head, which a packet ring carries: ingot_gpu_parse_read_first).
+# c3r: 604 -> 567 us per step (round 4); c2r (one chunk per header, widened
+# into chunk 0's window) gains nothing from it (18.2 vs 18.8 us, round 3), so
+# it times the chunk table.
+READ_FIRST = {"c3r"}
 # Strong scaling (--scaling strong): the whole job's frames, split over the
 # ranks (BASELINE.json configs[3]: 64 M frames over 8 GPUs); other configs
 # split their single-GPU batch.
@@ -100,7 +106,7 @@ STREAMS = {"c2": 2, "c2m": 2, "c3": 1, "c3p": 1, "c3r": 1, "c3s": 3, "c4": 1, "c
 # i * STAGGER_US behind stream 0 (ingot_gpu_stream_delay), so the streams'
 # launches do not ramp up and drain in lockstep.  0 = start together.
 # Measured (tools/stagger_ab.py, interleaved, 20-step regions after a 5-step
-# warm-up as the driver runs them; profiles/r02_stagger_ab.json): C2 12.32-12.38
+# warm-up as the driver runs them; history/profiles/r02_stagger_ab.json): C2 12.32-12.38
 # -> 12.18-12.20 us/step at 5-7 us, 12.5 at 12 us; 200-step regions unchanged.
 STAGGER_US = {"c2": 6.0}
 FLOW_BINS = 1 << 16
@@ -194,6 +200,39 @@ def host_cpu_share():
                      "effective_cpus": n}
 
 
+def physical_core_pick(cpus, want):
+    """One CPU per physical core among `cpus` (SMT siblings dropped: a
+    sibling shares its core's pipelines), spread round-robin over the L3
+    domains (CCDs) so that workers do not crowd one CCD's cache, up to
+    `want`.  Returns (picked cpus, description).  Falls back to `cpus` in
+    order when sysfs has no topology."""
+    def rd(c, rel):
+        return _read(f"/sys/devices/system/cpu/cpu{c}/{rel}")
+
+    cores, order = {}, []
+    for c in cpus:
+        pkg, core = rd(c, "topology/physical_package_id"), rd(c, "topology/core_id")
+        if pkg is None or core is None:
+            return list(cpus[:want]), {"topology": "unavailable"}
+        key = (pkg, rd(c, "topology/die_id"), core)
+        if key not in cores:
+            cores[key] = (c, rd(c, "cache/index3/id") or pkg)
+            order.append(key)
+    by_l3 = {}
+    for key in order:
+        c, l3 = cores[key]
+        by_l3.setdefault(l3, []).append(c)
+    picked, queues = [], [list(v) for v in by_l3.values()]
+    while len(picked) < want and any(queues):
+        for q in queues:
+            if q and len(picked) < want:
+                picked.append(q.pop(0))
+    used_l3 = {cores[k][1] for k in order if cores[k][0] in picked}
+    return picked, {"topology": "sysfs", "physical_cores_available": len(order),
+                    "physical_cores_used": len(picked), "l3_domains_used": len(used_l3),
+                    "smt_siblings_skipped": len(cpus) - len(order)}
+
+
 def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode="parse",
                  segs=None):
     """Time the oracle (the C restatement of ingot's parse) on the host's
@@ -224,7 +263,18 @@ def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode
             oracle.parse_batch(arena_np, off_np, lens_np, chain, stride=stride, n=n,
                                nthreads=t, lib=lib)
 
-    cpus, share = host_cpu_share()
+    allowed, share = host_cpu_share()
+    # One worker per physical core of the allowed set, one core short of a
+    # CPU quota: the quota is charged for this process's other threads too
+    # (the HIP runtime's), and workers filling it exactly get throttled
+    # mid-run — the round-3 spread (0.18) came from that and from SMT
+    # siblings sharing a core.
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else allowed
+    want = len(allowed)
+    if share["cpu_quota"] is not None and share["cpu_quota"] < len(aff):
+        want = max(1, min(len(allowed), int(share["cpu_quota"]) - 1))
+    cpus, topo = physical_core_pick(aff, want)
+    share = {**share, **topo, "quota_headroom_cpus": len(allowed) - len(cpus)}
     pin = (ctypes.c_int * len(cpus))(*cpus)
     lib.oracle_set_affinity(ctypes.cast(pin, ctypes.c_void_p), len(cpus))
 
@@ -247,18 +297,19 @@ def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode
 
     try:
         single = measure(1, budget_s / 2)
-        runs = sorted((measure(len(cpus), budget_s / 3) for _ in range(3)), key=lambda r: r[0])
+        runs = sorted((measure(len(cpus), budget_s / 5) for _ in range(5)), key=lambda r: r[0])
     finally:
         lib.oracle_set_passes(1)
         lib.oracle_set_affinity(None, 0)
-    mp, reps, el = runs[1]
-    spread = (runs[2][0] - runs[0][0]) / mp if mp else 0.0
+    mp, reps, el = runs[2]
+    spread = (runs[-1][0] - runs[0][0]) / mp if mp else 0.0
     what = {"parse": "parse_slice", "read": "parse_read", "modify": "parse + set_destination"}
     return {
         "value": round(mp, 3), "unit": "Mpkt/s", "cores": len(cpus), "kind": "port",
         "sample": f"{reps} passes x {n} frames of the benchmark batch (same bytes), "
                   f"{el:.2f} s wall on {len(cpus)} threads, each pinned to one of the CPUs "
-                  f"this process may use (affinity capped by the cgroup CPU quota); median of 3 "
+                  f"this process may use, one per physical core across the L3 domains, one short of "
+                  f"the cgroup CPU quota; median of 5 "
                   f"runs; each thread repeats its share, cache-resident after the first pass; "
                   f"C restatement of ingot {what.get(mode, mode)} (oracle/), -march={arch}",
         "single_core_value": round(single[0], 3),
@@ -1145,8 +1196,10 @@ def run_config(args, config, env):
         seg_off, seg_len, pkt_seg, head_chunks = read_chunks(
             torch, off, stride, rlens.to(torch.int32), recs0, READ_CHUNKS[config], dev)
 
+    read_first = config in READ_FIRST
+
     def runner(nstreams, record, flows_only=False, dense=False, ring=False, group=G,
-               first=False):
+               first=read_first):
         if ring:
             return RingRunner(torch, lib, ctx, chain, n, stride, arenas,
                               ring_outs if record == 16 else outs8, streams[0], record, group)
@@ -1162,7 +1215,7 @@ def run_config(args, config, env):
                                 streams[:nstreams])
         if mode == "read":
             return ReadRunner(torch, lib, ctx, chain, n, arenas, seg_off, seg_len, pkt_seg,
-                              outs, streams[:nstreams], dense, first)
+                              outs, streams[:nstreams], dense, first and not dense)
         return Runner(torch, lib, ctx, chain, n, stride, arenas, off, lens, outs,
                       streams[:nstreams], record)
 
@@ -1236,8 +1289,11 @@ def run_config(args, config, env):
     if mode == "read":
         # the header chunks read like a frame of the header span's length;
         # descriptors: pkt_seg (4 B) + (u64 off, u16 len) per header chunk
+        # (read_first: chunk 0's 8-B (offset << 16) | length per packet
+        # instead of its table entry, later header chunks from the table)
         hc = head_chunks.cpu().numpy().astype(np.int64)
-        rd, wr = algorithmic_bytes(recs_np, recs_np["payload_off"], 0, 4 + 10 * hc, 16)
+        desc = 4 + 8 + 10 * np.maximum(hc - 1, 0) if read_first else 4 + 10 * hc
+        rd, wr = algorithmic_bytes(recs_np, recs_np["payload_off"], 0, desc, 16)
     elif mode == "packed":
         # descriptors: the u16 length, read by the parse and once more by the
         # tile-sum pass; tile sums and bases: 12 B per 64 packets
@@ -1365,11 +1421,13 @@ def run_config(args, config, env):
             variants[f"streams{args.streams}_dense_table"] = {
                 "value": round(n * vsteps / (ms / 1e3) / 1e6, 2),
                 "us_per_step": round(ms * 1e3 / vsteps, 3)}
-            # chunk 0's descriptor per packet (ingot_gpu_parse_read_first)
-            r = runner(args.streams, 16, first=True)
+            # the other descriptor form: chunk 0 from the table
+            # (ingot_gpu_parse_read) / per packet (ingot_gpu_parse_read_first)
+            r = runner(args.streams, 16, first=not read_first)
             r.run(min(args.warmup, 50))
             ms, _ = r.run(vsteps, gate)
-            variants[f"streams{args.streams}_first_chunk_inline"] = {
+            variants[f"streams{args.streams}_" +
+                     ("chunk_table" if read_first else "first_chunk_inline")] = {
                 "value": round(n * vsteps / (ms / 1e3) / 1e6, 2),
                 "us_per_step": round(ms * 1e3 / vsteps, 3)}
             del r
@@ -1418,7 +1476,8 @@ def run_config(args, config, env):
         cpu = cpu_baseline(a_np, o_np, l_np, stride or 0, m, chain, args.cpu_budget,
                            mode="parse" if flows else mode, segs=segs)
     kname = {"modify": ", parse + setters",
-             "read": ", LAYOUT_SEGMENTED (parse_read)",
+             "read": ", LAYOUT_SEGMENTED (parse_read" +
+                     (", chunk 0 per packet: ingot_gpu_parse_read_first)" if read_first else ")"),
              "packed": ", LAYOUT_PACKED + k_tile_sums/k_group_scan",
              "flows": ", OUT_FLOWS16 (parse + Toeplitz hash; the step adds "
                       "k_flow_count16 / k_flow_reduce16)"}.get(mode, "")
@@ -1441,7 +1500,11 @@ def run_config(args, config, env):
             "frames_per_gpu": n,
             "frames_total": n_total,
             "chain": chain_name,
-            "layout": f"strided {stride} B" if stride else "packed, u64 offsets + u16 lengths",
+            "layout": (("chunk lists: u32 pkt_seg bounds, u64 seg_off + u16 seg_len per chunk" +
+                        ("; chunk 0 as one u64 (offset << 16) | length per packet"
+                         if read_first else "") + f" ({READ_CHUNKS[config]})")
+                       if mode == "read" else
+                       f"strided {stride} B" if stride else "packed, u64 offsets + u16 lengths"),
             "record_bytes": args.record,
             "streams": streams_n,
             "arena_copies_rotated": reps,

@@ -503,7 +503,11 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              lane from L2/HBM (default), 1 = ballot the
  *                              lanes whose chain outruns the window, re-stage
  *                              a window twice as large for just those frames
- *                              (compacted) and walk them again
+ *                              (compacted) and walk them again; 2 = fetch
+ *                              only the (up to 4) chunks right after those
+ *                              lanes' windows into image slots no lane needs
+ *                              any more (ballot + prefix scan) and re-walk
+ *                              them from LDS (resume-style)
  *   INGOT_TUNE_READ_PLAN       ingot_gpu_parse_read (16-B records): 16-B
  *                              pieces staged in LDS for each of a packet's
  *                              first four chunks (a packet's last chunk, the

@@ -74,7 +74,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
     constexpr uint32_t SKIP =
         NCH == 0 ? 0u
         : FLOWS && LAYOUT == LAYOUT_INDEXED && !TUN ? INGOT_FLOW_SKIP
-        : RECM && !SLOW && (LAYOUT == LAYOUT_INDEXED || LAYOUT == LAYOUT_PACKED) ? INGOT_REC_SKIP
+        : RECM && SLOW != 1 && (LAYOUT == LAYOUT_INDEXED || LAYOUT == LAYOUT_PACKED) ? INGOT_REC_SKIP
                                                                                   : 0u;
     static_assert(SKIP <= 12u, "the walk reads the ethertype at frame byte 12");
 
@@ -189,7 +189,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
         static_assert(!SLOW || (LAYOUT == LAYOUT_INDEXED && MODE == OUT_REC16),
                       "the compacted slow path is built for indexed 16-B records");
         using FR = typename std::conditional<LAYOUT == LAYOUT_SEGMENTED, SegFrame<NCH>,
-                                             Frame<NCH, SLOW != 0>>::type;
+                                             Frame<NCH, SLOW == 1>>::type;
         FR fr;
         fr.win = (const lds_u32*)wimg;
         fr.p = lane;
@@ -260,9 +260,12 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
                 args.flow[i] = counted ? (h & args.bin_mask) : INGOT_FLOW_NONE;
                 if (args.hash) args.hash[i] = h;
             }
+        } else if constexpr (SLOW == 2) {
+            ext_walk<NCH, CHAIN>(valid, wimg, lane, a.arena, base, nch, sh - SKIP, take, len,
+                                 a.arena + off, static_cast<uint4*>(a.out) + i, a.policy);
         } else {
             walk<CHAIN, false>(fr, r, nullptr, nullptr);
-            if constexpr (SLOW)
+            if constexpr (SLOW == 1)
                 slow_rewalk<NCH, CHAIN>(fr, r, valid, wimg, lane, a.arena, base, sh, len);
             if (valid) store_rec(static_cast<uint4*>(a.out) + i, pack(r), a.policy);
         }
@@ -450,7 +453,7 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
     // costs 19% (C3) / 15% (C3s).  The ring kernel's 16-B records are stored
     // at device scope (`sc1`, written through the XCD's L2) instead of nt:
     // 2 streams 12.32 -> 11.90 us/step, 1 stream 15.33 -> 15.19 (interleaved
-    // A/B, profiles/r02_store_scope_ab.json); 8-B records, the rewrite ring
+    // A/B, history/profiles/r02_store_scope_ab.json); 8-B records, the rewrite ring
     // and the packed / slotted kernels gain nothing from it (or lose: C3 sc1
     // without nt 588 -> 608 us).  4 = plain loads and stores.
     const bool ring = t.pipeline != 1 && !t.window_strided && layout_kind == LAYOUT_STRIDED &&
@@ -506,7 +509,7 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
     // evicted by then.  PMC read bytes per C3 frame: fixed 2 chunks 217,
     // 3 chunks 206, line-completing 172 — the line floor of the walk's bytes
     // is 169 (tools/line_floor.py); us per launch C3 562 -> 544, C3p 583 ->
-    // 553, C4 302 -> 288 (round 2, interleaved; profiles/r02_window_ab.json).
+    // 553, C4 302 -> 288 (round 2, interleaved; history/profiles/r02_window_ab.json).
     // The tunnel chain's records (outer headers ~80 B, the inner chain past
     // them) take at least 6 chunks, then to the line end, at most 9: C6 400 ->
     // 394 us (fixed 8; a minimum of 2 loses: 468).  Field and rewrite modes
@@ -545,6 +548,12 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
     if (t.slow_path == 1 && mode == OUT_REC16 && !host && !t.window_indexed)
         return tun ? launch_chain<8, LAYOUT_INDEXED, OUT_REC16, ParseArgs, 1>(a, chain, g, s)
                    : launch_chain<3, LAYOUT_INDEXED, OUT_REC16, ParseArgs, 1>(a, chain, g, s);
+    // The resume-style slow path (INGOT_TUNE_SLOW_PATH = 2): the default
+    // line-completing windows, then only the missing chunks (ext_rewalk)
+    if (t.slow_path == 2 && mode == OUT_REC16 && !host && !t.window_indexed &&
+        layout_kind == LAYOUT_INDEXED)
+        return tun ? launch_chain<9, LAYOUT_INDEXED, OUT_REC16, ParseArgs, 2>(a, chain, g, s)
+                   : launch_chain<5, LAYOUT_INDEXED, OUT_REC16, ParseArgs, 2>(a, chain, g, s);
     switch (wi ? wi : tun ? 8 : host ? 5 : 3) {
     case 100: return launch_mode<0, LAYOUT_INDEXED>(a, chain, mode, g, s);
     case 2: return launch_mode<2, LAYOUT_INDEXED>(a, chain, mode, g, s);
@@ -612,7 +621,7 @@ hipError_t launch_flows_mode(const FlowArgs& a, int layout_kind, int chain, cons
     // one 16-B load per thread), so the default grid is one tile per wave like
     // the plain parse, the hardware dispatcher refilling CUs as blocks finish:
     // C5 flows kernel 314.8 us vs 329.5 persistent (plain parse of the same
-    // frames 312.8; profiles/r02_flows_grid_ab.json).  The 32-bit table is
+    // frames 312.8; history/profiles/r02_flows_grid_ab.json).  The 32-bit table is
     // built per block (1,152 entries from the key windows), so its grid is
     // persistent; INGOT_TUNE_FLOW_KERNEL = 2 makes the 16-bit one persistent
     // too.  Fixed max_blocks: grid-stride over that many blocks.
@@ -643,7 +652,7 @@ hipError_t launch_flows_mode(const FlowArgs& a, int layout_kind, int chain, cons
     // Device arenas: a line-completing window of 4 to 5 chunks (the 5-tuple
     // of an untagged v4 frame ends 26 B past byte 12's chunk, a v6 one 46 B):
     // C5 flows kernel 330 -> 326 us (fixed 5; 4 to 6 chunks 367, 3 to 5 392;
-    // round 2, interleaved, profiles/r02_window_ab.json).
+    // round 2, interleaved, history/profiles/r02_window_ab.json).
     int wi = t.window_indexed;
     if (!wi && !t.host_arena && layout_kind == LAYOUT_INDEXED) wi = 1045;
     if (wi > 20 && wi != 100) {  // line-completing windows (ParseArgs::linewin)
@@ -715,11 +724,11 @@ bool tuning_valid(int key, int value) {
     case INGOT_TUNE_FLOW_TABLE:
         return value == 0 || value == 16 || value == 32;
     case INGOT_TUNE_SLOW_PATH:
-        return value == 0 || value == 1;
+        return value >= 0 && value <= 2;
     case INGOT_TUNE_READ_PLAN:
         return (value >= 0 && value <= 16);
     case INGOT_TUNE_FLOW_KERNEL:
-        return value >= 0 && value <= 8;
+        return value >= 0 && value <= 9;
     default:
         return false;
     }

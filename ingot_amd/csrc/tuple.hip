@@ -276,7 +276,8 @@ hipError_t go_tuple(const FlowArgs& a, int chain, uint32_t g, hipStream_t s) {
 // (launch_flows checks).  variant (INGOT_TUNE_FLOW_KERNEL): 4 = EARLY, 5
 // chunks (the plain parse's window), 64 overflow slots; 5 = EARLY, 4 chunks;
 // 6 = LATE, 5 chunks; 7 = EARLY, 5 chunks, 128 overflow slots; 8 = LATE,
-// 5 chunks, each lane's missing chunks in its own window image's free slots.
+// 5 chunks, each lane's missing chunks in its own window image's free slots;
+// 9 = 8 with 4-chunk windows (the table then fits 8 blocks per CU).
 hipError_t launch_flows_tuple(const FlowArgs& args, int chain, int variant, const Tuning& t,
                               hipStream_t s) {
     FlowArgs a = args;
@@ -287,6 +288,7 @@ hipError_t launch_flows_tuple(const FlowArgs& args, int chain, int variant, cons
     case 6: return go_tuple<5, 64, false>(a, chain, g, s);
     case 7: return go_tuple<5, 128, true>(a, chain, g, s);
     case 8: return go_tuple<5, 0, false>(a, chain, g, s);
+    case 9: return go_tuple<4, 0, false>(a, chain, g, s);
     default: return go_tuple<5, 64, true>(a, chain, g, s);
     }
 }

@@ -1190,6 +1190,156 @@ __device__ __forceinline__ void slow_rewalk(const Frame<NCH, true>& fr, Rec& r, 
     }
 }
 
+// A lane's frame over its window plus up to EXT_MAX extension chunks staged
+// in other slots of the wave's image (ext_walk): staged chunk c < nch is the
+// lane's own slot_of(p, c), chunk nch + e is image slot q[e].  Bytes past
+// `avail` are read from L2/HBM as in Frame.
+constexpr uint32_t EXT_MAX = 4;
+template <uint32_t NCH>
+struct FrameExt {
+    static constexpr bool kRead = false;
+    static constexpr bool kProbe = false;
+    const lds_u32* win;
+    uint32_t p, sh, avail, len;  // as Frame; avail covers the extension too
+    const uint8_t* g;
+    uint32_t nch, q0, q1, q2, q3;  // window chunks; the extension's image slots
+
+    __device__ __forceinline__ uint32_t dw(uint32_t b) const {
+        const uint32_t c = b >> 4;
+        const uint32_t e = c - nch;
+        const uint32_t slot = c < nch ? slot_of<NCH>(p, c)
+                              : e == 0u ? q0 : e == 1u ? q1 : e == 2u ? q2 : q3;
+        return win[slot * 4u + ((b >> 2) & 3u)];
+    }
+    __device__ __forceinline__ uint32_t be(uint32_t i, uint32_t n) const {
+        if (i + n <= avail) {
+            const uint32_t b = sh + i;
+            const uint32_t a = b & ~3u;
+            const uint32_t d0 = dw(a);
+            const uint32_t d1 = ((b & 3u) + n > 4u) ? dw(a + 4u) : 0u;
+            return __builtin_bswap32(__builtin_amdgcn_alignbyte(d1, d0, b & 3u)) >> (32u - 8u * n);
+        }
+        uint32_t v = 0;
+        for (uint32_t k = 0; k < n; ++k) v = (v << 8) | g[i + k];
+        return v;
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t hdr, Field f) const {
+        return (be(hdr + f.byte0(), f.nbytes()) >> f.rshift()) & f.mask();
+    }
+};
+
+// The resume-style slow path (INGOT_TUNE_SLOW_PATH = 2).
+// Pass 1 walks every lane over its window, probing.  The lanes whose chain
+// ran past it (ballot) need the chunks right after their window: up to
+// EXT_MAX, not past the frame.  Those chunks only are fetched (the window is
+// not re-staged) into image slots nobody needs any more — every slot of a
+// lane whose walk finished, and a missing lane's own slots past its window:
+// row k of the image is ballot-scanned for free slots (running count of the
+// earlier rows + popcount of the row's ballot below the lane = the slot's
+// rank among free slots), and free slot F receives extension chunk F of the
+// wave (owner lane: binary search over the inclusive prefix scan of the
+// lanes' chunk counts).  One LDS-DMA instruction per image row.  Pass 2
+// re-walks the missing lanes from LDS (window + extension), bytes past both
+// from L2/HBM.
+template <uint32_t NCH, int CHAIN>
+__device__ __forceinline__ void ext_walk(bool valid, uint32_t* wimg, uint32_t lane,
+                                         const uint8_t* arena, int64_t base, uint32_t nch,
+                                         uint32_t sh, uint32_t take, uint32_t len,
+                                         const uint8_t* g, uint4* out, uint32_t pol) {
+    bool miss;
+    {   // pass 1: probe the window; a lane done walking stores its record
+        // now, so no record stays live across the fetch and pass 2
+        Frame<NCH, true> f{(const lds_u32*)wimg, lane, sh, take, len, g};
+        Rec r;
+        walk<CHAIN, false>(f, r, nullptr, nullptr);
+        miss = valid && f.miss;
+        if (valid && !miss) store_rec(out, pack(r), pol);
+    }
+    const uint64_t M = __ballot(miss);
+    if (!M) return;
+    uint32_t m = 0;
+    if (miss) {
+        const uint32_t last = (sh + len - 1u) >> 4;  // staged chunk of the frame's last byte
+        const uint32_t rest = last + 1u > nch ? last + 1u - nch : 0u;
+        m = rest < EXT_MAX ? rest : EXT_MAX;
+    }
+    uint32_t x = m;  // inclusive prefix scan of the counts
+#pragma unroll
+    for (uint32_t d = 1; d < WAVE; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d);
+        if (lane >= d) x += y;
+    }
+    const uint32_t S = x - m;
+    const uint32_t TOT = (uint32_t)__shfl((int)x, (int)(WAVE - 1u));
+    // every lane's reads of the image have returned before LDS-DMA reuses it
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint64_t rowB[NCH];     // free-slot ballot of each image row (wave-uniform)
+    uint32_t cum[NCH + 1];  // free slots in the rows before k (wave-uniform)
+    cum[0] = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < NCH; ++k) {
+        const uint32_t q = k * WAVE + lane;
+        const uint32_t pp = q / NCH;
+        const uint32_t c = (q - pp * NCH) ^ swz<NCH>(pp);
+        const uint32_t np = (uint32_t)__shfl((int)nch, (int)pp);
+        const bool free = !((M >> pp) & 1ull) || c >= np;
+        const uint64_t B = __ballot(free);
+        rowB[k] = B;
+        const uint32_t F = cum[k] + (uint32_t)__popcll(B & lt);
+        cum[k + 1] = cum[k] + (uint32_t)__popcll(B);
+        if (cum[k] < TOT) {  // wave-uniform
+            uint32_t j = 0;  // owner: the first lane whose inclusive count exceeds F
+#pragma unroll
+            for (uint32_t s2 = WAVE / 2; s2; s2 >>= 1) {
+                const uint32_t v = (uint32_t)__shfl((int)x, (int)(j + s2 - 1u));
+                if (v <= F) j += s2;
+            }
+            j = j < WAVE ? j : WAVE - 1u;
+            const uint32_t sj = (uint32_t)__shfl((int)S, (int)j);
+            const uint32_t nj = (uint32_t)__shfl((int)nch, (int)j);
+            const int64_t bj = (int64_t)__shfl((long long)base, (int)j);
+            if (free && F < TOT)
+                stage16(arena + bj + 16u * (nj + F - sj), wimg + k * WAVE * 4u, false);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!miss) return;
+    // image slot of free slot t: its row (cum) and its set bit in the row
+    auto free_slot = [&](uint32_t t) -> uint32_t {
+        uint32_t k = 0, c0 = 0;
+        uint64_t B = rowB[0];
+#pragma unroll
+        for (uint32_t kk = 1; kk < NCH; ++kk) {
+            const bool in = t >= cum[kk];
+            k = in ? kk : k;
+            B = in ? rowB[kk] : B;
+            c0 = in ? cum[kk] : c0;
+        }
+        return k * WAVE + nth_set_bit(B, t - c0);
+    };
+    // chunks placed for this lane (all of them unless the free slots ran out)
+    const uint32_t placed = S + m <= cum[NCH] ? m : (cum[NCH] > S ? cum[NCH] - S : 0u);
+    FrameExt<NCH> f;
+    f.win = (const lds_u32*)wimg;
+    f.p = lane;
+    f.sh = sh;
+    f.len = len;
+    f.g = g;
+    f.nch = nch;
+    f.q0 = placed > 0u ? free_slot(S) : 0u;
+    f.q1 = placed > 1u ? free_slot(S + 1u) : 0u;
+    f.q2 = placed > 2u ? free_slot(S + 2u) : 0u;
+    f.q3 = placed > 3u ? free_slot(S + 3u) : 0u;
+    const uint32_t end = 16u * (nch + placed) - sh;  // staged byte sh + i = frame byte i
+    f.avail = end < len ? end : len;
+    // pass 2: the missing lanes, from the window and the extension
+    Rec r;
+    walk<CHAIN, false>(f, r, nullptr, nullptr);
+    store_rec(out, pack(r), pol);
+}
+
 // Blocks of `kernel` one CU holds at once (its LDS / VGPR footprint), queried
 // once per (kernel instance, device).  Keyed by the kernel's address: every
 // k_parse<..., ARGS> instance has the same function type, and their LDS

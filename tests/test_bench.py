@@ -416,3 +416,26 @@ def test_sublines_carry_c3_c4_c5_in_order():
         assert bench.subline_names(a) == []
     with pytest.raises(SystemExit):
         bench.subline_names(argparse.Namespace(**{**vars(args), "sublines": "c3,c9"}))
+
+
+def test_physical_core_pick_skips_smt_and_spreads_over_l3(monkeypatch):
+    """cpu_baseline's pinning: one CPU per physical core (SMT sibling
+    dropped), round-robin over L3 domains (CCDs), capped at `want`."""
+    # 2 CCDs x 4 cores x 2 threads: cpu c and c + 8 are siblings; CCD = core // 4
+    def fake(path):
+        parts = str(path).split("/")
+        c = int(parts[5][3:])
+        core = c % 8
+        rel = "/".join(parts[6:])
+        return {"topology/physical_package_id": "0", "topology/die_id": "0",
+                "topology/core_id": str(core), "cache/index3/id": str(core // 4)}.get(rel)
+
+    monkeypatch.setattr(bench, "_read", fake)
+    picked, info = bench.physical_core_pick(list(range(16)), 6)
+    assert len(picked) == 6 and len({c % 8 for c in picked}) == 6  # distinct cores
+    assert all(c < 8 for c in picked)  # first thread of each core
+    assert {c // 4 for c in picked[:2]} == {0, 1}  # alternate CCDs
+    assert info["physical_cores_available"] == 8 and info["smt_siblings_skipped"] == 8
+    assert info["l3_domains_used"] == 2
+    monkeypatch.setattr(bench, "_read", lambda p: None)
+    assert bench.physical_core_pick([3, 1, 2], 2)[0] == [3, 1]

@@ -24,7 +24,7 @@ import subprocess
 import sys
 from pathlib import Path
 
-ROOT = Path(__file__).resolve().parent.parent
+ROOT = Path(__file__).resolve().parents[2]
 KERNELS = {"k_read": "stream_read", "k_reg": "stream_copy",
            "k_parse_pipe<4u, 2u, 0, 0>": "parse", "k_parse_pipe<4u, 2u, 0, 1>": "parse_rec8"}
 

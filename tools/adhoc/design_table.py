@@ -11,7 +11,7 @@ import argparse
 import json
 from pathlib import Path
 
-ROOT = Path(__file__).resolve().parent.parent
+ROOT = Path(__file__).resolve().parents[2]
 DESC = {
     "c2": "C2 1 M × 64 B slots, UdpParser", "c2m": "C2m parse-and-decr-v4 in place",
     "c2r": "C2r C2 frames as the reference's 4-chunk `parse_read`",

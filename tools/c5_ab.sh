@@ -10,6 +10,6 @@ for v in "$@"; do args+=(--variant "$v"); done
 mkdir -p gpurun_out
 timeout -k 10 240 python3 tools/c5_same_run.py --reps 10 "${args[@]}" \
     --out gpurun_out/${tag}_events.json > gpurun_out/${tag}_events.log 2>&1
-timeout -k 10 400 python3 tools/pmc_kernels.py --out gpurun_out/${tag}_pmc.json -- \
+timeout -k 10 400 python3 tools/pmc_kernels.py --sized --out gpurun_out/${tag}_pmc.json -- \
     python3 tools/c5_same_run.py --reps 2 "${args[@]}" --out /tmp/c5_pmc_run.json \
     > gpurun_out/${tag}_pmc.log 2>&1

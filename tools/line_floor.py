@@ -155,7 +155,7 @@ def main():
         lt, lg = lines(groups)
         res[f"needed_plus_linewin{m_}_{k_}"] = {"lines_per_frame_tile": round(lt, 4),
                                               "read_bytes_per_frame": round(lt * 128 + 10, 2)}
-    pmc = [ROOT / "profiles" / f"r02_pmc_{args.config}.json"]
+    pmc = [ROOT / "history" / "profiles" / f"r02_pmc_{args.config}.json"]
     if pmc[-1].exists():
         p = json.loads(pmc[-1].read_text())
         res["pmc"] = {"file": pmc[-1].name, "kernel": p.get("kernel"),
