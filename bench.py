@@ -1358,6 +1358,11 @@ def run_config(args, config, env):
                    "source": f"{pf.relative_to(ROOT)} (rocprofv3 --pmc FETCH_SIZE x2 + "
                              "WRITE_SIZE, separate passes, same kernel sources)",
                    "kernel": t.get("kernel")}
+        if t.get("fetch_bytes_sized"):
+            # the x2 correction cross-checked by the L2 -> memory read
+            # requests counted by size (32/64/128 B) in a pass of their own
+            traffic["fetch_bytes_sized"] = t["fetch_bytes_sized"]
+            traffic["sized_vs_corrected"] = t.get("sized_vs_corrected")
 
     # --- variants (outside the timed region; same data) ---
     variants = {}

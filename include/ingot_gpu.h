@@ -461,7 +461,7 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              frames: k = 2, 3, 5 or 8); 1000 + 10 m + k:
  *                              the same from at least m chunks.  Defaults:
  *                              records 25 (the tunnel chain 1069; packed
- *                              tunnel frames 8), flows 1045, fields /
+ *                              tunnel frames 8), flows 1056, fields /
  *                              rewrites 3 (tunnel 8), mapped host memory 5
  *   INGOT_TUNE_WINDOW_STRIDED  16-B chunks staged per slot: 2,3,4,5,8 or 100
  *                              (default 4 for slots <= 64 B, else 3)

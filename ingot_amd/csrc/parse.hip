@@ -649,12 +649,16 @@ hipError_t launch_flows_mode(const FlowArgs& a, int layout_kind, int chain, cons
         default: return launch_chain<5, LAYOUT_STRIDED, MODE>(a, chain, g, s, pc);
         }
     }
-    // Device arenas: a line-completing window of 4 to 5 chunks (the 5-tuple
-    // of an untagged v4 frame ends 26 B past byte 12's chunk, a v6 one 46 B):
-    // C5 flows kernel 330 -> 326 us (fixed 5; 4 to 6 chunks 367, 3 to 5 392;
-    // round 2, interleaved, history/profiles/r02_window_ab.json).
+    // Device arenas: a line-completing window of 5 to 6 chunks (the 5-tuple
+    // of an untagged v4 frame ends 26 B past byte 12's chunk, a v6 one 46 B,
+    // and an IPv6 EH chain's ports later): the C5 flows kernel, interleaved
+    // beside the 4-to-5 window of rounds 2-3 on three boxes, 358.0 -> 350.8,
+    // 356.9 -> 349.3, 362.6 -> 350.9 us (-2..-3%; profiles/r03_c5_*_ab.json,
+    // r04_c5_window_ab.json) at equal PMC bytes (210.5 B/frame): fewer lanes
+    // read EH / port bytes past the window one by one, although 6-chunk
+    // images fit 6 blocks per CU instead of 7.  4-to-6 windows: 367 (round 2).
     int wi = t.window_indexed;
-    if (!wi && !t.host_arena && layout_kind == LAYOUT_INDEXED) wi = 1045;
+    if (!wi && !t.host_arena && layout_kind == LAYOUT_INDEXED) wi = 1056;
     if (wi > 20 && wi != 100) {  // line-completing windows (ParseArgs::linewin)
         FlowArgs b = a;
         b.p.linewin = wi > 1000 ? (uint32_t)(wi - 1000) / 10u : 2u;

@@ -1306,8 +1306,15 @@ __device__ __forceinline__ void ext_walk(bool valid, uint32_t* wimg, uint32_t la
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!miss) return;
-    // image slot of free slot t: its row (cum) and its set bit in the row
-    auto free_slot = [&](uint32_t t) -> uint32_t {
+    // chunks placed for this lane (all of them unless the free slots ran out)
+    const uint32_t placed = S + m <= cum[NCH] ? m : (cum[NCH] > S ? cum[NCH] - S : 0u);
+    // image slot of free slot S + e: its row (by cum) and its set bit in the
+    // row's ballot (fully unrolled, constant indices: the arrays stay in
+    // registers)
+    uint32_t qv[EXT_MAX];
+#pragma unroll
+    for (uint32_t e = 0; e < EXT_MAX; ++e) {
+        const uint32_t t = S + e;
         uint32_t k = 0, c0 = 0;
         uint64_t B = rowB[0];
 #pragma unroll
@@ -1317,10 +1324,8 @@ __device__ __forceinline__ void ext_walk(bool valid, uint32_t* wimg, uint32_t la
             B = in ? rowB[kk] : B;
             c0 = in ? cum[kk] : c0;
         }
-        return k * WAVE + nth_set_bit(B, t - c0);
-    };
-    // chunks placed for this lane (all of them unless the free slots ran out)
-    const uint32_t placed = S + m <= cum[NCH] ? m : (cum[NCH] > S ? cum[NCH] - S : 0u);
+        qv[e] = e < placed ? k * WAVE + nth_set_bit(B, t - c0) : 0u;
+    }
     FrameExt<NCH> f;
     f.win = (const lds_u32*)wimg;
     f.p = lane;
@@ -1328,10 +1333,10 @@ __device__ __forceinline__ void ext_walk(bool valid, uint32_t* wimg, uint32_t la
     f.len = len;
     f.g = g;
     f.nch = nch;
-    f.q0 = placed > 0u ? free_slot(S) : 0u;
-    f.q1 = placed > 1u ? free_slot(S + 1u) : 0u;
-    f.q2 = placed > 2u ? free_slot(S + 2u) : 0u;
-    f.q3 = placed > 3u ? free_slot(S + 3u) : 0u;
+    f.q0 = qv[0];
+    f.q1 = qv[1];
+    f.q2 = qv[2];
+    f.q3 = qv[3];
     const uint32_t end = 16u * (nch + placed) - sh;  // staged byte sh + i = frame byte i
     f.avail = end < len ? end : len;
     // pass 2: the missing lanes, from the window and the extension

@@ -26,10 +26,16 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 
 
+SIZED = ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")
+
+
 def run_pass(counter: str, config: str, outdir: Path, steps: int, extra=()) -> list[float]:
-    d = outdir / counter.lower()
+    """One --pmc pass; `counter` may name several counters of one pass
+    ("A B C"): then the values are {counter: [per dispatch]}."""
+    many = counter.split()
+    d = outdir / many[0].lower()
     d.mkdir(parents=True, exist_ok=True)
-    cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", str(d), "-o", "run",
+    cmd = ["rocprofv3", "--pmc", *many, "--output-format", "csv", "-d", str(d), "-o", "run",
            "--", sys.executable, str(ROOT / "bench.py"), "--config", config, "--steps", str(steps),
            "--warmup", "2", "--streams", "1", "--no-cpu-baseline", "--no-variants", "--no-gate",
            "--no-host-path", "--no-sublines",
@@ -42,17 +48,18 @@ def run_pass(counter: str, config: str, outdir: Path, steps: int, extra=()) -> l
     files = glob.glob(str(d / "**" / "*counter_collection.csv"), recursive=True)
     if not files:
         raise RuntimeError(f"no counter_collection.csv under {d}")
-    vals = {}
+    vals = {c: {} for c in many}
     names = {}
     with open(files[0]) as f:
         for row in csv.DictReader(f):
             name = row.get("Kernel_Name", "")
             if "k_parse" not in name and "k_modify" not in name:
                 continue
-            if row.get("Counter_Name") != counter:
+            c = row.get("Counter_Name")
+            if c not in vals:
                 continue
-            key = row.get("Dispatch_Id") or row.get("Correlation_Id") or str(len(vals))
-            vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
+            key = row.get("Dispatch_Id") or row.get("Correlation_Id") or str(len(vals[c]))
+            vals[c][key] = vals[c].get(key, 0.0) + float(row["Counter_Value"])
             names[key] = name
     # the timed launches: the most-dispatched parse kernel (the generator's
     # and the algorithmic-bytes pass's dispatches are a handful)
@@ -61,7 +68,8 @@ def run_pass(counter: str, config: str, outdir: Path, steps: int, extra=()) -> l
         count[k] = count.get(k, 0) + 1
     top = max(count, key=count.get)
     KERNELS.add(top)
-    return [v for k, v in vals.items() if names[k] == top]
+    out = {c: [v for k, v in vs.items() if names[k] == top] for c, vs in vals.items()}
+    return out if len(many) > 1 else out[many[0]]
 
 
 KERNELS: set = set()
@@ -84,6 +92,9 @@ def main():
     out = ROOT / "gpurun_out" / f"pmc_{args.config}{suffix}"
     fetch = run_pass("FETCH_SIZE", args.config, out, args.steps, extra)
     write = run_pass("WRITE_SIZE", args.config, out, args.steps, extra)
+    # cross-check of the x2 correction: the L2 -> memory read requests by
+    # size in a pass of their own (3 TCC counters)
+    sized = run_pass(" ".join(SIZED), args.config, out, args.steps, extra)
     # the first dispatches include the generator's and the algorithmic-bytes
     # pass: keep the timed ones (all k_parse dispatches are the same launch)
     f_kib = sorted(fetch)[len(fetch) // 2]
@@ -109,6 +120,12 @@ def main():
         "traffic_bytes_per_launch": f_kib * 1024 * 2 + w_kib * 1024,
         "correction": "FETCH_SIZE x2 on gfx950 (MI355X_MICROARCH.md:298)",
     }
+    med = {c: sorted(v)[len(v) // 2] if v else 0.0 for c, v in sized.items()}
+    res["read_requests_by_size"] = {"32B": med[SIZED[0]], "64B": med[SIZED[1]],
+                                    "128B": med[SIZED[2]]}
+    res["fetch_bytes_sized"] = 32 * med[SIZED[0]] + 64 * med[SIZED[1]] + 128 * med[SIZED[2]]
+    res["sized_vs_corrected"] = (round(res["fetch_bytes_sized"] / res["fetch_bytes_corrected"], 4)
+                                 if res["fetch_bytes_corrected"] else None)
     res["tune"] = args.tune
     prof = ROOT / "profiles" / f"{args.tag}_pmc_{args.config}{suffix}.json"
     prof.write_text(json.dumps(res, indent=1) + "\n")
