@@ -730,7 +730,7 @@ bool tuning_valid(int key, int value) {
     case INGOT_TUNE_SLOW_PATH:
         return value >= 0 && value <= 2;
     case INGOT_TUNE_READ_PLAN:
-        return (value >= 0 && value <= 16);
+        return (value >= 0 && value <= 17);
     case INGOT_TUNE_FLOW_KERNEL:
         return value >= 0 && value <= 9;
     default:

@@ -30,11 +30,17 @@ namespace {
 // per-packet array a.first, indexed by the packet like pkt_seg, so it is
 // loaded together with the chunk bounds — one HBM round trip before the
 // staging instead of two (pkt_seg, then the chunk table at pkt_seg[i]).
+//
+// LAZY (with FIRST; INGOT_TUNE_READ_PLAN 17): the chunk bounds are not
+// loaded per tile at all — chunk 0 comes from a.first — but by the walk, per
+// lane, only when it needs them (SegFrameP::bounds): one descriptor stream
+// (8 B per packet) instead of two for packets whose headers lie in chunk 0.
 template <int CS0, int CS1, int CS2, int CS3, int CHAIN, int MODE, bool DENSE = false,
-          bool PIPE = false, int NPRE = 3, bool FIRST = false>
+          bool PIPE = false, int NPRE = 3, bool FIRST = false, bool LAZY = false>
 __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
     static_assert(!(FIRST && PIPE), "the lookahead kernel loads chunk 0 from the table");
-    using FR = SegFrameP<CS0, CS1, CS2, CS3, DENSE, NPRE>;
+    static_assert(!LAZY || (FIRST && NPRE == 0), "lazy bounds: chunk 0 per packet, no prefetch");
+    using FR = SegFrameP<CS0, CS1, CS2, CS3, DENSE, NPRE, LAZY>;
     static_assert((CS1 == 0 || NPRE >= 1) && (CS2 == 0 || NPRE >= 2) && (CS3 == 0 || NPRE >= 3),
                   "a chunk staged in planes needs its descriptor up front");
     constexpr uint32_t P = CS0 + CS1 + CS2 + CS3;
@@ -52,10 +58,16 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
     uint64_t t = (uint64_t)blockIdx.x * WAVES + wave;
     if (t >= ntiles) return;
 
-    // packet i's chunk bounds (clamped index: always one load pair)
+    // packet i's chunk bounds (clamped index: always one load pair); LAZY:
+    // none yet (FR::kUnknown for a packet of the batch, 0 past its end)
     auto load_pkt = [&](uint64_t tt, uint32_t& s0, uint32_t& ns) {
         uint64_t i = tt * WAVE + lane;
         const bool v = i < a.n;
+        if constexpr (LAZY) {
+            s0 = 0;
+            ns = v ? FR::kUnknown : 0u;
+            return;
+        }
         if (!v) i = a.n - 1u;
         const uint32_t b0 = a.pkt_seg[i], b1 = a.pkt_seg[i + 1];
         s0 = v ? b0 : 0u;
@@ -78,7 +90,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
         uint64_t i = tt * WAVE + lane;
         if (i >= a.n) i = a.n - 1u;
         const uint64_t v = a.first[i];
-        o = ns ? v >> 16 : 0u;
+        o = ns ? v >> 16 : 0u;  // (LAZY: ns is kUnknown for every packet of the batch)
         l = ns ? (uint32_t)(v & 0xffffu) : 0u;
     };
     uint32_t s0, nseg, s0n = 0, nsn = 0;
@@ -196,6 +208,8 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
         fr.s0 = s0;
         fr.k = 0;
         fr.nseg = nseg;
+        fr.pkt_seg = a.pkt_seg;
+        fr.pi = i;
         fr.L = 0;
         fr.b0 = base0;
         fr.span0 = 16u * n0;
@@ -254,7 +268,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
 // persist_cus != 0 (the PIPE kernels): a persistent grid of the blocks the
 // device holds at once.
 template <int CS0, int CS1, int CS2, int CS3, int MODE, bool DENSE = false, bool PIPE = false,
-          int NPRE = 3, bool FIRST = false>
+          int NPRE = 3, bool FIRST = false, bool LAZY = false>
 hipError_t launch_read(const ParseArgs& a, int chain, uint32_t grid, hipStream_t s,
                        uint32_t persist_cus = 0) {
     auto go = [&](auto kernel) {
@@ -267,16 +281,16 @@ hipError_t launch_read(const ParseArgs& a, int chain, uint32_t grid, hipStream_t
     };
     switch (chain) {
     case INGOT_CHAIN_UDP_PARSER:
-        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_UDP_PARSER, MODE, DENSE, PIPE, NPRE, FIRST>);
+        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_UDP_PARSER, MODE, DENSE, PIPE, NPRE, FIRST, LAZY>);
         break;
     case INGOT_CHAIN_GENERIC_ULP:
-        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENERIC_ULP, MODE, DENSE, PIPE, NPRE, FIRST>);
+        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENERIC_ULP, MODE, DENSE, PIPE, NPRE, FIRST, LAZY>);
         break;
     case INGOT_CHAIN_VLAN_ULP:
-        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_VLAN_ULP, MODE, DENSE, PIPE, NPRE, FIRST>);
+        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_VLAN_ULP, MODE, DENSE, PIPE, NPRE, FIRST, LAZY>);
         break;
     default:
-        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENEVE_OVER_V6, MODE, DENSE, PIPE, NPRE, FIRST>);
+        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENEVE_OVER_V6, MODE, DENSE, PIPE, NPRE, FIRST, LAZY>);
         break;
     }
     return hipGetLastError();
@@ -320,6 +334,8 @@ hipError_t launch_segmented(const ParseArgs& a, int chain, int mode, const Tunin
             return launch_read<4, 0, 0, 0, OUT_REC16, false, false, 3, true>(a, chain, g, s);
         ParseArgs b = a;
         b.linewin = 3u;
+        if (t.read_plan == 17)  // chunk bounds loaded lazily by the walk
+            return launch_read<5, 0, 0, 0, OUT_REC16, false, false, 0, true, true>(b, chain, g, s);
         return launch_read<5, 0, 0, 0, OUT_REC16, false, false, 3, true>(b, chain, g, s);
     }
     if (mode == OUT_FIELDS) return launch_read<4, 0, 0, 0, OUT_FIELDS>(a, chain, g, s);

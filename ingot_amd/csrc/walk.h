@@ -276,8 +276,14 @@ struct SegFrame : Frame<NCH> {
 // cut from one buffer, like the reference bench's one chunk per header) is
 // staged with chunk 0's pieces and read from there.
 // Offsets are logical as in SegFrame; `len` is the current chunk's end.
-template <int CS0, int CS1, int CS2, int CS3, bool DENSE = false, int NPRE = 3>
+// LAZY (ingot_gpu_parse_read_first with INGOT_TUNE_READ_PLAN 17): the
+// packet's chunk bounds (pkt_seg[pi], pkt_seg[pi + 1]) are not loaded up
+// front — chunk 0 comes per packet — but on the first more() / advance(),
+// i.e. only by a walk that leaves chunk 0 or fails in it (NPRE = 0: no later
+// descriptor is prefetched, since they are found through the bounds).
+template <int CS0, int CS1, int CS2, int CS3, bool DENSE = false, int NPRE = 3, bool LAZY = false>
 struct SegFrameP {
+    static_assert(!LAZY || NPRE == 0, "lazy bounds: no descriptor prefetch");
     static constexpr bool kRead = true;
     static constexpr bool kProbe = false;
     const lds_u32* win;  // this wave's image: 64 x CS0 slots, then the planes
@@ -288,7 +294,19 @@ struct SegFrameP {
     const uint8_t* arena;
     const uint64_t* seg_off;
     const uint16_t* seg_len;
-    uint32_t s0, k, nseg;
+    mutable uint32_t s0, nseg;  // LAZY: nseg == kUnknown until bounds() loads them
+    uint32_t k;
+    const uint32_t* pkt_seg;  // LAZY: the bounds array and this packet's index
+    uint64_t pi;
+    static constexpr uint32_t kUnknown = 0xffffffffu;
+    __device__ __forceinline__ void bounds() const {
+        if constexpr (LAZY) {
+            if (nseg == kUnknown) {
+                s0 = pkt_seg[pi];
+                nseg = pkt_seg[pi + 1] - s0;
+            }
+        }
+    }
     uint64_t o0, o1, o2, o3;  // the first four chunks' offsets and lengths
     uint32_t l0, l1, l2, l3;
     int64_t b0;      // chunk 0's window: arena bytes [b0, b0 + span0) staged
@@ -329,7 +347,10 @@ struct SegFrameP {
     __device__ __forceinline__ uint32_t get(uint32_t hdr, Field f) const {
         return (be(hdr + f.byte0(), f.nbytes()) >> f.rshift()) & f.mask();
     }
-    __device__ __forceinline__ bool more() const { return k + 1 < nseg; }
+    __device__ __forceinline__ bool more() const {
+        bounds();
+        return k + 1 < nseg;
+    }
     // chunk e's staged pieces: chunk 0 always; later ones unless last
     __device__ __forceinline__ static uint32_t staged(uint32_t e, uint32_t nseg) {
         return e == 0 ? CS0 : (e + 1 < nseg ? cs(e) : 0u);
@@ -351,6 +372,7 @@ struct SegFrameP {
         }
     }
     __device__ __forceinline__ void advance() {
+        bounds();
         ++k;
         L = len;
         // chunks 1..NPRE that are not the packet's last had their

@@ -304,12 +304,20 @@ def test_scattered_and_aliased_chunks(torch, plan):
         assert np.array_equal(chunk.cpu().numpy().view(np.uint16), w_chunk)
 
 
+@pytest.mark.parametrize("lazy", [False, True])
 @pytest.mark.parametrize("chain", list(Chain))
-def test_first_chunk_descriptor_path_is_bit_exact(ctx, torch, chain):
+def test_first_chunk_descriptor_path_is_bit_exact(ctx, torch, chain, lazy):
     """ingot_gpu_parse_read_first: chunk 0's descriptor per packet, loaded
-    beside the chunk bounds.  Records and the remainder's chunk index equal
-    the oracle's (and so ingot_gpu_parse_read's) over 1-8 chunks per packet,
-    empty chunks and packets without chunks, including the read KATs."""
+    beside the chunk bounds (lazy: INGOT_TUNE_READ_PLAN 17, the bounds loaded
+    by the walk only when it leaves chunk 0 or fails in it).  Records and the
+    remainder's chunk index equal the oracle's (and so ingot_gpu_parse_read's)
+    over 1-8 chunks per packet, empty chunks and packets without chunks,
+    including the read KATs."""
+    from ingot_amd.abi import TUNE_READ_PLAN
+
+    if lazy:
+        ctx = ingot_amd.Context(0)
+        ctx.set_tuning(TUNE_READ_PLAN, 17)
     prof = GenProfile.GENEVE_ADVERSARIAL if chain == TUN else GenProfile.ADVERSARIAL
     frames = frames_of(prof, 30_000, seed=71 + int(chain))
     frames += frames_of(GenProfile.GENEVE if chain == TUN else GenProfile.MIXED, 10_000, seed=73)
