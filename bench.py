@@ -90,6 +90,11 @@ READ_CHUNKS = {"c3r": "split2", "c2r": "per_header"}
 # into chunk 0's window) gains nothing from it (18.2 vs 18.8 us, round 3), so
 # it times the chunk table.
 READ_FIRST = {"c3r"}
+# ... and with the chunk bounds loaded only by walks that leave chunk 0 or
+# fail in it (INGOT_TUNE_READ_PLAN 17, the header-split shape: every header
+# in the mblk head): c3r 562.4 -> 548.7 us per launch, PMC read 176 B per
+# packet (profiles/r04_c3r_lazy_bounds_ab.json).
+READ_LAZY = {"c3r"}
 # Strong scaling (--scaling strong): the whole job's frames, split over the
 # ranks (BASELINE.json configs[3]: 64 M frames over 8 GPUs); other configs
 # split their single-GPU batch.
@@ -980,6 +985,21 @@ def gate_policy(flows: bool, world: int, backend: str, no_gate: bool) -> str:
     return "hold"
 
 
+def jsonable(x, path="line"):
+    """The line with numpy scalars / arrays made plain Python (an array is
+    named on stderr: it should have been reduced to a number)."""
+    if isinstance(x, dict):
+        return {k: jsonable(v, f"{path}.{k}") for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [jsonable(v, f"{path}[{i}]") for i, v in enumerate(x)]
+    if isinstance(x, np.ndarray):
+        log(f"[bench] {path} is an array {x.shape}")
+        return x.tolist() if x.size <= 64 else f"<array {x.shape} at {path}>"
+    if isinstance(x, np.generic):
+        return x.item()
+    return x
+
+
 T_START = time.perf_counter()
 
 
@@ -1088,7 +1108,7 @@ def main():
         result["sublines"] = subs
         result["wall_s_command"] = round(time.perf_counter() - T_START, 2)
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(jsonable(result)), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -1197,6 +1217,11 @@ def run_config(args, config, env):
             torch, off, stride, rlens.to(torch.int32), recs0, READ_CHUNKS[config], dev)
 
     read_first = config in READ_FIRST
+    read_lazy = read_first and config in READ_LAZY and not args.tune
+    if read_lazy:
+        from ingot_amd import abi as _abi
+
+        ctx.set_tuning(_abi.TUNE_READ_PLAN, 17)
 
     def runner(nstreams, record, flows_only=False, dense=False, ring=False, group=G,
                first=read_first):
@@ -1291,9 +1316,13 @@ def run_config(args, config, env):
         # descriptors: pkt_seg (4 B) + (u64 off, u16 len) per header chunk
         # (read_first: chunk 0's 8-B (offset << 16) | length per packet
         # instead of its table entry, later header chunks from the table)
+        # (read_lazy: pkt_seg only for the packets whose walk needed the
+        # bounds: more than one header chunk, or a parse error)
         hc = head_chunks.cpu().numpy().astype(np.int64)
-        desc = 4 + 8 + 10 * np.maximum(hc - 1, 0) if read_first else 4 + 10 * hc
-        rd, wr = algorithmic_bytes(recs_np, recs_np["payload_off"], 0, desc, 16)
+        dbytes = 4 + 8 + 10 * np.maximum(hc - 1, 0) if read_first else 4 + 10 * hc
+        if read_lazy:
+            dbytes = dbytes - 4 * ((hc <= 1) & (recs_np["status"] == 0))
+        rd, wr = algorithmic_bytes(recs_np, recs_np["payload_off"], 0, dbytes, 16)
     elif mode == "packed":
         # descriptors: the u16 length, read by the parse and once more by the
         # tile-sum pass; tile sums and bases: 12 B per 64 packets
@@ -1460,6 +1489,8 @@ def run_config(args, config, env):
         host_path = host_inclusive_live(torch, ingot_amd, ctx, arenas[0], off, lens, stride,
                                         chain, n)
 
+    if read_lazy:
+        ctx.set_tuning(_abi.TUNE_READ_PLAN, 0)
     if rank != 0:
         return None
     cpu = None
@@ -1482,7 +1513,8 @@ def run_config(args, config, env):
                            mode="parse" if flows else mode, segs=segs)
     kname = {"modify": ", parse + setters",
              "read": ", LAYOUT_SEGMENTED (parse_read" +
-                     (", chunk 0 per packet: ingot_gpu_parse_read_first)" if read_first else ")"),
+                     (", chunk 0 per packet: ingot_gpu_parse_read_first" if read_first else "") +
+                     (", chunk bounds on demand: INGOT_TUNE_READ_PLAN 17)" if read_lazy else ")"),
              "packed": ", LAYOUT_PACKED + k_tile_sums/k_group_scan",
              "flows": ", OUT_FLOWS16 (parse + Toeplitz hash; the step adds "
                       "k_flow_count16 / k_flow_reduce16)"}.get(mode, "")
@@ -1507,7 +1539,10 @@ def run_config(args, config, env):
             "chain": chain_name,
             "layout": (("chunk lists: u32 pkt_seg bounds, u64 seg_off + u16 seg_len per chunk" +
                         ("; chunk 0 as one u64 (offset << 16) | length per packet"
-                         if read_first else "") + f" ({READ_CHUNKS[config]})")
+                         if read_first else "") +
+                        ("; bounds loaded only by walks that leave chunk 0 or fail "
+                         "(INGOT_TUNE_READ_PLAN 17)" if read_lazy else "") +
+                        f" ({READ_CHUNKS[config]})")
                        if mode == "read" else
                        f"strided {stride} B" if stride else "packed, u64 offsets + u16 lengths"),
             "record_bytes": args.record,

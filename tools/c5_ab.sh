@@ -13,3 +13,4 @@ timeout -k 10 240 python3 tools/c5_same_run.py --reps 10 "${args[@]}" \
 timeout -k 10 400 python3 tools/pmc_kernels.py --sized --out gpurun_out/${tag}_pmc.json -- \
     python3 tools/c5_same_run.py --reps 2 "${args[@]}" --out /tmp/c5_pmc_run.json \
     > gpurun_out/${tag}_pmc.log 2>&1
+rm -rf gpurun_out/${tag}_pmc  # raw rocprofv3 CSVs: the JSON holds the result

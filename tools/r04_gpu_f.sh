@@ -16,3 +16,5 @@ done
 timeout -k 10 400 python3 tools/pmc_kernels.py --sized --out $O/r04f_c3r_pmc.json -- \
     python3 bench.py --config c3r --steps 5 --warmup 2 --no-cpu-baseline --no-variants \
     --no-gate --tune read_plan=17 > $O/r04f_c3r_pmc.log 2>&1
+rm -rf $O/r04f_c3r_pmc
+du -sk $O/* 2>/dev/null | sort -n | tail -4; grep -h "is an array" $O/r04f_*.err | sort | uniq -c
