@@ -207,10 +207,13 @@ def host_cpu_share():
 
 def physical_core_pick(cpus, want):
     """One CPU per physical core among `cpus` (SMT siblings dropped: a
-    sibling shares its core's pipelines), spread round-robin over the L3
-    domains (CCDs) so that workers do not crowd one CCD's cache, up to
-    `want`.  Returns (picked cpus, description).  Falls back to `cpus` in
-    order when sysfs has no topology."""
+    sibling shares its core's pipelines), all in ONE socket (the package of
+    the first allowed CPU, or the one with the most cores if that has fewer
+    than `want`: the sample's memory is then local to every worker), spread
+    round-robin over that socket's L3 domains (CCDs) so that workers do not
+    crowd one CCD's cache, up to `want`.  Returns (picked cpus,
+    description).  Falls back to `cpus` in order when sysfs has no
+    topology."""
     def rd(c, rel):
         return _read(f"/sys/devices/system/cpu/cpu{c}/{rel}")
 
@@ -223,6 +226,13 @@ def physical_core_pick(cpus, want):
         if key not in cores:
             cores[key] = (c, rd(c, "cache/index3/id") or pkg)
             order.append(key)
+    per_pkg = {}
+    for key in order:
+        per_pkg.setdefault(key[0], []).append(key)
+    pkg = order[0][0]
+    if len(per_pkg[pkg]) < want:
+        pkg = max(per_pkg, key=lambda k: len(per_pkg[k]))
+    order = per_pkg[pkg]
     by_l3 = {}
     for key in order:
         c, l3 = cores[key]
@@ -233,9 +243,25 @@ def physical_core_pick(cpus, want):
             if q and len(picked) < want:
                 picked.append(q.pop(0))
     used_l3 = {cores[k][1] for k in order if cores[k][0] in picked}
-    return picked, {"topology": "sysfs", "physical_cores_available": len(order),
+    return picked, {"topology": "sysfs", "socket": pkg, "sockets_available": len(per_pkg),
+                    "physical_cores_available": len(cores),
+                    "physical_cores_in_socket": len(order),
                     "physical_cores_used": len(picked), "l3_domains_used": len(used_l3),
-                    "smt_siblings_skipped": len(cpus) - len(order)}
+                    "smt_siblings_skipped": len(cpus) - len(cores)}
+
+
+def _cgroup_throttled_us():
+    """cgroup v2 cpu.stat throttled_usec of this process's cgroup (None
+    when unavailable)."""
+    for line in (_read("/proc/self/cgroup") or "").splitlines():
+        hid, _, path = line.split(":", 2)
+        if hid == "0":
+            st = _read(Path("/sys/fs/cgroup", *[x for x in path.split("/") if x], "cpu.stat"))
+            for kv in (st or "").splitlines():
+                k, _, v = kv.partition(" ")
+                if k == "throttled_usec":
+                    return int(v)
+    return None
 
 
 def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode="parse",
@@ -247,7 +273,9 @@ def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode
     machine), and 1 worker.  Each worker repeats its contiguous share of the
     sample `passes` times per call, so thread start-up is amortised; a share
     is then cache-resident after the first pass — generous to the CPU.  The
-    all-worker figure is the median of three sub-runs (spread reported).
+    all-worker figure is the median of three sub-runs (spread reported, with
+    the CPU share the workers obtained and the cgroup's throttled time in
+    each, which name host load when the spread is large).
     mode "read": parse_read over `segs` = (seg_off, seg_len, pkt_seg);
     "modify": parse + the same setter in place."""
     import ctypes
@@ -282,6 +310,19 @@ def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode
     share = {**share, **topo, "quota_headroom_cpus": len(allowed) - len(cpus)}
     pin = (ctypes.c_int * len(cpus))(*cpus)
     lib.oracle_set_affinity(ctypes.cast(pin, ctypes.c_void_p), len(cpus))
+    # the sample's pages first-touched by this thread pinned to the chosen
+    # socket: local memory for every worker (the caller's copies may sit on
+    # the other socket)
+    import resource
+
+    main_aff = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None
+    if main_aff is not None:
+        os.sched_setaffinity(0, cpus)
+    arena_np = np.array(arena_np, copy=True)
+    off_np = None if off_np is None else np.array(off_np, copy=True)
+    lens_np = None if lens_np is None else np.array(lens_np, copy=True)
+    if segs is not None:
+        segs = tuple(np.array(x, copy=True) for x in segs)
 
     def measure(t, budget):
         lib.oracle_set_passes(1)
@@ -291,6 +332,7 @@ def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode
         once = max(time.perf_counter() - t0, 1e-6)
         passes = max(1, min(10000, int(budget / 4 / once)))
         lib.oracle_set_passes(passes)
+        ru0, th0 = resource.getrusage(resource.RUSAGE_SELF), _cgroup_throttled_us()
         calls, t0 = 0, time.perf_counter()
         while True:
             one_call(t)
@@ -298,29 +340,42 @@ def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode
             el = time.perf_counter() - t0
             if el > budget:
                 break
-        return calls * passes * n / el / 1e6, calls * passes, el
+        ru1, th1 = resource.getrusage(resource.RUSAGE_SELF), _cgroup_throttled_us()
+        cpu_s = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+        return (calls * passes * n / el / 1e6, calls * passes, el,
+                # CPU time the workers obtained per wall second and worker
+                # (< 1: descheduled — other load on these cores, or the
+                # cgroup quota), and the cgroup's throttled time in the run
+                round(cpu_s / (el * t), 3),
+                None if th0 is None or th1 is None else round((th1 - th0) / 1e3, 1))
 
     try:
-        single = measure(1, budget_s / 2)
-        runs = sorted((measure(len(cpus), budget_s / 5) for _ in range(5)), key=lambda r: r[0])
+        single = measure(1, budget_s / 3)
+        runs = sorted((measure(len(cpus), budget_s / 3) for _ in range(3)), key=lambda r: r[0])
     finally:
         lib.oracle_set_passes(1)
         lib.oracle_set_affinity(None, 0)
-    mp, reps, el = runs[2]
+        if main_aff is not None:
+            os.sched_setaffinity(0, main_aff)
+    mp, reps, el = runs[1][:3]
     spread = (runs[-1][0] - runs[0][0]) / mp if mp else 0.0
     what = {"parse": "parse_slice", "read": "parse_read", "modify": "parse + set_destination"}
     return {
         "value": round(mp, 3), "unit": "Mpkt/s", "cores": len(cpus), "kind": "port",
         "sample": f"{reps} passes x {n} frames of the benchmark batch (same bytes), "
                   f"{el:.2f} s wall on {len(cpus)} threads, each pinned to one of the CPUs "
-                  f"this process may use, one per physical core across the L3 domains, one short of "
-                  f"the cgroup CPU quota; median of 5 "
+                  f"this process may use, one per physical core of one socket across its L3 "
+                  f"domains, one short of the cgroup CPU quota, sample copied NUMA-local; "
+                  f"median of 3 "
                   f"runs; each thread repeats its share, cache-resident after the first pass; "
                   f"C restatement of ingot {what.get(mode, mode)} (oracle/), -march={arch}",
         "single_core_value": round(single[0], 3),
         "scaling_vs_single": round(mp / single[0], 2) if single[0] else None,
         "run_spread": round(spread, 4),
         "runs": [round(r[0], 3) for r in runs],
+        "runs_cpu_share": [r[3] for r in runs],
+        "runs_throttled_ms": [r[4] for r in runs],
+        "single_core_cpu_share": single[3],
         "cpu_model": _cpu_model(),
         **share,
     }

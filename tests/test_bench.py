@@ -439,3 +439,22 @@ def test_physical_core_pick_skips_smt_and_spreads_over_l3(monkeypatch):
     assert info["l3_domains_used"] == 2
     monkeypatch.setattr(bench, "_read", lambda p: None)
     assert bench.physical_core_pick([3, 1, 2], 2)[0] == [3, 1]
+
+
+def test_physical_core_pick_stays_in_one_socket(monkeypatch):
+    """Two sockets x 2 CCDs x 4 cores (cpu c: socket c // 8, CCD c // 4):
+    the workers stay in the first allowed CPU's socket (NUMA-local sample)
+    unless it has too few cores."""
+    def fake(path):
+        parts = str(path).split("/")
+        c = int(parts[5][3:])
+        rel = "/".join(parts[6:])
+        return {"topology/physical_package_id": str(c // 8), "topology/die_id": "0",
+                "topology/core_id": str(c % 8), "cache/index3/id": str(c // 4)}.get(rel)
+
+    monkeypatch.setattr(bench, "_read", fake)
+    picked, info = bench.physical_core_pick(list(range(16)), 6)
+    assert all(c < 8 for c in picked) and info["socket"] == "0"
+    assert info["sockets_available"] == 2 and info["l3_domains_used"] == 2
+    picked, info = bench.physical_core_pick(list(range(6, 16)), 6)  # socket 0 has 2 cores here
+    assert all(c >= 8 for c in picked) and info["socket"] == "1"

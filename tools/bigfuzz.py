@@ -83,14 +83,16 @@ def main():
         arena, off, lens = ingot_amd.gen_frames(prof, n, seed=args.seed + 10 + int(chain))
         a, o, ln = arena.cpu().numpy(), off.cpu().numpy(), lens.cpu().numpy()
         w_rec = oracle.parse_batch(a, o, ln, chain, nthreads=16)
-        c1 = ingot_amd.Context(0)
-        c1.set_tuning(TUNE_SLOW_PATH, 1)
-        g = c1.parse(arena, off, lens, chain)
-        torch.cuda.synchronize()
-        bad = int((g.cpu().numpy().reshape(n, -1) != w_rec.view(np.uint8).reshape(n, -1))
-                  .any(axis=1).sum())
-        res[f"{chain.name}/slow_path"] = {"record_mismatches": bad}
-        print(chain.name, "slow_path", res[f"{chain.name}/slow_path"], flush=True)
+        for sp in (1, 2):  # round 2: re-stage compacted; round 4: resume-style
+            c1 = ingot_amd.Context(0)
+            c1.set_tuning(TUNE_SLOW_PATH, sp)
+            g = c1.parse(arena, off, lens, chain)
+            torch.cuda.synchronize()
+            bad = int((g.cpu().numpy().reshape(n, -1) != w_rec.view(np.uint8).reshape(n, -1))
+                      .any(axis=1).sum())
+            key = f"{chain.name}/slow_path" + ("" if sp == 1 else str(sp))
+            res[key] = {"record_mismatches": bad}
+            print(chain.name, key, res[key], flush=True)
         # 4 chunks per packet at 3 sorted random cuts (empty chunks included)
         rng = np.random.default_rng(args.seed + int(chain))
         cuts = np.sort(rng.integers(0, ln.astype(np.int64)[:, None] + 1, size=(n, 3)), axis=1)
@@ -116,7 +118,21 @@ def main():
                                                           "chunk_mismatches": badc}
             print(chain.name, f"parse_read plan {plan}", res[f"{chain.name}/parse_read_plan{plan}"],
                   flush=True)
-        del arena, off, lens, d_so, d_sl, d_ps
+        # round 3/4: chunk 0 per packet (parse_read_first), bounds per tile or
+        # on demand (READ_PLAN 17)
+        first = ingot_amd.first_chunks(d_so, d_sl, d_ps)
+        for plan in (0, 17):
+            c2 = ingot_amd.Context(0)
+            c2.set_tuning(TUNE_READ_PLAN, plan)
+            r, ch = c2.parse_read(arena, d_so, d_sl, d_ps, chain, first=first)
+            torch.cuda.synchronize()
+            bad = int((r.cpu().numpy().reshape(n, -1) != w_r.view(np.uint8).reshape(n, -1))
+                      .any(axis=1).sum())
+            badc = int((ch.cpu().numpy().view(np.uint16) != w_ch).sum())
+            key = f"{chain.name}/parse_read_first" + ("_lazy" if plan else "")
+            res[key] = {"record_mismatches": bad, "chunk_mismatches": badc}
+            print(chain.name, key, res[key], flush=True)
+        del arena, off, lens, d_so, d_sl, d_ps, first
         torch.cuda.empty_cache()
     # flows on the VLAN chain
     arena, off, lens = ingot_amd.gen_frames(GenProfile.FLOWS, n, seed=args.seed)
@@ -146,8 +162,33 @@ def main():
     res["flows/VlanUlp/lane_addr_1025"] = {
         "flow_mismatches": int((f3.cpu().numpy().view(np.uint32) != w_flow).sum())}
     print("flows fk3", res["flows/VlanUlp/lane_addr_1025"], flush=True)
+    # round 4: the compacted 5-tuple kernels (tuple.hip, FLOW_KERNEL 4-9) and
+    # the default window, on the FLOWS frames and on adversarial frames
+    for fk in (0, 4, 5, 6, 7, 8, 9):
+        c4 = ingot_amd.Context(0)
+        c4.set_tuning(TUNE_FLOW_KERNEL, fk)
+        f4 = c4.flow_hist(arena, off, lens, Chain.VlanUlp)
+        torch.cuda.synchronize()
+        res[f"flows/VlanUlp/fk{fk}"] = {
+            "flow_mismatches": int((f4.cpu().numpy().view(np.uint32) != w_flow).sum())}
+        print("flows", fk, res[f"flows/VlanUlp/fk{fk}"], flush=True)
     del arena, off, lens
     torch.cuda.empty_cache()
+    for chain in (Chain.GenericUlp, Chain.VlanUlp):
+        arena, off, lens = ingot_amd.gen_frames(GenProfile.ADVERSARIAL, n,
+                                                seed=args.seed + 40 + int(chain))
+        oracle.flow_hist(arena.cpu().numpy(), off.cpu().numpy(), lens.cpu().numpy(), chain)
+        w_adv = oracle.flow_hist.last_flows
+        for fk in (0, 4, 5, 6, 7, 8, 9):
+            c4 = ingot_amd.Context(0)
+            c4.set_tuning(TUNE_FLOW_KERNEL, fk)
+            f4 = c4.flow_hist(arena, off, lens, chain)
+            torch.cuda.synchronize()
+            key = f"flows_adversarial/{chain.name}/fk{fk}"
+            res[key] = {"flow_mismatches": int((f4.cpu().numpy().view(np.uint32) != w_adv).sum())}
+            print(key, res[key], flush=True)
+        del arena, off, lens
+        torch.cuda.empty_cache()
     for chain in (Chain.UdpParser, Chain.GenericUlp, Chain.VlanUlp):
         arena, _, _ = ingot_amd.gen_frames(GenProfile.ADVERSARIAL, n, seed=args.seed + 20 +
                                            int(chain), stride=64)

@@ -7,7 +7,7 @@
 #      -> profiles/<tag>_<cfg>_streams1_kernel_stats.csv (its own JSON line:
 #      gpurun_out/prof_<cfg>.log, checked by tools/check_profiles.py);
 #   3. the bench line itself (default streams, gated) -> gpurun_out/bench_<cfg>.log.
-#   /usr/local/graft/bin/gpurun --timeout 1200 -- bash tools/profile_round.sh r02 [cfgs...]
+#   /usr/local/graft/bin/gpurun --timeout 1200 -- bash tools/profile_round.sh r04 [cfgs...]
 set -u
 tag=${1:-r02}; shift || true
 cfgs=${*:-"c2 c2m c2r c3 c3p c3r c3s c4 c5 c6"}
@@ -30,5 +30,8 @@ for cfg in $cfgs; do
     f=$(find $R/gpurun_out/prof_$cfg -name "*kernel_stats.csv" | head -1)
     cp "$f" $R/gpurun_out/${tag}_${cfg}_streams1_kernel_stats.csv
     $S 300 bench_$cfg python bench.py --config $cfg --steps $s --warmup 20 || exit $?
+    # raw rocprofv3 output: the JSON / summary above hold the results, and
+    # gpurun copies gpurun_out/ back only below 64 MiB
+    rm -rf gpurun_out/pmc_$cfg gpurun_out/prof_$cfg
 done
 echo profile-round-done
