@@ -251,6 +251,114 @@ __global__ __launch_bounds__(BLOCK) void k_flows_tuple(FlowArgs args) {
     }
 }
 
+// The table-in-image flows kernel (INGOT_TUNE_FLOW_KERNEL 10 / 11): k_parse's
+// flows mode without the block's LDS copy of the Toeplitz table.  That
+// 2,304-B table is what keeps the flows kernel at 7 blocks per CU where the
+// plain parse's 5-chunk images fit 8 (160 KiB / 20 KiB).  Here each wave
+// copies the table into its own window image after the walk, once the hash
+// input words are parked in the image's tail (three 16-B loads per lane from
+// the kernel arguments, cache hits after the first tiles), hashes from there,
+// and the next tile's staging overwrites it.  One extra L2 round trip per tile for
+// an eighth more resident waves.
+template <uint32_t NCH, int CHAIN>
+__global__ __launch_bounds__(BLOCK, 8) void k_flows_imgtab(FlowArgs args) {
+    const ParseArgs& a = args.p;
+    constexpr uint32_t SKIP = 12u;
+    constexpr uint32_t WAVE_DW = WAVE * NCH * 4u;
+    static_assert(WAVE_DW >= FLOW_TAB16 + 9u * WAVE, "the table and the parked words fit");
+    __shared__ __attribute__((aligned(32))) uint32_t s_win[WAVES * WAVE_DW];
+    const uint32_t lane = threadIdx.x & (WAVE - 1u);
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
+    uint32_t* wimg = s_win + wave * WAVE_DW;
+    const uint64_t ntiles = (a.n + WAVE - 1u) / WAVE;
+    const uint32_t mis = (uint32_t)((uintptr_t)a.arena & 31u);
+    const uint64_t tstep = (uint64_t)gridDim.x * WAVES;
+
+    for (uint64_t t = (uint64_t)blockIdx.x * WAVES + wave; t < ntiles; t += tstep) {
+        const uint64_t i = t * WAVE + lane;
+        const bool valid = i < a.n;
+        const uint64_t off = valid ? a.off[i] : 0u;
+        const uint32_t len = valid ? (uint32_t)a.len[i] : 0u;
+        const uint32_t sh = (uint32_t)((off + SKIP + mis) & 15u);
+        const int64_t base = (int64_t)off + (int64_t)SKIP - (int64_t)sh;
+        uint32_t wend = SKIP + 16u * NCH - sh;
+        if (a.linewin) {
+            const uint32_t lp = (uint32_t)((uintptr_t)(a.arena + base) >> 4) & 7u;
+            uint32_t want = ((lp + a.linewin + 7u) & ~7u) - lp;
+            if (want > NCH) want = NCH;
+            wend = SKIP + 16u * want - sh;
+        }
+        const uint32_t take = len < wend ? len : wend;
+        const int32_t staged = (int32_t)take - ((int32_t)SKIP - (int32_t)sh);
+        const uint32_t nch = staged > 0 ? ((uint32_t)staged + 15u) >> 4 : 0u;
+        // every lane's reads of the image (the previous tile's table) are done
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (uint32_t k = 0; k < NCH; ++k) {
+            const uint32_t q = k * WAVE + lane;
+            const uint32_t pp = q / NCH;
+            const uint32_t c = (q - pp * NCH) ^ swz<NCH>(pp);
+            const uint32_t np = (uint32_t)__shfl((int)nch, (int)pp);
+            const int64_t bp = (int64_t)__shfl((long long)base, (int)pp);
+            if (c < np) stage16(a.arena + bp + 16u * c, wimg + k * WAVE * 4u, false);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        Frame<NCH> fr{(const lds_u32*)wimg, lane, sh - SKIP, take, len, a.arena + off};
+        Rec r;
+        walk<CHAIN, false>(fr, r, nullptr, nullptr);
+        bool counted;
+        {
+            FlowWords x;
+            counted = valid && flow_words(fr, r, x);
+            // the image is free once every lane's reads of it have returned:
+            // park the hash input words behind where the table will go
+            // (word k of lane L at dword FLOW_TAB16 + 64 k + L), so that no
+            // register holds them across the table's fetch
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (uint32_t k = 0; k < 9; ++k) wimg[FLOW_TAB16 + k * WAVE + lane] = x.w[k];
+        }
+        // copy the table in (FLOW_TAB16 dwords = 144 16-B pieces) from the
+        // kernel arguments: plain 16-B loads + LDS stores (the arguments are
+        // not a global-address-space source for LDS-DMA)
+#pragma unroll
+        for (uint32_t k = 0; k < (FLOW_TAB16 / 4u + WAVE - 1u) / WAVE; ++k) {
+            const uint32_t q = k * WAVE + lane;
+            if (q < FLOW_TAB16 / 4u)
+                reinterpret_cast<uint4*>(wimg)[q] = reinterpret_cast<const uint4*>(args.tab16)[q];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        FlowWords x;
+#pragma unroll
+        for (uint32_t k = 0; k < 9; ++k) x.w[k] = wimg[FLOW_TAB16 + k * WAVE + lane];
+        const uint32_t h = counted ? toeplitz9_16(x, wimg) : 0u;
+        if (valid) {
+            args.flow[i] = counted ? (h & args.bin_mask) : INGOT_FLOW_NONE;
+            if (args.hash) args.hash[i] = h;
+        }
+    }
+}
+
+template <uint32_t NCH>
+hipError_t go_imgtab(const FlowArgs& a, int chain, uint32_t g, hipStream_t s) {
+    switch (chain) {
+    case INGOT_CHAIN_UDP_PARSER:
+        hipLaunchKernelGGL((k_flows_imgtab<NCH, INGOT_CHAIN_UDP_PARSER>), dim3(g), dim3(BLOCK), 0,
+                           s, a);
+        break;
+    case INGOT_CHAIN_GENERIC_ULP:
+        hipLaunchKernelGGL((k_flows_imgtab<NCH, INGOT_CHAIN_GENERIC_ULP>), dim3(g), dim3(BLOCK),
+                           0, s, a);
+        break;
+    default:
+        hipLaunchKernelGGL((k_flows_imgtab<NCH, INGOT_CHAIN_VLAN_ULP>), dim3(g), dim3(BLOCK), 0,
+                           s, a);
+        break;
+    }
+    return hipGetLastError();
+}
+
 template <uint32_t NCH, uint32_t OVF, bool EARLY>
 hipError_t go_tuple(const FlowArgs& a, int chain, uint32_t g, hipStream_t s) {
     switch (chain) {
@@ -277,12 +385,18 @@ hipError_t go_tuple(const FlowArgs& a, int chain, uint32_t g, hipStream_t s) {
 // chunks (the plain parse's window), 64 overflow slots; 5 = EARLY, 4 chunks;
 // 6 = LATE, 5 chunks; 7 = EARLY, 5 chunks, 128 overflow slots; 8 = LATE,
 // 5 chunks, each lane's missing chunks in its own window image's free slots;
-// 9 = 8 with 4-chunk windows (the table then fits 8 blocks per CU).
+// 9 = 8 with 4-chunk windows (the table then fits 8 blocks per CU);
+// 10 / 11 = k_flows_imgtab (the table copied into each wave's image per
+// tile) with 4..5 / 2..5-chunk windows.
 hipError_t launch_flows_tuple(const FlowArgs& args, int chain, int variant, const Tuning& t,
                               hipStream_t s) {
     FlowArgs a = args;
     a.p.linewin = 2;  // the plain parse's line-completing window (2..NCH)
     const uint32_t g = grid_for(a.p.n, t.max_blocks);
+    if (variant == 10 || variant == 11) {  // table in the image: 4..5 / 2..5 windows
+        a.p.linewin = variant == 10 ? 4u : 2u;
+        return go_imgtab<5>(a, chain, g, s);
+    }
     switch (variant) {
     case 5: return go_tuple<4, 64, true>(a, chain, g, s);
     case 6: return go_tuple<5, 64, false>(a, chain, g, s);
