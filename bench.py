@@ -264,8 +264,11 @@ def _cgroup_throttled_us():
     return None
 
 
+CPU_WORKERS = 0  # bench.py --cpu-workers: workers of the all-core baseline (0 = quota - 1)
+
+
 def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode="parse",
-                 segs=None):
+                 segs=None, workers=None):
     """Time the oracle (the C restatement of ingot's parse) on the host's
     cores over the same frames, bounded: one worker pinned to each CPU this
     process may use (host_cpu_share: affinity mask capped by the cgroup CPU
@@ -306,6 +309,9 @@ def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode
     want = len(allowed)
     if share["cpu_quota"] is not None and share["cpu_quota"] < len(aff):
         want = max(1, min(len(allowed), int(share["cpu_quota"]) - 1))
+    workers = CPU_WORKERS if workers is None else workers
+    if workers:
+        want = max(1, min(want, int(workers)))
     cpus, topo = physical_core_pick(aff, want)
     share = {**share, **topo, "quota_headroom_cpus": len(allowed) - len(cpus)}
     pin = (ctypes.c_int * len(cpus))(*cpus)
@@ -1098,6 +1104,8 @@ def main():
                     help="INGOT_TUNE_* knob for this run, e.g. slow_path=1 (A/B and "
                          "profiling of variants; results never depend on it)")
     ap.add_argument("--cpu-budget", type=float, default=1.5)
+    ap.add_argument("--cpu-workers", type=int, default=0,
+                    help="workers of the all-core CPU baseline (0: one short of the CPU quota)")
     ap.add_argument("--rotate-mib", type=int, default=512,
                     help="minimum bytes of distinct arenas rotated across steps")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
@@ -1108,6 +1116,8 @@ def main():
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
     subline_names(args)  # a bad --sublines fails before any GPU work
+    global CPU_WORKERS
+    CPU_WORKERS = args.cpu_workers
 
     # --- one process per GPU: under a launcher (WORLD_SIZE set) its world
     # must be --gpus; without one, start the ranks here (nothing has touched

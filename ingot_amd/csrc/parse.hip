@@ -732,7 +732,7 @@ bool tuning_valid(int key, int value) {
     case INGOT_TUNE_READ_PLAN:
         return (value >= 0 && value <= 17);
     case INGOT_TUNE_FLOW_KERNEL:
-        return value >= 0 && value <= 11;
+        return value >= 0 && value <= 13;
     default:
         return false;
     }
