@@ -885,10 +885,17 @@ def kernel_sources_sha() -> str:
     return h.hexdigest()[:16]
 
 
+KERNEL_FILE = {"k_parse_read": "read.hip", "k_flows_imgtab": "tuple.hip",
+               "k_parse_pipe": "ring.hip", "k_modify_pipe": "ring.hip",
+               "k_parse_ring": "ring.hip"}
+
+
 def kernel_family(mode: str, ring: bool) -> str:
     """The dominant kernel this config launches (parse.hip's dispatch)."""
     if mode == "read":
         return "k_parse_read"
+    if mode == "flows":  # offset-addressed frames, 16-bit table (tuple.hip)
+        return "k_flows_imgtab"
     if mode == "modify":
         return "k_modify_pipe" if ring else "k_parse"
     return "k_parse_pipe" if ring else "k_parse"
@@ -1581,8 +1588,9 @@ def run_config(args, config, env):
                      (", chunk 0 per packet: ingot_gpu_parse_read_first" if read_first else "") +
                      (", chunk bounds on demand: INGOT_TUNE_READ_PLAN 17)" if read_lazy else ")"),
              "packed": ", LAYOUT_PACKED + k_tile_sums/k_group_scan",
-             "flows": ", OUT_FLOWS16 (parse + Toeplitz hash; the step adds "
-                      "k_flow_count16 / k_flow_reduce16)"}.get(mode, "")
+             "flows": " (tuple.hip: parse + Toeplitz hash from the 16-bit table, copied "
+                      "into each wave's image per tile; the step adds k_flow_count16 / "
+                      "k_flow_reduce16)"}.get(mode, "")
     read_frac_step = step_rd / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS
     return {
         "metric": METRIC,
@@ -1632,7 +1640,7 @@ def run_config(args, config, env):
             "traffic": traffic["bytes_per_launch"] if traffic else None,
             "traffic_detail": traffic,
             "kernel": (traffic or {}).get("kernel") or
-                      f"{family} (ingot_amd/csrc/parse.hip){kname}",
+                      f"{family} (ingot_amd/csrc/{KERNEL_FILE.get(family, 'parse.hip')}){kname}",
             "kernel_sources_sha": sha,
             "batches_per_launch": per_launch,
             "launch_mean_us": round(launch_ms * 1e3, 3),

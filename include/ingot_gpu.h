@@ -528,14 +528,24 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              default to 1, and ingot_gpu_parse_read_dense
  *                              always stages {4,0,0,0} (the knob is ignored)
  *   INGOT_TUNE_FLOW_KERNEL     ingot_gpu_flow_hist at the default windows:
- *                              0 = stage, walk, hash, store per tile
- *                              (default: one tile per wave with the 16-bit
- *                              table, a persistent grid with the 32-bit one);
- *                              1 = the next tile's staging issued before the
- *                              hash of this one (persistent); 2 = the default
- *                              kernel on a persistent grid; 3 = the default
- *                              kernel with the address block's source (LDS
- *                              window or L2) chosen per lane, not per wave
+ *                              0 = measured default: offset-addressed device
+ *                              frames with the 16-bit table use 13, others
+ *                              stage, walk, hash, store per tile (one tile
+ *                              per wave with the 16-bit table, a persistent
+ *                              grid with the 32-bit one); 1 = the next
+ *                              tile's staging issued before the hash of this
+ *                              one (persistent); 2 = that kernel on a
+ *                              persistent grid; 3 = it with the address
+ *                              block's source (LDS window or L2) chosen per
+ *                              lane; 4-9 = the plain parse's window + the
+ *                              5-tuple's missing chunks fetched by a
+ *                              ballot / prefix-scan compacted LDS-DMA (4 / 5
+ *                              / 7 EARLY, 6 / 8 / 9 LATE);
+ *                              10-13 = the table copied into each wave's
+ *                              image per tile (8 blocks per CU; 10 / 11 / 12
+ *                              windows of 4-5 / 2-5 / 3-5 chunks, 13 = 10
+ *                              with per-lane address sources); 14 = the
+ *                              round-3/4 kernel with a block-wide LDS table
  *   INGOT_TUNE_RING_GRID       ingot_gpu_parse_ring: 256-thread blocks per
  *                              CU (1..8; 0 = measured default).  The ring's
  *                              tiles in flight per wave follow
