@@ -1,6 +1,10 @@
-// tuple.hip — config 5's flow classification with the 5-tuple's missing
-// chunks fetched by a wavefront ballot + prefix scan (INGOT_TUNE_FLOW_KERNEL
-// 4..7).
+// tuple.hip — config 5's flow classification kernels:
+//   * k_flows_imgtab (INGOT_TUNE_FLOW_KERNEL 10-13; 13 is the default for
+//     offset-addressed device frames): the plain parse's 5-chunk window and
+//     walk, the Toeplitz table copied into each wave's image per tile
+//     instead of a block-wide LDS copy, so the kernel fits 8 blocks per CU;
+//   * k_flows_tuple (4-9, A/B): the 5-tuple's chunks past the window
+//     fetched by a wavefront ballot + prefix scan, described here.
 //
 // The flows kernel needs bytes the plain parse never reads: the IPv6
 // addresses (frame bytes 22..54 behind 0-2 VLAN tags) and the L4 ports.
