@@ -276,9 +276,9 @@ def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode
     machine), and 1 worker.  Each worker repeats its contiguous share of the
     sample `passes` times per call, so thread start-up is amortised; a share
     is then cache-resident after the first pass — generous to the CPU.  The
-    all-worker figure is the median of three sub-runs (spread reported, with
-    the CPU share the workers obtained and the cgroup's throttled time in
-    each, which name host load when the spread is large).
+    all-worker figure is the median of three sub-runs whose workers got their
+    cores (spread reported, with the CPU share the workers obtained and the
+    cgroup's throttled time in each, which name host load).
     mode "read": parse_read over `segs` = (seg_off, seg_len, pkt_seg);
     "modify": parse + the same setter in place."""
     import ctypes
@@ -355,15 +355,28 @@ def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode
                 round(cpu_s / (el * t), 3),
                 None if th0 is None or th1 is None else round((th1 - th0) / 1e3, 1))
 
+    # The baseline is defined on uncontended cores: the box shares its host,
+    # and a run whose workers got < CLEAN_SHARE of their cores' time measured
+    # other tenants (tools/cpu_share_probe.py: 4-15 workers scale linearly
+    # at share >= 0.98; contended runs fall to 0.5-0.6).  Up to MAX_RUNS runs
+    # until 3 are clean; the value is the median of the clean ones (all runs
+    # reported), or of all runs if fewer than 3 were clean.
+    CLEAN_SHARE, MAX_RUNS = 0.9, 7
     try:
         single = measure(1, budget_s / 3)
-        runs = sorted((measure(len(cpus), budget_s / 3) for _ in range(3)), key=lambda r: r[0])
+        all_runs = []
+        while len(all_runs) < MAX_RUNS:
+            all_runs.append(measure(len(cpus), budget_s / 3))
+            if sum(1 for r in all_runs if r[3] >= CLEAN_SHARE) >= 3:
+                break
     finally:
         lib.oracle_set_passes(1)
         lib.oracle_set_affinity(None, 0)
         if main_aff is not None:
             os.sched_setaffinity(0, main_aff)
-    mp, reps, el = runs[1][:3]
+    clean = [r for r in all_runs if r[3] >= CLEAN_SHARE]
+    runs = sorted(clean if len(clean) >= 3 else all_runs, key=lambda r: r[0])
+    mp, reps, el = runs[len(runs) // 2][:3]
     spread = (runs[-1][0] - runs[0][0]) / mp if mp else 0.0
     what = {"parse": "parse_slice", "read": "parse_read", "modify": "parse + set_destination"}
     return {
@@ -372,14 +385,18 @@ def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode
                   f"{el:.2f} s wall on {len(cpus)} threads, each pinned to one of the CPUs "
                   f"this process may use, one per physical core of one socket across its L3 "
                   f"domains, one short of the cgroup CPU quota, sample copied NUMA-local; "
-                  f"median of 3 "
-                  f"runs; each thread repeats its share, cache-resident after the first pass; "
+                  f"median of 3 runs whose workers got >= {CLEAN_SHARE} of their cores "
+                  f"(up to {MAX_RUNS} runs); each thread repeats its share, cache-resident after "
+                  f"the first pass; "
                   f"C restatement of ingot {what.get(mode, mode)} (oracle/), -march={arch}",
         "single_core_value": round(single[0], 3),
         "scaling_vs_single": round(mp / single[0], 2) if single[0] else None,
         "run_spread": round(spread, 4),
         "runs": [round(r[0], 3) for r in runs],
         "runs_cpu_share": [r[3] for r in runs],
+        "runs_all": [[round(r[0], 3), r[3]] for r in all_runs],
+        "clean_runs": len(clean),
+        "clean_share_threshold": CLEAN_SHARE,
         "runs_throttled_ms": [r[4] for r in runs],
         "single_core_cpu_share": single[3],
         "cpu_model": _cpu_model(),
