@@ -216,7 +216,7 @@ __global__ __launch_bounds__(BLOCK) void k_flows_tuple(FlowArgs args) {
                 if constexpr (OVF == 0) return wimg[slot_of<NCH>(lane, nch + c - c0) * 4u + (q & 3u)];
                 else return ovf[(S + c - c0) * 4u + (q & 3u)];
             }
-            return ldg(reinterpret_cast<const uint32_t*>(a.arena + base + 4u * q), 0);
+            return *reinterpret_cast<const uint32_t*>(a.arena + base + 4u * q);
         };
         FlowWords x;
 #pragma unroll
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(BLOCK) void k_flows_tuple(FlowArgs args) {
 // the kernel arguments, cache hits after the first tiles), hashes from there,
 // and the next tile's staging overwrites it.  One extra L2 round trip per tile for
 // an eighth more resident waves.
-template <uint32_t NCH, int CHAIN, bool LANES, bool PORTS>
+template <uint32_t NCH, int CHAIN, bool LANES>
 __global__ __launch_bounds__(BLOCK, 8) void k_flows_imgtab(FlowArgs args) {
     const ParseArgs& a = args.p;
     constexpr uint32_t SKIP = 12u;
@@ -309,11 +309,11 @@ __global__ __launch_bounds__(BLOCK, 8) void k_flows_imgtab(FlowArgs args) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         Frame<NCH> fr{(const lds_u32*)wimg, lane, sh - SKIP, take, len, a.arena + off};
         Rec r;
-        walk<CHAIN, false, PORTS>(fr, r, nullptr, nullptr);
+        walk<CHAIN, false>(fr, r, nullptr, nullptr);
         bool counted;
         {
             FlowWords x;
-            counted = valid && flow_words<PORTS>(fr, r, x, LANES);
+            counted = valid && flow_words(fr, r, x, LANES);
             // the image is free once every lane's reads of it have returned:
             // park the hash input words behind where the table will go
             // (word k of lane L at dword FLOW_TAB16 + 64 k + L), so that no
@@ -344,19 +344,19 @@ __global__ __launch_bounds__(BLOCK, 8) void k_flows_imgtab(FlowArgs args) {
     }
 }
 
-template <uint32_t NCH, bool LANES = false, bool PORTS = false>
+template <uint32_t NCH, bool LANES = false>
 hipError_t go_imgtab(const FlowArgs& a, int chain, uint32_t g, hipStream_t s) {
     switch (chain) {
     case INGOT_CHAIN_UDP_PARSER:
-        hipLaunchKernelGGL((k_flows_imgtab<NCH, INGOT_CHAIN_UDP_PARSER, LANES, PORTS>), dim3(g),
+        hipLaunchKernelGGL((k_flows_imgtab<NCH, INGOT_CHAIN_UDP_PARSER, LANES>), dim3(g),
                            dim3(BLOCK), 0, s, a);
         break;
     case INGOT_CHAIN_GENERIC_ULP:
-        hipLaunchKernelGGL((k_flows_imgtab<NCH, INGOT_CHAIN_GENERIC_ULP, LANES, PORTS>), dim3(g),
+        hipLaunchKernelGGL((k_flows_imgtab<NCH, INGOT_CHAIN_GENERIC_ULP, LANES>), dim3(g),
                            dim3(BLOCK), 0, s, a);
         break;
     default:
-        hipLaunchKernelGGL((k_flows_imgtab<NCH, INGOT_CHAIN_VLAN_ULP, LANES, PORTS>), dim3(g),
+        hipLaunchKernelGGL((k_flows_imgtab<NCH, INGOT_CHAIN_VLAN_ULP, LANES>), dim3(g),
                            dim3(BLOCK), 0, s, a);
         break;
     }
@@ -392,17 +392,14 @@ hipError_t go_tuple(const FlowArgs& a, int chain, uint32_t g, hipStream_t s) {
 // 9 = 8 with 4-chunk windows (the table then fits 8 blocks per CU);
 // 10 / 11 / 12 = k_flows_imgtab (the table copied into each wave's image per
 // tile) with 4..5 / 2..5 / 3..5-chunk windows; 13 = 10 with the address
-// block's source chosen per lane (flow_words `lanes`); 15 = 13 with the port
-// word read in the walk's L4 step (walk<…, PORTS>).
+// block's source chosen per lane (flow_words `lanes`).
 hipError_t launch_flows_tuple(const FlowArgs& args, int chain, int variant, const Tuning& t,
                               hipStream_t s) {
     FlowArgs a = args;
     a.p.linewin = 2;  // the plain parse's line-completing window (2..NCH)
     const uint32_t g = grid_for(a.p.n, t.max_blocks);
-    if ((variant >= 10 && variant <= 13) || variant == 15 || variant == 16) {  // table in the image
-        a.p.linewin = variant == 11 ? 2u : variant == 12 ? 3u : 4u;  // 4..5 / 2..5 / 3..5
-        if (variant == 15) return go_imgtab<5, true, true>(a, chain, g, s);
-        if (variant == 16) return go_imgtab<5, false, true>(a, chain, g, s);
+    if (variant >= 10 && variant <= 13) {  // table in the image: 4..5 / 2..5 / 3..5 windows
+        a.p.linewin = variant == 11 ? 2u : variant == 12 ? 3u : 4u;
         return variant == 13 ? go_imgtab<5, true>(a, chain, g, s) : go_imgtab<5>(a, chain, g, s);
     }
     switch (variant) {

@@ -29,20 +29,6 @@ constexpr uint32_t BLOCK = WAVE * WAVES;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) void lds_void;
 
-// Frame bytes read by lanes (past the staged window): global-address-space
-// loads.  Through a plain pointer held in a Frame the compiler cannot prove
-// the address space and emits flat loads, which also count in lgkmcnt, so
-// every wait for an LDS read of the window waits for them too.
-typedef __attribute__((address_space(1))) const uint8_t glb_u8;
-typedef __attribute__((address_space(1))) const uint32_t glb_u32;
-typedef uint32_t glb_v4_t __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) const glb_v4_t glb_v4;
-__device__ __forceinline__ glb_u8* glb(const uint8_t* p) { return (glb_u8*)p; }
-template <class T>
-__device__ __forceinline__ T ldg(const T* p, uint64_t i) {
-    return ((__attribute__((address_space(1))) const T*)p)[i];
-}
-
 // HBM -> LDS staging of one 16-B chunk per lane (LDS-DMA).  `nt` (uniform,
 // INGOT_TUNE_CACHE_POLICY bit 0) marks the frame bytes non-temporal: they are
 // read once per launch.
@@ -188,13 +174,13 @@ struct Frame {
     __device__ __forceinline__ void be_words_global8(uint32_t i, uint32_t nw,
                                                      uint32_t* out) const {
         const uintptr_t at = (uintptr_t)(g + i);
-        glb_v4* q = (glb_v4*)(at & ~(uintptr_t)15);
+        const uint4* q = reinterpret_cast<const uint4*>(at & ~(uintptr_t)15);
         const uint32_t r = (uint32_t)(at & 15u);
         const uint32_t end = r + 4u * nw;
-        const glb_v4_t z = {0u, 0u, 0u, 0u};
-        const glb_v4_t c0 = q[0];
-        const glb_v4_t c1 = end > 16u ? q[1] : z;
-        const glb_v4_t c2 = end > 32u ? q[2] : z;
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        const uint4 c0 = q[0];
+        const uint4 c1 = end > 16u ? q[1] : z;
+        const uint4 c2 = end > 32u ? q[2] : z;
         const uint32_t d[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y,
                                 c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
         const uint32_t s = r >> 2;
@@ -212,7 +198,7 @@ struct Frame {
     __device__ __forceinline__ uint32_t be32(uint32_t i) const {
         if (i + 4u <= avail) return be(i, 4);
         const uintptr_t at = (uintptr_t)(g + i);
-        glb_u32* d = (glb_u32*)(at & ~(uintptr_t)3);
+        const uint32_t* d = reinterpret_cast<const uint32_t*>(at & ~(uintptr_t)3);
         const uint32_t r = (uint32_t)(at & 3u);
         const uint32_t d0 = d[0];
         const uint32_t d1 = r ? d[1] : 0u;
@@ -226,7 +212,7 @@ struct Frame {
     // for the same one DRAM sector.
     __device__ __forceinline__ uint32_t beyond(uint32_t i, uint32_t n) const {
         uint32_t v = 0;
-        for (uint32_t k = 0; k < n; ++k) v = (v << 8) | glb(g)[i + k];
+        for (uint32_t k = 0; k < n; ++k) v = (v << 8) | g[i + k];
         return v;
     }
 
@@ -271,8 +257,8 @@ struct SegFrame : Frame<NCH> {
     // next_chunk(): the next chunk starts at logical offset `len`.
     __device__ __forceinline__ void advance() {
         ++k;
-        const uint32_t l = ldg(seg_len, s0 + k);
-        this->g = arena + ldg(seg_off, s0 + k) - this->len;
+        const uint32_t l = seg_len[s0 + k];
+        this->g = arena + seg_off[s0 + k] - this->len;
         const uint32_t e = this->len + l;
         this->len = e > 65535u ? 65535u : e;  // record offsets are u16
     }
@@ -316,8 +302,8 @@ struct SegFrameP {
     __device__ __forceinline__ void bounds() const {
         if constexpr (LAZY) {
             if (nseg == kUnknown) {
-                s0 = ldg(pkt_seg, pi);
-                nseg = ldg(pkt_seg, pi + 1) - s0;
+                s0 = pkt_seg[pi];
+                nseg = pkt_seg[pi + 1] - s0;
             }
         }
     }
@@ -355,7 +341,7 @@ struct SegFrameP {
             return __builtin_bswap32(__builtin_amdgcn_alignbyte(d1, d0, b & 3u)) >> (32u - 8u * n);
         }
         uint32_t v = 0;
-        for (uint32_t j = 0; j < n; ++j) v = (v << 8) | glb(g)[i + j];
+        for (uint32_t j = 0; j < n; ++j) v = (v << 8) | g[i + j];
         return v;
     }
     __device__ __forceinline__ uint32_t get(uint32_t hdr, Field f) const {
@@ -396,10 +382,10 @@ struct SegFrameP {
         else if (NPRE >= 2 && k + 1 < nseg && k == 2) enter(o2, l2, pb(2), staged(2, nseg));
         else if (NPRE >= 3 && k + 1 < nseg && k == 3) enter(o3, l3, pb(3), staged(3, nseg));
         else if constexpr (DENSE) {
-            const uint64_t v = ldg(seg_off, s0 + k);  // (offset << 16) | length
+            const uint64_t v = seg_off[s0 + k];  // (offset << 16) | length
             enter(v >> 16, (uint32_t)(v & 0xffffu), 0u, 0u);
         } else {
-            enter(ldg(seg_off, s0 + k), ldg(seg_len, s0 + k), 0u, 0u);
+            enter(seg_off[s0 + k], seg_len[s0 + k], 0u, 0u);
         }
     }
 };
@@ -408,7 +394,6 @@ struct Rec {
     uint32_t status, err_layer, l3_kind, l4_kind, n_vlan, n_v6ext, l4_proto, flags;
     uint32_t l3_off, l4_off, payload_off, ethertype;
     uint32_t o_udp, o_gen, i_eth;  // tunnel: outer_udp / outer_encap / inner_eth offsets
-    uint32_t ports;  // walk<…, PORTS>: a TCP / UDP header's first 4 bytes (big-endian)
 };
 
 __device__ __forceinline__ uint2 pack8(const Rec& r) {
@@ -523,11 +508,7 @@ __device__ __forceinline__ uint32_t read_error(const FR& f, uint32_t code) {
     return code;
 }
 
-// PORTS (the flows kernels): a TCP / UDP header's port word is read in the
-// L4 step, beside TCP's data offset, into r.ports — for a lane whose L4
-// header lies past its window, in the same round trip as the walk's own last
-// read instead of a dependent one after the walk.
-template <int CHAIN, bool FIELDS, bool PORTS = false, class FR>
+template <int CHAIN, bool FIELDS, class FR>
 __device__ __forceinline__ void walk(FR& f, Rec& r, ingot_fields* F, ingot_tunnel_fields* T) {
     constexpr bool TUN = CHAIN == INGOT_CHAIN_GENEVE_OVER_V6;
     constexpr uint32_t L_L3 = CHAIN == INGOT_CHAIN_VLAN_ULP ? 2u : TUN ? 5u : 1u;
@@ -844,7 +825,6 @@ __device__ __forceinline__ void walk(FR& f, Rec& r, ingot_fields* F, ingot_tunne
     r.l4_off = p;
     if (kind == INGOT_L4_TCP) {
         if (len - p < tcp::LEN) FAIL(L_L4, INGOT_ERR_TOO_SMALL);
-        if constexpr (PORTS) r.ports = f.be32(p);
         const uint32_t doff = f.get(p, tcp::data_offset);
         const uint32_t opt = doff * 4u > 20u ? doff * 4u - 20u : 0u;  // tcp.rs:28
         if (len - p - tcp::LEN < opt) FAIL(L_L4, INGOT_ERR_TOO_SMALL);
@@ -865,7 +845,6 @@ __device__ __forceinline__ void walk(FR& f, Rec& r, ingot_fields* F, ingot_tunne
         p += tcp::LEN + opt;
     } else if (kind == INGOT_L4_UDP) {
         if (len - p < udp::LEN) FAIL(L_L4, INGOT_ERR_TOO_SMALL);
-        if constexpr (PORTS) r.ports = f.be32(p);
         if constexpr (FIELDS) {
             F->l4_source = (uint16_t)f.get(p, udp::source);
             F->l4_destination = (uint16_t)f.get(p, udp::destination);
@@ -1073,17 +1052,14 @@ struct FlowWords {
 // LDS (a split wave runs both paths, each under its lanes' mask) — so that a
 // window ending before some lanes' IPv6 addresses does not send every lane
 // of the wave to L2.
-// PORTS: the port word is the one the walk read (walk<…, PORTS>).
-template <bool PORTS = false, class FR>
+template <class FR>
 __device__ __forceinline__ bool flow_words(const FR& f, const Rec& r, FlowWords& x,
                                            bool lanes = false) {
 #pragma unroll
     for (uint32_t k = 0; k < 9; ++k) x.w[k] = 0;
     if (r.status != INGOT_OK || r.l3_kind == INGOT_L3_NONE) return false;
     const bool ports = r.l4_kind == INGOT_L4_TCP || r.l4_kind == INGOT_L4_UDP;
-    uint32_t pw = 0u;
-    if constexpr (PORTS) pw = r.ports;  // 0 unless the walk parsed TCP / UDP
-    else pw = ports ? f.be32(r.l4_off) : 0u;
+    const uint32_t pw = ports ? f.be32(r.l4_off) : 0u;
     const bool v6 = r.l3_kind == INGOT_L3_IPV6;
     const uint32_t a = r.l3_off + (v6 ? ipv6::SOURCE_BYTE : 12u);  // source address
     const uint32_t naddr = v6 ? 8u : 2u;                            // address words
@@ -1266,7 +1242,7 @@ struct FrameExt {
             return __builtin_bswap32(__builtin_amdgcn_alignbyte(d1, d0, b & 3u)) >> (32u - 8u * n);
         }
         uint32_t v = 0;
-        for (uint32_t k = 0; k < n; ++k) v = (v << 8) | glb(g)[i + k];
+        for (uint32_t k = 0; k < n; ++k) v = (v << 8) | g[i + k];
         return v;
     }
     __device__ __forceinline__ uint32_t get(uint32_t hdr, Field f) const {
