@@ -545,7 +545,12 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              image per tile (8 blocks per CU; 10 / 11 / 12
  *                              windows of 4-5 / 2-5 / 3-5 chunks, 13 = 10
  *                              with per-lane address sources); 14 = the
- *                              round-3/4 kernel with a block-wide LDS table
+ *                              round-3/4 kernel with a block-wide LDS table;
+ *                              15 = 13 without a table (the hash bit by bit
+ *                              from the key windows); 16 = 15 with the key
+ *                              windows' scalar loads one word ahead; 17 =
+ *                              15 with the key held in SGPRs (each window
+ *                              one scalar shift)
  *   INGOT_TUNE_RING_GRID       ingot_gpu_parse_ring: 256-thread blocks per
  *                              CU (1..8; 0 = measured default).  The ring's
  *                              tiles in flight per wave follow

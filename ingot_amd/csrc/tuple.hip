@@ -344,6 +344,105 @@ __global__ __launch_bounds__(BLOCK, 8) void k_flows_imgtab(FlowArgs args) {
     }
 }
 
+// The table-free flows kernel (INGOT_TUNE_FLOW_KERNEL 15): k_flows_imgtab's
+// staging, walk and per-lane address source, and the hash computed bit by bit
+// from the key windows in SGPRs (toeplitz9_bits16): no table copy per tile
+// (one L2 round trip and 2,304 B of LDS writes), no parked words, no LDS reads
+// for the hash; the images are the block's only LDS (20 KiB, 8 blocks per CU).
+template <uint32_t NCH, int CHAIN, int HASH>
+__global__ __launch_bounds__(BLOCK, 8) void k_flows_bits(FlowArgs args) {
+    const ParseArgs& a = args.p;
+    constexpr uint32_t SKIP = 12u;
+    constexpr uint32_t WAVE_DW = WAVE * NCH * 4u;
+    __shared__ __attribute__((aligned(16))) uint32_t s_win[WAVES * WAVE_DW];
+    const uint32_t lane = threadIdx.x & (WAVE - 1u);
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
+    uint32_t* wimg = s_win + wave * WAVE_DW;
+    const uint64_t ntiles = (a.n + WAVE - 1u) / WAVE;
+    const uint32_t mis = (uint32_t)((uintptr_t)a.arena & 31u);
+    const uint64_t tstep = (uint64_t)gridDim.x * WAVES;
+    // HASH 2: the key as nine 64-bit pairs of consecutive dwords (key dword k
+    // = window 32 k; dword 9's top 31 bits = window 287 << 1), in SGPRs
+    uint64_t P[9];
+#pragma unroll
+    for (uint32_t k = 0; k < 9; ++k) {
+        const uint32_t hi = args.w[32u * k];
+        const uint32_t lo = k < 8u ? args.w[32u * (k + 1u)] : args.w[287] << 1;
+        P[k] = HASH == 2 ? ((uint64_t)hi << 32) | lo : 0u;
+    }
+
+    for (uint64_t t = (uint64_t)blockIdx.x * WAVES + wave; t < ntiles; t += tstep) {
+        const uint64_t i = t * WAVE + lane;
+        const bool valid = i < a.n;
+        const uint64_t off = valid ? a.off[i] : 0u;
+        const uint32_t len = valid ? (uint32_t)a.len[i] : 0u;
+        const uint32_t sh = (uint32_t)((off + SKIP + mis) & 15u);
+        const int64_t base = (int64_t)off + (int64_t)SKIP - (int64_t)sh;
+        uint32_t wend = SKIP + 16u * NCH - sh;
+        if (a.linewin) {
+            const uint32_t lp = (uint32_t)((uintptr_t)(a.arena + base) >> 4) & 7u;
+            uint32_t want = ((lp + a.linewin + 7u) & ~7u) - lp;
+            if (want > NCH) want = NCH;
+            wend = SKIP + 16u * want - sh;
+        }
+        const uint32_t take = len < wend ? len : wend;
+        const int32_t staged = (int32_t)take - ((int32_t)SKIP - (int32_t)sh);
+        const uint32_t nch = staged > 0 ? ((uint32_t)staged + 15u) >> 4 : 0u;
+        // every lane's reads of the image (previous tile) have returned
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (uint32_t k = 0; k < NCH; ++k) {
+            const uint32_t q = k * WAVE + lane;
+            const uint32_t pp = q / NCH;
+            const uint32_t c = (q - pp * NCH) ^ swz<NCH>(pp);
+            const uint32_t np = (uint32_t)__shfl((int)nch, (int)pp);
+            const int64_t bp = (int64_t)__shfl((long long)base, (int)pp);
+            if (c < np) stage16(a.arena + bp + 16u * c, wimg + k * WAVE * 4u, false);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        Frame<NCH> fr{(const lds_u32*)wimg, lane, sh - SKIP, take, len, a.arena + off};
+        Rec r;
+        walk<CHAIN, false>(fr, r, nullptr, nullptr);
+        FlowWords x;
+        const bool counted = valid && flow_words(fr, r, x, true);
+        // the key windows in the kernel arguments (FlowArgs is the only
+        // argument, at offset 0); the pointer is made opaque per tile so that
+        // the 144 windows are loaded where the hash uses them instead of held
+        // in SGPRs (spilled) across the loop
+        kar_u32* W = (kar_u32*)((__attribute__((address_space(4))) const uint8_t*)
+                                    __builtin_amdgcn_kernarg_segment_ptr() +
+                                offsetof(FlowArgs, w));
+        asm volatile("" : "+s"(W));
+        uint32_t h = 0u;
+        if constexpr (HASH == 1) h = counted ? toeplitz9_bits16p(x, W) : 0u;
+        else if constexpr (HASH == 2) h = counted ? toeplitz9_bits16s(x, P) : 0u;
+        else h = counted ? toeplitz9_bits16(x, W) : 0u;
+        if (valid) {
+            args.flow[i] = counted ? (h & args.bin_mask) : INGOT_FLOW_NONE;
+            if (args.hash) args.hash[i] = h;
+        }
+    }
+}
+
+template <uint32_t NCH, int HASH>
+hipError_t go_bits(const FlowArgs& a, int chain, uint32_t g, hipStream_t s) {
+    switch (chain) {
+    case INGOT_CHAIN_UDP_PARSER:
+        hipLaunchKernelGGL((k_flows_bits<NCH, INGOT_CHAIN_UDP_PARSER, HASH>), dim3(g), dim3(BLOCK), 0,
+                           s, a);
+        break;
+    case INGOT_CHAIN_GENERIC_ULP:
+        hipLaunchKernelGGL((k_flows_bits<NCH, INGOT_CHAIN_GENERIC_ULP, HASH>), dim3(g), dim3(BLOCK), 0,
+                           s, a);
+        break;
+    default:
+        hipLaunchKernelGGL((k_flows_bits<NCH, INGOT_CHAIN_VLAN_ULP, HASH>), dim3(g), dim3(BLOCK), 0, s,
+                           a);
+        break;
+    }
+    return hipGetLastError();
+}
+
 template <uint32_t NCH, bool LANES = false>
 hipError_t go_imgtab(const FlowArgs& a, int chain, uint32_t g, hipStream_t s) {
     switch (chain) {
@@ -392,12 +491,20 @@ hipError_t go_tuple(const FlowArgs& a, int chain, uint32_t g, hipStream_t s) {
 // 9 = 8 with 4-chunk windows (the table then fits 8 blocks per CU);
 // 10 / 11 / 12 = k_flows_imgtab (the table copied into each wave's image per
 // tile) with 4..5 / 2..5 / 3..5-chunk windows; 13 = 10 with the address
-// block's source chosen per lane (flow_words `lanes`).
+// block's source chosen per lane (flow_words `lanes`); 15 = k_flows_bits
+// (13 without a table: the hash bit by bit from the key windows); 16 = 15 with
+// the windows' scalar loads issued one input word ahead; 17 = 15 with the key
+// held in SGPRs and each window one scalar shift (no loads).
 hipError_t launch_flows_tuple(const FlowArgs& args, int chain, int variant, const Tuning& t,
                               hipStream_t s) {
     FlowArgs a = args;
     a.p.linewin = 2;  // the plain parse's line-completing window (2..NCH)
     const uint32_t g = grid_for(a.p.n, t.max_blocks);
+    if (variant >= 15 && variant <= 17) {  // no table: the hash from the key in SGPRs
+        a.p.linewin = 4u;
+        if (variant == 17) return go_bits<5, 2>(a, chain, g, s);
+        return variant == 16 ? go_bits<5, 1>(a, chain, g, s) : go_bits<5, 0>(a, chain, g, s);
+    }
     if (variant >= 10 && variant <= 13) {  // table in the image: 4..5 / 2..5 / 3..5 windows
         a.p.linewin = variant == 11 ? 2u : variant == 12 ? 3u : 4u;
         return variant == 13 ? go_imgtab<5, true>(a, chain, g, s) : go_imgtab<5>(a, chain, g, s);
