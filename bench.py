@@ -902,7 +902,7 @@ def kernel_sources_sha() -> str:
     return h.hexdigest()[:16]
 
 
-KERNEL_FILE = {"k_parse_read": "read.hip", "k_flows_imgtab": "tuple.hip",
+KERNEL_FILE = {"k_parse_read": "read.hip", "k_flows_bits": "tuple.hip",
                "k_parse_pipe": "ring.hip", "k_modify_pipe": "ring.hip",
                "k_parse_ring": "ring.hip"}
 
@@ -912,7 +912,7 @@ def kernel_family(mode: str, ring: bool) -> str:
     if mode == "read":
         return "k_parse_read"
     if mode == "flows":  # offset-addressed frames, 16-bit table (tuple.hip)
-        return "k_flows_imgtab"
+        return "k_flows_bits"
     if mode == "modify":
         return "k_modify_pipe" if ring else "k_parse"
     return "k_parse_pipe" if ring else "k_parse"

@@ -529,7 +529,7 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              always stages {4,0,0,0} (the knob is ignored)
  *   INGOT_TUNE_FLOW_KERNEL     ingot_gpu_flow_hist at the default windows:
  *                              0 = measured default: offset-addressed device
- *                              frames with the 16-bit table use 13, others
+ *                              frames with the 16-bit table use 15, others
  *                              stage, walk, hash, store per tile (one tile
  *                              per wave with the 16-bit table, a persistent
  *                              grid with the 32-bit one); 1 = the next
@@ -547,10 +547,7 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              with per-lane address sources); 14 = the
  *                              round-3/4 kernel with a block-wide LDS table;
  *                              15 = 13 without a table (the hash bit by bit
- *                              from the key windows); 16 = 15 with the key
- *                              windows' scalar loads one word ahead; 17 =
- *                              15 with the key held in SGPRs (each window
- *                              one scalar shift)
+ *                              from the key windows)
  *   INGOT_TUNE_RING_GRID       ingot_gpu_parse_ring: 256-thread blocks per
  *                              CU (1..8; 0 = measured default).  The ring's
  *                              tiles in flight per wave follow

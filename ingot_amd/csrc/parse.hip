@@ -626,19 +626,20 @@ hipError_t launch_flows_mode(const FlowArgs& a, int layout_kind, int chain, cons
     // persistent; INGOT_TUNE_FLOW_KERNEL = 2 makes the 16-bit one persistent
     // too.  Fixed max_blocks: grid-stride over that many blocks.
     // Offset-addressed device frames, 16-bit table (the C5 case): the
-    // default (0) is k_flows_imgtab with the address block's source chosen
-    // per lane (tuple.hip, variant 13): the Toeplitz table copied into each
-    // wave's window image per tile instead of a block-wide LDS copy, so the
-    // 5-chunk images fit 8 blocks per CU like the plain parse.  Measured on
-    // C5 beside the round-3/4 kernel (14 below): 356.4 -> 332.4 us and
-    // 352.8 -> 335.9 (variant 10) on two boxes, 1.10x the plain parse
-    // (profiles/r04_c5_flows_variants_ab.json).  4..13: the other tuple.hip
-    // variants.
+    // default (0) is k_flows_bits (tuple.hip, variant 15): the plain parse's
+    // staging and walk, the address block's source chosen per lane, and the
+    // Toeplitz hash bit by bit from the key windows in SGPRs — no table, so
+    // the 5-chunk images fit 8 blocks per CU like the plain parse.  Measured
+    // on C5 in six interleaved runs: 1.3-2.2% faster than the table-in-image
+    // kernel (13, the default before it; itself 6-7% faster than the
+    // round-3/4 kernel, 14 below), 1.07-1.09x the plain parse
+    // (profiles/r04_c5_table_free_hash_ab.json, r04_c5_flows_variants_ab.json).
+    // 4..13: the other tuple.hip variants.
     const bool tuple_ok = H16 && layout_kind == LAYOUT_INDEXED && !t.host_arena &&
                           !t.window_indexed && chain != INGOT_CHAIN_GENEVE_OVER_V6;
     if (tuple_ok && (t.flow_kernel == 0 || (t.flow_kernel >= 4 && t.flow_kernel <= 13) ||
-                     (t.flow_kernel >= 15 && t.flow_kernel <= 17)))
-        return launch_flows_tuple(a, chain, t.flow_kernel ? t.flow_kernel : 13, t, s);
+                     t.flow_kernel == 15))
+        return launch_flows_tuple(a, chain, t.flow_kernel ? t.flow_kernel : 15, t, s);
     // 14: the round-3/4 k_parse flows kernel (block-wide LDS table)
     const uint32_t pc =
         t.max_blocks || (H16 && (t.flow_kernel == 0 || t.flow_kernel == 3 || t.flow_kernel == 14))
@@ -744,7 +745,7 @@ bool tuning_valid(int key, int value) {
     case INGOT_TUNE_READ_PLAN:
         return (value >= 0 && value <= 17);
     case INGOT_TUNE_FLOW_KERNEL:
-        return value >= 0 && value <= 17;
+        return value >= 0 && value <= 15;
     default:
         return false;
     }

@@ -1,8 +1,11 @@
 // tuple.hip — config 5's flow classification kernels:
-//   * k_flows_imgtab (INGOT_TUNE_FLOW_KERNEL 10-13; 13 is the default for
+//   * k_flows_bits (INGOT_TUNE_FLOW_KERNEL 15, the default for
 //     offset-addressed device frames): the plain parse's 5-chunk window and
-//     walk, the Toeplitz table copied into each wave's image per tile
-//     instead of a block-wide LDS copy, so the kernel fits 8 blocks per CU;
+//     walk, and the Toeplitz hash computed bit by bit from the key windows in
+//     SGPRs — no table, so the block's LDS is its window images (8 blocks per
+//     CU) and no tile copies a table;
+//   * k_flows_imgtab (10-13; 13 the round-4 default before it): the table
+//     copied into each wave's image per tile instead of a block-wide LDS copy;
 //   * k_flows_tuple (4-9, A/B): the 5-tuple's chunks past the window
 //     fetched by a wavefront ballot + prefix scan, described here.
 //
@@ -349,7 +352,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_flows_imgtab(FlowArgs args) {
 // from the key windows in SGPRs (toeplitz9_bits16): no table copy per tile
 // (one L2 round trip and 2,304 B of LDS writes), no parked words, no LDS reads
 // for the hash; the images are the block's only LDS (20 KiB, 8 blocks per CU).
-template <uint32_t NCH, int CHAIN, int HASH>
+template <uint32_t NCH, int CHAIN>
 __global__ __launch_bounds__(BLOCK, 8) void k_flows_bits(FlowArgs args) {
     const ParseArgs& a = args.p;
     constexpr uint32_t SKIP = 12u;
@@ -361,15 +364,6 @@ __global__ __launch_bounds__(BLOCK, 8) void k_flows_bits(FlowArgs args) {
     const uint64_t ntiles = (a.n + WAVE - 1u) / WAVE;
     const uint32_t mis = (uint32_t)((uintptr_t)a.arena & 31u);
     const uint64_t tstep = (uint64_t)gridDim.x * WAVES;
-    // HASH 2: the key as nine 64-bit pairs of consecutive dwords (key dword k
-    // = window 32 k; dword 9's top 31 bits = window 287 << 1), in SGPRs
-    uint64_t P[9];
-#pragma unroll
-    for (uint32_t k = 0; k < 9; ++k) {
-        const uint32_t hi = args.w[32u * k];
-        const uint32_t lo = k < 8u ? args.w[32u * (k + 1u)] : args.w[287] << 1;
-        P[k] = HASH == 2 ? ((uint64_t)hi << 32) | lo : 0u;
-    }
 
     for (uint64_t t = (uint64_t)blockIdx.x * WAVES + wave; t < ntiles; t += tstep) {
         const uint64_t i = t * WAVE + lane;
@@ -413,10 +407,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_flows_bits(FlowArgs args) {
                                     __builtin_amdgcn_kernarg_segment_ptr() +
                                 offsetof(FlowArgs, w));
         asm volatile("" : "+s"(W));
-        uint32_t h = 0u;
-        if constexpr (HASH == 1) h = counted ? toeplitz9_bits16p(x, W) : 0u;
-        else if constexpr (HASH == 2) h = counted ? toeplitz9_bits16s(x, P) : 0u;
-        else h = counted ? toeplitz9_bits16(x, W) : 0u;
+        const uint32_t h = counted ? toeplitz9_bits16(x, W) : 0u;
         if (valid) {
             args.flow[i] = counted ? (h & args.bin_mask) : INGOT_FLOW_NONE;
             if (args.hash) args.hash[i] = h;
@@ -424,19 +415,19 @@ __global__ __launch_bounds__(BLOCK, 8) void k_flows_bits(FlowArgs args) {
     }
 }
 
-template <uint32_t NCH, int HASH>
+template <uint32_t NCH>
 hipError_t go_bits(const FlowArgs& a, int chain, uint32_t g, hipStream_t s) {
     switch (chain) {
     case INGOT_CHAIN_UDP_PARSER:
-        hipLaunchKernelGGL((k_flows_bits<NCH, INGOT_CHAIN_UDP_PARSER, HASH>), dim3(g), dim3(BLOCK), 0,
+        hipLaunchKernelGGL((k_flows_bits<NCH, INGOT_CHAIN_UDP_PARSER>), dim3(g), dim3(BLOCK), 0,
                            s, a);
         break;
     case INGOT_CHAIN_GENERIC_ULP:
-        hipLaunchKernelGGL((k_flows_bits<NCH, INGOT_CHAIN_GENERIC_ULP, HASH>), dim3(g), dim3(BLOCK), 0,
+        hipLaunchKernelGGL((k_flows_bits<NCH, INGOT_CHAIN_GENERIC_ULP>), dim3(g), dim3(BLOCK), 0,
                            s, a);
         break;
     default:
-        hipLaunchKernelGGL((k_flows_bits<NCH, INGOT_CHAIN_VLAN_ULP, HASH>), dim3(g), dim3(BLOCK), 0, s,
+        hipLaunchKernelGGL((k_flows_bits<NCH, INGOT_CHAIN_VLAN_ULP>), dim3(g), dim3(BLOCK), 0, s,
                            a);
         break;
     }
@@ -492,18 +483,15 @@ hipError_t go_tuple(const FlowArgs& a, int chain, uint32_t g, hipStream_t s) {
 // 10 / 11 / 12 = k_flows_imgtab (the table copied into each wave's image per
 // tile) with 4..5 / 2..5 / 3..5-chunk windows; 13 = 10 with the address
 // block's source chosen per lane (flow_words `lanes`); 15 = k_flows_bits
-// (13 without a table: the hash bit by bit from the key windows); 16 = 15 with
-// the windows' scalar loads issued one input word ahead; 17 = 15 with the key
-// held in SGPRs and each window one scalar shift (no loads).
+// (13 without a table: the hash bit by bit from the key windows; the default).
 hipError_t launch_flows_tuple(const FlowArgs& args, int chain, int variant, const Tuning& t,
                               hipStream_t s) {
     FlowArgs a = args;
     a.p.linewin = 2;  // the plain parse's line-completing window (2..NCH)
     const uint32_t g = grid_for(a.p.n, t.max_blocks);
-    if (variant >= 15 && variant <= 17) {  // no table: the hash from the key in SGPRs
+    if (variant == 15) {  // no table: the hash from the key windows (SGPRs)
         a.p.linewin = 4u;
-        if (variant == 17) return go_bits<5, 2>(a, chain, g, s);
-        return variant == 16 ? go_bits<5, 1>(a, chain, g, s) : go_bits<5, 0>(a, chain, g, s);
+        return go_bits<5>(a, chain, g, s);
     }
     if (variant >= 10 && variant <= 13) {  // table in the image: 4..5 / 2..5 / 3..5 windows
         a.p.linewin = variant == 11 ? 2u : variant == 12 ? 3u : 4u;

@@ -1169,76 +1169,6 @@ __device__ __forceinline__ uint32_t toeplitz9_bits16(const FlowWords& x, kar_u32
     return h;
 }
 
-// toeplitz9_bits16 with the key windows fetched by explicit 64-B scalar
-// loads, one word ahead: word k+1's 16 windows are in flight while word k's
-// 16 v_bitop3 issue (the compiler's own schedule waits for every load right
-// after issuing it).  SMEM loads return out of order, so each wait is
-// lgkmcnt(0); the asm ties the destination registers to the wait so nothing
-// reads them before it.
-typedef uint32_t s16_t __attribute__((ext_vector_type(16)));
-__device__ __forceinline__ s16_t sload16(kar_u32* p) {
-    s16_t v;
-    asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(v) : "s"(p));
-    return v;
-}
-__device__ __forceinline__ void swait(s16_t& v) {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(v));
-}
-// andxor as a volatile asm: kept in program order with the loads and waits
-__device__ __forceinline__ uint32_t andxor_v(uint32_t a, uint32_t b, uint32_t c) {
-    uint32_t r;
-    asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6a" : "=v"(r) : "v"(a), "s"(b), "v"(c));
-    return r;
-}
-__device__ __forceinline__ uint32_t and_v(uint32_t a, uint32_t b) {
-    uint32_t r;
-    asm volatile("v_and_b32 %0, %1, %2" : "=v"(r) : "s"(b), "v"(a));
-    return r;
-}
-__device__ __forceinline__ uint32_t toeplitz9_bits16p(const FlowWords& x, kar_u32* W) {
-    uint32_t t[16];
-    s16_t A = sload16(W + 16);
-    swait(A);
-#pragma unroll
-    for (uint32_t k = 0; k < 9; ++k) {
-        s16_t B;
-        if (k < 8) B = sload16(W + 32u * (k + 1u) + 16u);
-#pragma unroll
-        for (uint32_t q = 0; q < 16; ++q)
-            t[q] = k == 0 ? and_v(x.w[0], A[15u - q]) : andxor_v(x.w[k], A[15u - q], t[q]);
-        if (k < 8) {
-            swait(B);
-            A = B;
-        }
-    }
-    uint32_t h = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < 16; ++q) h |= ((uint32_t)__builtin_popcount(t[q]) & 1u) << q;
-    return h;
-}
-
-// toeplitz9_bits16 with no memory access at all: the key's ten dwords stay
-// in SGPRs for the whole kernel as nine 64-bit pairs P[k] = key dwords k, k+1
-// (P[k] bit 63 = key bit 32 k), and each window is one scalar shift:
-// W[32 k + 31 - q] = low 32 bits of P[k] >> (q + 1).
-__device__ __forceinline__ uint32_t toeplitz9_bits16s(const FlowWords& x, const uint64_t* P) {
-    uint32_t t[16];
-#pragma unroll
-    for (uint32_t k = 0; k < 9; ++k) {
-        uint64_t pk = P[k];
-        asm volatile("" : "+s"(pk));  // the shifts stay here (not 144 values hoisted)
-#pragma unroll
-        for (uint32_t q = 0; q < 16; ++q) {
-            const uint32_t wq = (uint32_t)(pk >> (q + 1u));
-            t[q] = k == 0 ? (x.w[0] & wq) : andxor(x.w[k], wq, t[q]);
-        }
-    }
-    uint32_t h = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < 16; ++q) h |= ((uint32_t)__builtin_popcount(t[q]) & 1u) << q;
-    return h;
-}
-
 template <bool H16, class FR>
 __device__ __forceinline__ bool flow_hash(const FR& f, const Rec& r, const uint32_t* tab,
                                           uint32_t& h, bool lanes = false) {

@@ -164,7 +164,7 @@ def main():
     print("flows fk3", res["flows/VlanUlp/lane_addr_1025"], flush=True)
     # round 4: the compacted 5-tuple kernels (tuple.hip, FLOW_KERNEL 4-9) and
     # the default window, on the FLOWS frames and on adversarial frames
-    for fk in (0, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 15, 16, 17):
+    for fk in (0, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 15):
         c4 = ingot_amd.Context(0)
         c4.set_tuning(TUNE_FLOW_KERNEL, fk)
         f4 = c4.flow_hist(arena, off, lens, Chain.VlanUlp)
@@ -179,7 +179,7 @@ def main():
                                                 seed=args.seed + 40 + int(chain))
         oracle.flow_hist(arena.cpu().numpy(), off.cpu().numpy(), lens.cpu().numpy(), chain)
         w_adv = oracle.flow_hist.last_flows
-        for fk in (0, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 15, 16, 17):
+        for fk in (0, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 15):
             c4 = ingot_amd.Context(0)
             c4.set_tuning(TUNE_FLOW_KERNEL, fk)
             f4 = c4.flow_hist(arena, off, lens, chain)
