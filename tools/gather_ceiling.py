@@ -37,6 +37,7 @@ LIB = ROOT / "tools" / "bin" / "libgather_ceiling.so"
 CONFIGS = {  # name: (GenProfile, frames, Chain)
     "c3": ("MIXED", 1 << 24, "GenericUlp"),
     "c4": ("VLAN_V6EH", 1 << 23, "VlanUlp"),
+    "c5": ("FLOWS", 1 << 23, "VlanUlp"),  # + the flows kernel (flow ids, histogram off)
 }
 
 
@@ -116,6 +117,11 @@ def main():
             lib.gc_touch(a_p, o_p, l_p, ctypes.c_uint64(n), ctypes.c_uint32(12), sp_p, out_p, P(s))
 
         runs = {"parse": run_parse, "stage": run_stage, "touch": run_touch}
+        if name == "c5":
+            def run_flows():
+                ctx.flow_hist(arena, off, lens, ch, flow=out)
+
+            runs["flows"] = run_flows
         for f in runs.values():  # warm
             for _ in range(3):
                 f()
@@ -148,7 +154,11 @@ def main():
                "lines_per_frame": {"header": round(lt / n, 3), "staged": round(ls / n, 3)}}
         rep["G_lines_per_s"] = {"touch (header lines)": round(lt / med["touch"] / 1e3, 2),
                                 "stage (window lines)": round(ls / med["stage"] / 1e3, 2),
-                                "parse (window lines)": round(ls / med["parse"] / 1e3, 2)}
+                                "parse (header lines)": round(lt / med["parse"] / 1e3, 2)}
+        rep["parse_over_touch"] = round(med["parse"] / med["touch"], 3)
+        if "flows" in med:
+            rep["flows_over_touch"] = round(med["flows"] / med["touch"], 3)
+            rep["flows_over_parse"] = round(med["flows"] / med["parse"], 3)
         rep["TB_per_s_of_lines"] = {k: round(v * 128 / 1e3, 3)
                                     for k, v in rep["G_lines_per_s"].items()}
         res["configs"][name] = rep
@@ -156,6 +166,34 @@ def main():
                                                     "G_lines_per_s")}), flush=True)
         del arena, off, lens, rec, out, span
         torch.cuda.empty_cache()
+    # reference: the same touch kernel over consecutive 128-B lines (one line
+    # per lane, 2 GiB), i.e. the streaming line rate
+    n = 1 << 24
+    buf = torch.zeros(n * 128 + 256, dtype=torch.uint8, device="cuda:0")
+    off = torch.arange(n, dtype=torch.int64, device="cuda:0") * 128
+    lens = torch.full((n,), 128, dtype=torch.int16, device="cuda:0")
+    span = torch.full((n,), 1, dtype=torch.int16, device="cuda:0")
+    out = torch.empty(n, dtype=torch.int32, device="cuda:0")
+    s = torch.cuda.current_stream().cuda_stream
+    args_t = (P(buf.data_ptr()), P(off.data_ptr()), P(lens.data_ptr()), ctypes.c_uint64(n),
+              ctypes.c_uint32(0), P(span.data_ptr()), P(out.data_ptr()), P(s))
+    for _ in range(3):
+        lib.gc_touch(*args_t)
+    torch.cuda.synchronize()
+    us = []
+    for _ in range(args.reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.launches):
+            lib.gc_touch(*args_t)
+        e1.record()
+        torch.cuda.synchronize()
+        us.append(e0.elapsed_time(e1) * 1e3 / args.launches)
+    m = statistics.median(us)
+    res["streaming_lines"] = {"lines": n, "median_us": round(m, 2),
+                              "G_lines_per_s": round(n / m / 1e3, 2),
+                              "TB_per_s_of_lines": round(n * 128 / m / 1e6, 3)}
+    print("streaming", json.dumps(res["streaming_lines"]), flush=True)
     Path(args.out).parent.mkdir(parents=True, exist_ok=True)
     Path(args.out).write_text(json.dumps(res, indent=1))
 
