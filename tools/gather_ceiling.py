@@ -117,6 +117,27 @@ def main():
             lib.gc_touch(a_p, o_p, l_p, ctypes.c_uint64(n), ctypes.c_uint32(12), sp_p, out_p, P(s))
 
         runs = {"parse": run_parse, "stage": run_stage, "touch": run_touch}
+        if name == "c3":
+            # c3r: the same frames as [header chunk | payload chunk] through
+            # ingot_gpu_parse_read_first with chunk bounds on demand (the c3r
+            # line's path): the header chunk's lines are the touch lines
+            import bench
+            from ingot_amd import _lib, abi
+
+            seg_off, seg_len, pkt_seg, _ = bench.read_chunks(torch, off, None, lens, r, "split2",
+                                                             "cuda:0")
+            first = ingot_amd.first_chunks(seg_off, seg_len, pkt_seg)
+            ctx_r = ingot_amd.Context(0)
+            ctx_r.set_tuning(abi.TUNE_READ_PLAN, 17)
+            L = _lib.load()
+            rec_r = torch.empty((n, 16), dtype=torch.uint8, device="cuda:0")
+            rargs = (ctx_r._h, arena.data_ptr(), seg_off.data_ptr(), seg_len.data_ptr(),
+                     pkt_seg.data_ptr(), first.data_ptr(), n, int(ch), rec_r.data_ptr(), None)
+
+            def run_read_first():
+                L.ingot_gpu_parse_read_first(*rargs, s)
+
+            runs["parse_read_first (c3r)"] = run_read_first
         if name == "c5":
             def run_flows():
                 ctx.flow_hist(arena, off, lens, ch, flow=out)
@@ -156,6 +177,8 @@ def main():
                                 "stage (window lines)": round(ls / med["stage"] / 1e3, 2),
                                 "parse (header lines)": round(lt / med["parse"] / 1e3, 2)}
         rep["parse_over_touch"] = round(med["parse"] / med["touch"], 3)
+        if "parse_read_first (c3r)" in med:
+            rep["c3r_over_touch"] = round(med["parse_read_first (c3r)"] / med["touch"], 3)
         if "flows" in med:
             rep["flows_over_touch"] = round(med["flows"] / med["touch"], 3)
             rep["flows_over_parse"] = round(med["flows"] / med["parse"], 3)
