@@ -38,6 +38,7 @@ CONFIGS = {  # name: (GenProfile, frames, Chain)
     "c3": ("MIXED", 1 << 24, "GenericUlp"),
     "c4": ("VLAN_V6EH", 1 << 23, "VlanUlp"),
     "c5": ("FLOWS", 1 << 23, "VlanUlp"),  # + the flows kernel (flow ids, histogram off)
+    "c6": ("GENEVE", 1 << 23, "GeneveOverV6Tunnel"),
 }
 
 
