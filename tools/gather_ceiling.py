@@ -79,6 +79,9 @@ def main():
     import ingot_amd
     from ingot_amd import Chain, GenProfile
 
+    unknown = [c for c in args.configs.split(",") if c not in CONFIGS]
+    if unknown:
+        raise SystemExit(f"unknown configs {unknown}; known: {sorted(CONFIGS)}")
     if not LIB.exists():
         raise SystemExit(f"{LIB} missing: run with --build first (in the build container)")
     lib = ctypes.CDLL(str(LIB))
