@@ -26,6 +26,44 @@ def test_rss_verification_vectors(kats):
         assert oracle.toeplitz(key, src + dst + bytes(4)) == v["hash_addrs"]
 
 
+def _key_windows(key: bytes, nbits: int = 288):
+    """W[b] = the 32 key bits starting at input bit b (FlowArgs::w, api.cpp)."""
+    k = int.from_bytes(key, "big")
+    kb = len(key) * 8
+    return [(k >> (kb - 32 - b)) & 0xFFFFFFFF for b in range(nbits)]
+
+
+def _toeplitz16_bit_parity(words, W):
+    """k_flows_bits' form of the hash (walk.h toeplitz9_bits16): bit q of the
+    low 16 bits = parity(XOR_k words[k] & W[32 k + 31 - q])."""
+    h = 0
+    for q in range(16):
+        t = 0
+        for k, x in enumerate(words):
+            t ^= x & W[32 * k + 31 - q]
+        h |= (bin(t).count("1") & 1) << q
+    return h
+
+
+def test_bit_parity_form_is_the_toeplitz_hash(kats):
+    """The table-free hash of the default C5 kernel equals the Toeplitz hash's
+    low 16 bits (the flow bin), on the RSS vectors and on random 36-B inputs."""
+    key = bytes.fromhex(kats["rss_kats"]["key"])
+    W = _key_windows(key)
+    inputs = []
+    for v in kats["rss_kats"]["vectors"]:
+        src = ipaddress.ip_address(v["src"]).packed
+        dst = ipaddress.ip_address(v["dst"]).packed
+        ports = v["sport"].to_bytes(2, "big") + v["dport"].to_bytes(2, "big")
+        inputs.append(src + dst + ports)
+    rng = np.random.default_rng(5)
+    inputs += [rng.integers(0, 256, 36, dtype=np.uint8).tobytes() for _ in range(200)]
+    for data in inputs:
+        data = data + bytes(36 - len(data))
+        words = [int.from_bytes(data[4 * k:4 * k + 4], "big") for k in range(9)]
+        assert _toeplitz16_bit_parity(words, W) == oracle.toeplitz(key, data) & 0xFFFF
+
+
 def test_flow_hash_of_parsed_frames(kats):
     v = kats["rss_kats"]["vectors"][0]
     src = ipaddress.ip_address(v["src"]).packed
