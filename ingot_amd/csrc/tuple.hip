@@ -352,6 +352,8 @@ __global__ __launch_bounds__(BLOCK, 8) void k_flows_imgtab(FlowArgs args) {
 // from the key windows in SGPRs (toeplitz9_bits16): no table copy per tile
 // (one L2 round trip and 2,304 B of LDS writes), no parked words, no LDS reads
 // for the hash; the images are the block's only LDS (20 KiB, 8 blocks per CU).
+static_assert(std::is_standard_layout<FlowArgs>::value,
+              "k_flows_bits reads FlowArgs::w at offsetof() in the kernarg segment");
 template <uint32_t NCH, int CHAIN>
 __global__ __launch_bounds__(BLOCK, 8) void k_flows_bits(FlowArgs args) {
     const ParseArgs& a = args.p;
@@ -400,7 +402,8 @@ __global__ __launch_bounds__(BLOCK, 8) void k_flows_bits(FlowArgs args) {
         FlowWords x;
         const bool counted = valid && flow_words(fr, r, x, true);
         // the key windows in the kernel arguments (FlowArgs is the only
-        // argument, at offset 0); the pointer is made opaque per tile so that
+        // explicit argument: offset 0 of the kernarg segment, the hidden
+        // arguments follow it); the pointer is made opaque per tile so that
         // the 144 windows are loaded where the hash uses them instead of held
         // in SGPRs (spilled) across the loop
         kar_u32* W = (kar_u32*)((__attribute__((address_space(4))) const uint8_t*)
