@@ -1215,12 +1215,21 @@ def subline_names(args) -> list:
     return names
 
 
+# Sub-line warm-up floor (launches).  The gather-bound configs read 4 arena
+# copies of 6.5-13 GB; their first few dozen launches after the allocation
+# run 6-8% slower than the steady state (C5 at 20 steps: warm-up 5 -> 333 /
+# 331 us per flows launch, frac 0.445 / 0.449; warm-up 50 -> 309 us, 0.480;
+# 100 steps after warm-up 5 -> 313 us; tools/r04_c5_edge.sh,
+# profiles/r04_subline_warmup.json).  The main line keeps the driver's W.
+SUBLINE_WARMUP = 50
+
+
 def run_sublines(args, env, run, release=lambda: None):
-    """Each sub-line is `run(sub_args, name, env)` with the main line's steps
-    and warm-up, the config's own stream count, 16-B records and no variants
-    or host path; every rank runs them in the same order (their barriers and
-    collectives pair up).  Returns {name: line} on rank 0, None elsewhere or
-    when there are none."""
+    """Each sub-line is `run(sub_args, name, env)` with the main line's steps,
+    a warm-up of max(W, SUBLINE_WARMUP) launches, the config's own stream
+    count, 16-B records and no variants or host path; every rank runs them in
+    the same order (their barriers and collectives pair up).  Returns
+    {name: line} on rank 0, None elsewhere or when there are none."""
     names = subline_names(args)
     if not names:
         return None
@@ -1230,6 +1239,7 @@ def run_sublines(args, env, run, release=lambda: None):
         sub.config, sub.streams, sub.record, sub.timing = name, STREAMS[name], 16, "launches"
         sub.no_variants, sub.no_host_path = True, True
         sub.stagger_us = None
+        sub.warmup = max(args.warmup, SUBLINE_WARMUP)
         t0 = time.perf_counter()
         line = run(sub, name, env)
         if line is not None:

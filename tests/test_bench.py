@@ -385,7 +385,8 @@ def test_flow_runner_hold_policy_opens_only_at_hold(monkeypatch):
 
 def test_sublines_carry_c3_c4_c5_in_order():
     """The default line's sub-lines: C3, C4, C5 (BASELINE configs[2..4]),
-    each with the main line's steps / warm-up and its own stream count, no
+    each with the main line's steps, a warm-up of at least SUBLINE_WARMUP
+    launches and its own stream count, no
     variants; rank 0 returns them, other ranks None; other configs, --tune
     and --no-sublines carry none; unknown names fail early."""
     import argparse
@@ -404,8 +405,8 @@ def test_sublines_carry_c3_c4_c5_in_order():
     out = bench.run_sublines(args, env0, run, lambda: released.append(1))
     assert list(out) == ["c3", "c4", "c5"]
     assert [s[0] for s in seen] == ["c3", "c4", "c5"]
-    assert all(s[1] == s[0] and s[2:4] == (20, 5) and s[5] and s[6] and s[7] == 16
-               for s in seen)
+    assert all(s[1] == s[0] and s[2:4] == (20, bench.SUBLINE_WARMUP) and s[5] and s[6]
+               and s[7] == 16 for s in seen)
     assert [s[4] for s in seen] == [bench.STREAMS[c] for c in ("c3", "c4", "c5")]
     assert all("wall_s_subline" in v for v in out.values()) and len(released) == 3
     seen.clear()
