@@ -638,7 +638,7 @@ hipError_t launch_flows_mode(const FlowArgs& a, int layout_kind, int chain, cons
     const bool tuple_ok = H16 && layout_kind == LAYOUT_INDEXED && !t.host_arena &&
                           !t.window_indexed && chain != INGOT_CHAIN_GENEVE_OVER_V6;
     if (tuple_ok && (t.flow_kernel == 0 || (t.flow_kernel >= 4 && t.flow_kernel <= 13) ||
-                     (t.flow_kernel >= 15 && t.flow_kernel <= 17)))
+                     t.flow_kernel == 15))
         return launch_flows_tuple(a, chain, t.flow_kernel ? t.flow_kernel : 15, t, s);
     // 14: the round-3/4 k_parse flows kernel (block-wide LDS table)
     const uint32_t pc =
@@ -745,7 +745,7 @@ bool tuning_valid(int key, int value) {
     case INGOT_TUNE_READ_PLAN:
         return (value >= 0 && value <= 17);
     case INGOT_TUNE_FLOW_KERNEL:
-        return value >= 0 && value <= 17;
+        return value >= 0 && value <= 15;
     default:
         return false;
     }

@@ -492,8 +492,8 @@ hipError_t launch_flows_tuple(const FlowArgs& args, int chain, int variant, cons
     FlowArgs a = args;
     a.p.linewin = 2;  // the plain parse's line-completing window (2..NCH)
     const uint32_t g = grid_for(a.p.n, t.max_blocks);
-    if (variant >= 15 && variant <= 17) {  // no table: the hash from the key windows (SGPRs)
-        a.p.linewin = variant == 17 ? 2u : variant == 16 ? 3u : 4u;  // 4..5 / 3..5 / 2..5
+    if (variant == 15) {  // no table: the hash from the key windows (SGPRs)
+        a.p.linewin = 4u;
         return go_bits<5>(a, chain, g, s);
     }
     if (variant >= 10 && variant <= 13) {  // table in the image: 4..5 / 2..5 / 3..5 windows
