@@ -547,9 +547,7 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              with per-lane address sources); 14 = the
  *                              round-3/4 kernel with a block-wide LDS table;
  *                              15 = 13 without a table (the hash bit by bit
- *                              from the key windows); 16 = 15 with the
- *                              histogram's counts added by atomics in the
- *                              same kernel (no separate histogram pass)
+ *                              from the key windows)
  *   INGOT_TUNE_RING_GRID       ingot_gpu_parse_ring: 256-thread blocks per
  *                              CU (1..8; 0 = measured default).  The ring's
  *                              tiles in flight per wave follow

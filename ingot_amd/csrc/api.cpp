@@ -598,12 +598,9 @@ int ingot_gpu_flow_hist_ws(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uin
         a.tab16[e / 2] |= (acc & 0xffffu) << (16u * (e & 1u));
     }
     const hipStream_t s = (hipStream_t)stream;
-    a.hist = d_hist;  // used only by a kernel that fuses the histogram (FLOW_KERNEL 16)
-    bool hist_done = false;
-    if (int e = from_hip(ingot_gpu::launch_flows(a, layout, chain, tuning_for(ctx, d_arena), s,
-                                                 &hist_done)))
+    if (int e = from_hip(ingot_gpu::launch_flows(a, layout, chain, tuning_for(ctx, d_arena), s)))
         return e;
-    if (!d_hist || hist_done) return INGOT_GPU_SUCCESS;
+    if (!d_hist) return INGOT_GPU_SUCCESS;
     return from_hip(ingot_gpu::launch_flow_hist(d_flow, n, d_hist, bins, d_work, work_bytes, s));
 }
 

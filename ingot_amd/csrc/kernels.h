@@ -63,10 +63,6 @@ struct FlowArgs {
     uint32_t bin_mask;
     uint32_t addr_lanes;  // 1: address block read per lane (INGOT_TUNE_FLOW_KERNEL 3)
     uint32_t* hash;  // optional
-    // k_flows_bits<…, HIST> (INGOT_TUNE_FLOW_KERNEL 16): the histogram the
-    // counted bins are added to with device-scope atomics (launch_flows sets
-    // it, and then no separate histogram pass runs)
-    uint32_t* hist = nullptr;
     uint32_t w[FLOW_INPUT_BITS];
     alignas(16) uint32_t tab16[FLOW_TAB16_DW];  // entry (p, v) at half-word 16p + v
 };
@@ -167,10 +163,8 @@ struct Tuning {
 
 hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, int mode,
                         const Tuning& t, hipStream_t s);
-// hist_done (optional): set when the launched kernel also added the counted
-// bins to a.hist (FLOW_KERNEL 16), so the caller skips the histogram pass.
 hipError_t launch_flows(const FlowArgs& a, int layout_kind, int chain, const Tuning& t,
-                        hipStream_t s, bool* hist_done = nullptr);
+                        hipStream_t s);
 hipError_t launch_ring(const RingArgs& a, int chain, int mode, const Tuning& t, hipStream_t s);
 // Flow classification with the 5-tuple's chunks past the plain parse's
 // window fetched by a compacted LDS-DMA pass (tuple.hip): offset-addressed

@@ -638,7 +638,7 @@ hipError_t launch_flows_mode(const FlowArgs& a, int layout_kind, int chain, cons
     const bool tuple_ok = H16 && layout_kind == LAYOUT_INDEXED && !t.host_arena &&
                           !t.window_indexed && chain != INGOT_CHAIN_GENEVE_OVER_V6;
     if (tuple_ok && (t.flow_kernel == 0 || (t.flow_kernel >= 4 && t.flow_kernel <= 13) ||
-                     t.flow_kernel == 15 || t.flow_kernel == 16))
+                     t.flow_kernel == 15))
         return launch_flows_tuple(a, chain, t.flow_kernel ? t.flow_kernel : 15, t, s);
     // 14: the round-3/4 k_parse flows kernel (block-wide LDS table)
     const uint32_t pc =
@@ -692,8 +692,7 @@ hipError_t launch_flows_mode(const FlowArgs& a, int layout_kind, int chain, cons
 }
 
 hipError_t launch_flows(const FlowArgs& args, int layout_kind, int chain, const Tuning& t,
-                        hipStream_t s, bool* hist_done) {
-    if (hist_done) *hist_done = false;
+                        hipStream_t s) {
     if (args.p.n == 0) return hipSuccess;
     FlowArgs a = args;
     a.addr_lanes = t.flow_kernel == 3 ? 1u : 0u;
@@ -708,13 +707,6 @@ hipError_t launch_flows(const FlowArgs& args, int layout_kind, int chain, const 
     // Bins <= 65,536 and no full hash requested: the 16-bit table
     // (OUT_FLOWS16) suffices — the flow bins are identical.
     const bool h16 = t.flow_table != 32 && a.bin_mask <= 0xffffu && !a.hash;
-    // FLOW_KERNEL 16: k_flows_bits with the histogram's atomics fused in, on
-    // the path where k_flows_bits serves (launch_flows_mode's tuple_ok)
-    const bool fused = h16 && t.flow_kernel == 16 && a.hist && layout_kind == LAYOUT_INDEXED &&
-                       !t.host_arena && !t.window_indexed &&
-                       chain != INGOT_CHAIN_GENEVE_OVER_V6;
-    if (!fused) a.hist = nullptr;
-    if (fused && hist_done) *hist_done = true;
     return h16 ? launch_flows_mode<OUT_FLOWS16>(a, layout_kind, chain, t, s)
                : launch_flows_mode<OUT_FLOWS>(a, layout_kind, chain, t, s);
 }
@@ -753,7 +745,7 @@ bool tuning_valid(int key, int value) {
     case INGOT_TUNE_READ_PLAN:
         return (value >= 0 && value <= 17);
     case INGOT_TUNE_FLOW_KERNEL:
-        return value >= 0 && value <= 16;
+        return value >= 0 && value <= 15;
     default:
         return false;
     }

@@ -354,7 +354,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_flows_imgtab(FlowArgs args) {
 // for the hash; the images are the block's only LDS (20 KiB, 8 blocks per CU).
 static_assert(std::is_standard_layout<FlowArgs>::value,
               "k_flows_bits reads FlowArgs::w at offsetof() in the kernarg segment");
-template <uint32_t NCH, int CHAIN, bool HIST>
+template <uint32_t NCH, int CHAIN>
 __global__ __launch_bounds__(BLOCK, 8) void k_flows_bits(FlowArgs args) {
     const ParseArgs& a = args.p;
     constexpr uint32_t SKIP = 12u;
@@ -415,30 +415,22 @@ __global__ __launch_bounds__(BLOCK, 8) void k_flows_bits(FlowArgs args) {
             args.flow[i] = counted ? (h & args.bin_mask) : INGOT_FLOW_NONE;
             if (args.hash) args.hash[i] = h;
         }
-        // HIST: the bin's count, added where the hash is made (no flow-id
-        // re-read, no per-block partial rows); relaxed device-scope adds,
-        // visible to the next kernel on the stream
-        if constexpr (HIST) {
-            if (counted)
-                __hip_atomic_fetch_add(args.hist + (h & args.bin_mask), 1u, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-        }
     }
 }
 
-template <uint32_t NCH, bool HIST>
+template <uint32_t NCH>
 hipError_t go_bits(const FlowArgs& a, int chain, uint32_t g, hipStream_t s) {
     switch (chain) {
     case INGOT_CHAIN_UDP_PARSER:
-        hipLaunchKernelGGL((k_flows_bits<NCH, INGOT_CHAIN_UDP_PARSER, HIST>), dim3(g), dim3(BLOCK), 0,
+        hipLaunchKernelGGL((k_flows_bits<NCH, INGOT_CHAIN_UDP_PARSER>), dim3(g), dim3(BLOCK), 0,
                            s, a);
         break;
     case INGOT_CHAIN_GENERIC_ULP:
-        hipLaunchKernelGGL((k_flows_bits<NCH, INGOT_CHAIN_GENERIC_ULP, HIST>), dim3(g), dim3(BLOCK), 0,
+        hipLaunchKernelGGL((k_flows_bits<NCH, INGOT_CHAIN_GENERIC_ULP>), dim3(g), dim3(BLOCK), 0,
                            s, a);
         break;
     default:
-        hipLaunchKernelGGL((k_flows_bits<NCH, INGOT_CHAIN_VLAN_ULP, HIST>), dim3(g), dim3(BLOCK), 0, s,
+        hipLaunchKernelGGL((k_flows_bits<NCH, INGOT_CHAIN_VLAN_ULP>), dim3(g), dim3(BLOCK), 0, s,
                            a);
         break;
     }
@@ -494,16 +486,15 @@ hipError_t go_tuple(const FlowArgs& a, int chain, uint32_t g, hipStream_t s) {
 // 10 / 11 / 12 = k_flows_imgtab (the table copied into each wave's image per
 // tile) with 4..5 / 2..5 / 3..5-chunk windows; 13 = 10 with the address
 // block's source chosen per lane (flow_words `lanes`); 15 = k_flows_bits
-// (13 without a table: the hash bit by bit from the key windows; the default);
-// 16 = 15 with the histogram's atomics fused in (when a histogram is given).
+// (13 without a table: the hash bit by bit from the key windows; the default).
 hipError_t launch_flows_tuple(const FlowArgs& args, int chain, int variant, const Tuning& t,
                               hipStream_t s) {
     FlowArgs a = args;
     a.p.linewin = 2;  // the plain parse's line-completing window (2..NCH)
     const uint32_t g = grid_for(a.p.n, t.max_blocks);
-    if (variant == 15 || variant == 16) {  // no table: the hash from the key windows (SGPRs)
+    if (variant == 15) {  // no table: the hash from the key windows (SGPRs)
         a.p.linewin = 4u;
-        return a.hist ? go_bits<5, true>(a, chain, g, s) : go_bits<5, false>(a, chain, g, s);
+        return go_bits<5>(a, chain, g, s);
     }
     if (variant >= 10 && variant <= 13) {  // table in the image: 4..5 / 2..5 / 3..5 windows
         a.p.linewin = variant == 11 ? 2u : variant == 12 ? 3u : 4u;

@@ -205,7 +205,7 @@ def test_flow_kernels_every_setting(tune, profile, chain, stride):
 @pytest.mark.parametrize("tune", [{}, {"win": 3}, {"win": 4}, {"win": 8}, {"blocks": 5},
                                   {"fk": 1}, {"fk": 2}, {"win": 25}, {"fk": 3, "win": 1025},
                                   {"fk": 4}, {"fk": 5}, {"fk": 6}, {"fk": 7}, {"fk": 8}, {"fk": 9},
-                                  {"fk": 10}, {"fk": 11}, {"fk": 12}, {"fk": 13}, {"fk": 14}, {"fk": 15}, {"fk": 16},
+                                  {"fk": 10}, {"fk": 11}, {"fk": 12}, {"fk": 13}, {"fk": 14}, {"fk": 15},
                                   {"fk": 10, "blocks": 3}, {"fk": 14, "blocks": 5},
                                   {"fk": 4, "blocks": 3}, {"fk": 6, "blocks": 5}])
 @pytest.mark.parametrize("bins", [1 << 16, 1024])
@@ -310,7 +310,7 @@ def test_flow_hist_many_slices():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fk", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16])
+@pytest.mark.parametrize("fk", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 4097, 262_145])
 def test_flow_ids_ragged_batches(n, fk):
     """Ragged batch sizes on every flows grid (one tile per wave, the
