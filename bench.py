@@ -1219,7 +1219,7 @@ def subline_names(args) -> list:
 # copies of 6.5-13 GB; their first few dozen launches after the allocation
 # run 6-8% slower than the steady state (C5 at 20 steps: warm-up 5 -> 333 /
 # 331 us per flows launch, frac 0.445 / 0.449; warm-up 50 -> 309 us, 0.480;
-# 100 steps after warm-up 5 -> 313 us; tools/r04_c5_edge.sh,
+# 100 steps after warm-up 5 -> 313 us; tools/sessions/r04_c5_edge.sh,
 # profiles/r04_subline_warmup.json).  The main line keeps the driver's W.
 SUBLINE_WARMUP = 50
 
