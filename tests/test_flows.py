@@ -310,6 +310,34 @@ def test_flow_hist_many_slices():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fk", [0, 13, 15])
+@pytest.mark.parametrize("bins", [1, 2, 4096, 1 << 16])
+def test_flow_bins_extreme_bin_counts(fk, bins):
+    """The table-free default kernel at the bin-mask extremes (one bin, two
+    bins, the 16-bit maximum): flow ids and histogram equal the oracle's."""
+    import torch
+
+    import ingot_amd
+    from ingot_amd import GenProfile
+    from ingot_amd.abi import TUNE_FLOW_KERNEL
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    n = 4097
+    ctx = ingot_amd.Context(0)
+    ctx.set_tuning(TUNE_FLOW_KERNEL, fk)
+    arena, off, lens = ingot_amd.gen_frames(GenProfile.FLOWS, n, seed=bins + fk)
+    hist = torch.zeros(bins, dtype=torch.int32, device="cuda")
+    flow = ctx.flow_hist(arena, off, lens, Chain.VlanUlp, hist=hist, bins=bins, n=n,
+                         workspace=ctx.flow_hist_workspace(n, bins))
+    torch.cuda.synchronize()
+    w_hist, _ = oracle.flow_hist(arena.cpu().numpy(), off.cpu().numpy(), lens.cpu().numpy(),
+                                 Chain.VlanUlp, n=n, bins=bins)
+    assert (flow.cpu().numpy().view(np.uint32) == oracle.flow_hist.last_flows).all()
+    assert (hist.cpu().numpy().view(np.uint32) == w_hist).all()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("fk", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 4097, 262_145])
 def test_flow_ids_ragged_batches(n, fk):
