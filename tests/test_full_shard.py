@@ -1,7 +1,8 @@
 """Whole-batch parity at the benchmark sizes: every record (and every flow id
 and hash) of a full BASELINE config batch against the oracle over the exact
 device bytes — not a sample.  C3: 16,777,216 mixed frames (~13 GB); C4 and
-C5: one 8,388,608-frame shard of the 64 M-frame 8-GPU job.  Needs an MI355X
+C5: one 8,388,608-frame shard of the 64 M-frame 8-GPU job; C6: 8,388,608
+Geneve-over-IPv6 frames.  Needs an MI355X
 (`pytest -m gpu`); the oracle runs multi-threaded on the host copy."""
 import os
 
@@ -40,6 +41,7 @@ def _mismatches(got, want):
 @pytest.mark.parametrize("profile,chain,n,first", [
     ("MIXED", Chain.GenericUlp, 1 << 24, 0),            # C3, BASELINE configs[2]
     ("VLAN_V6EH", Chain.VlanUlp, 1 << 23, 5 << 23),     # C4 shard of rank 5 of 8
+    ("GENEVE", Chain.GeneveOverV6Tunnel, 1 << 23, 0),   # C6, the tunnel chain (§8f-1)
 ])
 def test_whole_batch_records_bit_exact(ctx, torch, profile, chain, n, first):
     arena, off, lens = ingot_amd.gen_frames(GenProfile[profile], n, first=first)
