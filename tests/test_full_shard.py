@@ -2,7 +2,7 @@
 and hash) of a full BASELINE config batch against the oracle over the exact
 device bytes — not a sample.  C3: 16,777,216 mixed frames (~13 GB); C4 and
 C5: one 8,388,608-frame shard of the 64 M-frame 8-GPU job; C6: 8,388,608
-Geneve-over-IPv6 frames.  Needs an MI355X
+Geneve-over-IPv6 frames; c3r: the C3 frames as header + payload chunks.  Needs an MI355X
 (`pytest -m gpu`); the oracle runs multi-threaded on the host copy."""
 import os
 
@@ -54,6 +54,36 @@ def test_whole_batch_records_bit_exact(ctx, torch, profile, chain, n, first):
     want = oracle.parse_batch(a, o, ln, chain, nthreads=THREADS)
     bad = _mismatches(got, want)
     assert bad.size == 0, (profile, bad[:5])
+
+
+def test_c3r_whole_batch_parse_read_first_bit_exact(ctx, torch):
+    """c3r (the C3 frames as [header chunk | payload chunk], the header-split
+    shape) through the bench line's path — ingot_gpu_parse_read_first with
+    chunk bounds on demand (INGOT_TUNE_READ_PLAN 17) — every record and
+    remainder chunk of the 16.7 M packets against the oracle's parse_read."""
+    import bench
+    from ingot_amd import abi
+
+    n = 1 << 24
+    arena, off, lens = ingot_amd.gen_frames(GenProfile.MIXED, n)
+    recs0 = ingot_amd.records_to_numpy(ctx.parse(arena, off, lens, Chain.GenericUlp))
+    seg_off, seg_len, pkt_seg, _ = bench.read_chunks(torch, off, None, lens, recs0, "split2",
+                                                     "cuda:0")
+    first = ingot_amd.first_chunks(seg_off, seg_len, pkt_seg)
+    c = ingot_amd.Context(0)
+    c.set_tuning(abi.TUNE_READ_PLAN, 17)
+    out, chunk = c.parse_read(arena, seg_off, seg_len, pkt_seg, Chain.GenericUlp, first=first)
+    torch.cuda.synchronize()
+    got, got_chunk = out.cpu().numpy(), chunk.cpu().numpy().view(np.uint16)
+    a = arena.cpu().numpy()
+    so, sl, ps = seg_off.cpu().numpy(), seg_len.cpu().numpy(), pkt_seg.cpu().numpy()
+    del arena, out, chunk, first, seg_off, seg_len, pkt_seg
+    torch.cuda.empty_cache()
+    want, _, want_chunk = oracle.parse_read_batch(a, so, sl, ps.view(np.uint32), Chain.GenericUlp,
+                                                  nthreads=THREADS)
+    bad = _mismatches(got, want)
+    assert bad.size == 0, bad[:5]
+    assert (got_chunk == want_chunk).all()
 
 
 def test_config5_whole_shard_flow_ids_and_hashes(ctx, torch):
