@@ -2,7 +2,8 @@
 and hash) of a full BASELINE config batch against the oracle over the exact
 device bytes — not a sample.  C3: 16,777,216 mixed frames (~13 GB); C4 and
 C5: one 8,388,608-frame shard of the 64 M-frame 8-GPU job; C6: 8,388,608
-Geneve-over-IPv6 frames; c3r: the C3 frames as header + payload chunks.  Needs an MI355X
+Geneve-over-IPv6 frames; c3r / c3p: the C3 frames as header + payload
+chunks / as lengths only.  Needs an MI355X
 (`pytest -m gpu`); the oracle runs multi-threaded on the host copy."""
 import os
 
@@ -84,6 +85,26 @@ def test_c3r_whole_batch_parse_read_first_bit_exact(ctx, torch):
     bad = _mismatches(got, want)
     assert bad.size == 0, bad[:5]
     assert (got_chunk == want_chunk).all()
+
+
+def test_c3p_whole_batch_packed_offsets_and_records(ctx, torch):
+    """C3p (the C3 frames back to back, lengths only): the offsets the
+    wavefront prefix scan derives equal the lengths' exclusive prefix sum and
+    every record equals the oracle's, all 16.7 M frames."""
+    n = 1 << 24
+    arena, off, lens = ingot_amd.gen_frames(GenProfile.MIXED, n)
+    off_out = torch.empty(n, dtype=torch.int64, device="cuda")
+    recs = ctx.parse_packed(arena, lens, Chain.GenericUlp, off_out=off_out)
+    torch.cuda.synchronize()
+    got, got_off = recs.cpu().numpy(), off_out.cpu().numpy()
+    a, o, ln = arena.cpu().numpy(), off.cpu().numpy(), lens.cpu().numpy()
+    del arena, recs, off_out
+    torch.cuda.empty_cache()
+    assert (got_off == o).all()
+    assert (o[1:] == np.cumsum(ln.astype(np.int64))[:-1]).all() and o[0] == 0
+    want = oracle.parse_batch(a, o, ln, Chain.GenericUlp, nthreads=THREADS)
+    bad = _mismatches(got, want)
+    assert bad.size == 0, bad[:5]
 
 
 def test_config5_whole_shard_flow_ids_and_hashes(ctx, torch):
