@@ -562,6 +562,9 @@ __device__ __forceinline__ void walk(FR& f, Rec& r, ingot_fields* F, ingot_tunne
     if constexpr (TUN) {
         // -- layer 1 outer_v6: #[ingot(from = "L3<Q>")] Ipv6 — the L3 choice
         // parses, then TryFrom keeps only the Ipv6 variant (choice.rs:153-187).
+        // The generated order is parse_choice -> slice step -> conversion
+        // (parse.rs:402-407), so under parse_read an IPv4 header that ends
+        // the last chunk is TooSmall before it can be Unwanted.
         if (et == ET_IPV4) {
             r.l3_kind = INGOT_L3_IPV4;
             r.l3_off = p;
@@ -569,8 +572,10 @@ __device__ __forceinline__ void walk(FR& f, Rec& r, ingot_fields* F, ingot_tunne
             const uint32_t ihl = f.get(p, ipv4::ihl);
             const uint32_t opt = ihl * 4u > 20u ? ihl * 4u - 20u : 0u;
             if (len - p - ipv4::LEN < opt) FAIL(1u, INGOT_ERR_TOO_SMALL);
-            r.payload_off = p + ipv4::LEN + opt;
             r.l4_proto = f.get(p, ipv4::protocol);
+            p += ipv4::LEN + opt;
+            r.payload_off = p;
+            NEXT_SLICE(1u);
             FAIL(1u, INGOT_ERR_UNWANTED);
         }
         if (et != ET_IPV6) FAIL(1u, INGOT_ERR_UNWANTED);
@@ -603,8 +608,9 @@ __device__ __forceinline__ void walk(FR& f, Rec& r, ingot_fields* F, ingot_tunne
         r.l4_proto = h;
         NEXT_SLICE(1u);
 
-        // -- layer 2 outer_udp: #[ingot(from = "L4<Q>")] Udp (TCP parses, then
-        // is Unwanted; anything else is Unwanted at the choice).
+        // -- layer 2 outer_udp: #[ingot(from = "L4<Q>")] Udp (TCP parses, takes
+        // the slice step, then is Unwanted; anything else is Unwanted at the
+        // choice).
         if (h == IPP_TCP) {
             r.l4_kind = INGOT_L4_TCP;
             r.l4_off = p;
@@ -612,7 +618,9 @@ __device__ __forceinline__ void walk(FR& f, Rec& r, ingot_fields* F, ingot_tunne
             const uint32_t doff = f.get(p, tcp::data_offset);
             const uint32_t opt = doff * 4u > 20u ? doff * 4u - 20u : 0u;
             if (len - p - tcp::LEN < opt) FAIL(2u, INGOT_ERR_TOO_SMALL);
-            r.payload_off = p + tcp::LEN + opt;
+            p += tcp::LEN + opt;
+            r.payload_off = p;
+            NEXT_SLICE(2u);
             FAIL(2u, INGOT_ERR_UNWANTED);
         }
         if (h != IPP_UDP) FAIL(2u, INGOT_ERR_UNWANTED);

@@ -548,11 +548,7 @@ static void geneve_chain(walk_t* w, uint32_t et, ingot_fields* inner, ingot_tunn
     }
     if (next_slice(w, 0) != PE_OK) return;
     if (layer_l3(w, 1, et, &proto) != PE_OK) return;
-    if (r->l3_kind != INGOT_L3_IPV6) {
-        fail(w, 1, PE_UNWANTED);
-        return;
-    }
-    if (T) {
+    if (T && r->l3_kind == INGOT_L3_IPV6) {
         const uint8_t* s = f + r->l3_off;
         T->outer_v6_version = (uint8_t)BITS(s, V6_VERSION);
         T->outer_v6_dscp = (uint8_t)BITS(s, V6_DSCP);
@@ -568,9 +564,17 @@ static void geneve_chain(walk_t* w, uint32_t et, ingot_fields* inner, ingot_tunn
         T->outer_v6_n_ext = r->n_v6ext;
         T->outer_l4_proto = (uint8_t)proto;
     }
+    /* The generated layer is parse_choice -> control -> slice step -> from=
+     * conversion (parse.rs:402-407): under parse_read an IPv4 outer header
+     * that ends the last chunk is TooSmall here (parse.rs:208-219,
+     * ingot-types/src/lib.rs:172-173) before TryFrom can say Unwanted. */
     if (next_slice(w, 1) != PE_OK) return;
-    if (layer_l4(w, 2, proto, 0, 1) != PE_OK) return;
-    if (T) {
+    if (r->l3_kind != INGOT_L3_IPV6) {
+        fail(w, 1, PE_UNWANTED);
+        return;
+    }
+    if (layer_l4(w, 2, proto, 0, 0) != PE_OK) return;
+    if (T && r->l4_kind == INGOT_L4_UDP) {
         const uint8_t* s = f + r->l4_off;
         T->outer_udp_off = r->l4_off;
         T->outer_udp_source = (uint16_t)be16(s);
@@ -578,7 +582,12 @@ static void geneve_chain(walk_t* w, uint32_t et, ingot_fields* inner, ingot_tunn
         T->outer_udp_length = (uint16_t)be16(s + 4);
         T->outer_udp_checksum = (uint16_t)be16(s + 6);
     }
+    /* likewise: slice step, then TryFrom<ValidL4> keeps only Udp */
     if (next_slice(w, 2) != PE_OK) return;
+    if (r->l4_kind != INGOT_L4_UDP) {
+        fail(w, 2, PE_UNWANTED);
+        return;
+    }
     e = parse_geneve(f + w->p, w->len - w->p, w->p, &used, T);
     if (e != PE_OK) {
         fail(w, 3, e);

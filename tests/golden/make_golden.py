@@ -547,6 +547,36 @@ def read_kats():
         chain="GeneveOverV6Tunnel", derived="split inside the outer IPv6 header",
         chunks=[hexs(OPTE_IN[:30]), hexs(OPTE_IN[30:])],
         expect=dict(ok=False, error="StraddledHeader", label="outer_v6")))
+    # Derived from the generated layer order parse_choice -> control -> slice
+    # step -> from= conversion (ingot-macros/src/parse.rs:402-407): the slice
+    # step (parse.rs:208-219) pulls the next chunk when the layer consumed its
+    # chunk and, with none left, fails at that layer's label with the
+    # reader's TooSmall (ingot-types/src/lib.rs:172-173) -- before TryFrom
+    # (choice.rs:153-187) can reject the variant.
+    v4_outer = list(OPTE_IN)
+    v4_outer[12:14] = [0x08, 0x00]  # IPv4 over byte 14 = 0x60: ihl 0 -> 20 B, ends at 34
+    out.append(dict(
+        name="tunnel_outer_ipv4_ends_last_chunk", source="ingot-macros/src/parse.rs:402-407",
+        chain="GeneveOverV6Tunnel", chunks=[hexs(v4_outer[:34])],
+        derived="outer IPv4 ends the only chunk: slice step fails before TryFrom",
+        expect=dict(ok=False, error="TooSmall", label="outer_v6", l3="ipv4", chunk=0)))
+    out.append(dict(
+        name="tunnel_outer_ipv4_then_chunk", source="ingot-macros/src/parse.rs:402-407",
+        chain="GeneveOverV6Tunnel", chunks=[hexs(v4_outer[:34]), hexs(v4_outer[34:])],
+        derived="outer IPv4 ends chunk 0, chunk 1 follows: slice step ok, TryFrom Unwanted",
+        expect=dict(ok=False, error="Unwanted", label="outer_v6", l3="ipv4", chunk=1)))
+    tcp_outer = list(OPTE_IN)
+    tcp_outer[20] = 6  # outer next_header TCP; data_offset = byte 66 (0x00) >> 4 = 0 -> 20 B, ends at 74
+    out.append(dict(
+        name="tunnel_outer_tcp_ends_last_chunk", source="ingot-macros/src/parse.rs:402-407",
+        chain="GeneveOverV6Tunnel", chunks=[hexs(tcp_outer[:74])],
+        derived="outer TCP ends the only chunk: slice step fails before TryFrom",
+        expect=dict(ok=False, error="TooSmall", label="outer_udp", l4="tcp", chunk=0)))
+    out.append(dict(
+        name="tunnel_outer_tcp_then_chunk", source="ingot-macros/src/parse.rs:402-407",
+        chain="GeneveOverV6Tunnel", chunks=[hexs(tcp_outer[:74]), hexs(tcp_outer[74:])],
+        derived="outer TCP ends chunk 0, chunk 1 follows: slice step ok, TryFrom Unwanted",
+        expect=dict(ok=False, error="Unwanted", label="outer_udp", l4="tcp", chunk=1)))
     return out
 
 

@@ -337,6 +337,46 @@ def test_first_chunk_descriptor_path_is_bit_exact(ctx, torch, chain, lazy):
     assert np.array_equal(chunk.cpu().numpy().view(np.uint16), w_chunk)
 
 
+@pytest.mark.parametrize("path", ["two_array", "first", "first_lazy", "dense"])
+def test_layer_order_audit_on_device(ctx, torch, kats, path):
+    """The layer-boundary audit (tests/test_read_order.py): every golden frame
+    through every chain, cut at each layer boundary into [head],
+    [head | tail] and [head | empty | tail] and at every byte into two chunks.
+    Device records and chunk indices equal the oracle's, which equal the
+    driver model's (parse.rs:357-416: slice step before the from=
+    conversion)."""
+    from ingot_amd.abi import TUNE_READ_PLAN
+    from tests.test_read_order import audit_cases, compare, expected
+
+    cases = audit_cases(kats)
+    want = expected(cases)
+    c = ctx
+    if path == "first_lazy":
+        c = ingot_amd.Context(0)
+        c.set_tuning(TUNE_READ_PLAN, 17)
+    for chain in Chain:
+        sub = [x for x in cases if x[0] == chain]
+        sub_want = [w for x, w in zip(cases, want) if x[0] == chain]
+        arena, seg_off, seg_len, pkt_seg = oracle.segments([x[1] for x in sub])
+        dev = lambda x, dt: torch.from_numpy(x.view(dt)).cuda()  # noqa: E731
+        d = (dev(arena, np.uint8), dev(seg_off, np.int64), dev(seg_len, np.int16),
+             dev(pkt_seg, np.int32))
+        if path == "dense":
+            dense = (seg_off.astype(np.uint64) << np.uint64(16)) | seg_len.astype(np.uint64)
+            recs, chunk = c.parse_read_dense(d[0], dev(dense, np.int64), d[3], chain)
+        elif path == "two_array":
+            recs, chunk = c.parse_read(*d, chain)
+        else:
+            recs, chunk = c.parse_read(*d, chain, first=ingot_amd.first_chunks(d[1], d[2], d[3]))
+        torch.cuda.synchronize()
+        rec = recs.cpu().numpy().view(ingot_amd.REC_DTYPE).reshape(-1)
+        ch = chunk.cpu().numpy().view(np.uint16)
+        bad = compare(sub, sub_want, rec, ch)
+        assert not bad, (path, chain.name, len(bad), bad[:5])
+        w_rec, _, w_chunk = oracle.parse_read_batch(arena, seg_off, seg_len, pkt_seg, chain)
+        assert rec.tobytes() == w_rec.tobytes() and np.array_equal(ch, w_chunk), (path, chain)
+
+
 def test_first_chunks_helper(torch):
     """first_chunks(): (offset << 16) | length of each packet's chunk 0, 0
     for a packet without chunks."""
