@@ -1125,7 +1125,7 @@ def main():
                     help="time gated regions with torch's default (system-fenced) events "
                          "instead of timing-only HIP events")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
-                    help="INGOT_TUNE_* knob for this run, e.g. slow_path=1 (A/B and "
+                    help="INGOT_TUNE_* knob for this run, e.g. window_indexed=1056 (A/B and "
                          "profiling of variants; results never depend on it)")
     ap.add_argument("--cpu-budget", type=float, default=1.5)
     ap.add_argument("--cpu-workers", type=int, default=0,

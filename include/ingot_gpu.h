@@ -418,8 +418,9 @@ void ingot_gpu_doorbell_destroy(ingot_gpu_doorbell* db);
  *     EVERY batch from the first one not published at launch onward are
  *     undefined (some tiles written, some not); batches published before the
  *     launch are complete.  Every launch ends, rung or not.  Doorbell values
- *     must increase monotonically across ring launches, db_first + nbatches
- *     must fit in 32 bits (else INGOT_GPU_ERANGE), and `db` must belong to
+ *     must increase monotonically across ring launches, the last batch's
+ *     value db_first + nbatches - 1 must fit in 32 bits (else
+ *     INGOT_GPU_ERANGE), and `db` must belong to
  *     ctx's device (else INGOT_GPU_EINVAL).
  * The arenas are read-only for the launch; a batch buffer must not be
  * rewritten while the launch may still read it (a ring reuses a slot only
@@ -461,8 +462,14 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              frames: k = 2, 3, 5 or 8); 1000 + 10 m + k:
  *                              the same from at least m chunks.  Defaults:
  *                              records 25 (the tunnel chain 1069; packed
- *                              tunnel frames 8), flows 1056, fields /
- *                              rewrites 3 (tunnel 8), mapped host memory 5
+ *                              tunnel frames 8), fields / rewrites 3 (tunnel
+ *                              8), mapped host memory 5.  Flows: offset-
+ *                              addressed device frames with 16-bit bins use
+ *                              k_flows_bits over a 4-to-5-chunk window; any
+ *                              explicit value here turns that kernel off and
+ *                              runs the k_parse flows mode with the value
+ *                              (its own default, for the full 32-bit hash,
+ *                              the tunnel chain and host memory: 1056)
  *   INGOT_TUNE_WINDOW_STRIDED  16-B chunks staged per slot: 2,3,4,5,8 or 100
  *                              (default 4 for slots <= 64 B, else 3)
  *   INGOT_TUNE_MAX_BLOCKS      grid cap in 256-thread blocks (0 = one
@@ -471,12 +478,7 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              array, 16- or 8-B records: the multi-tile kernel
  *                              that stages the next tile while parsing one
  *                              (double-buffered LDS).  0 = on, 2 blocks per CU
- *                              (default); 1 = off; k >= 2 = k tiles per wave.
- *                              Frames addressed by offset (16-B records, device
- *                              arenas, default windows, not the tunnel): k >= 2
- *                              = k tiles per wave with the next tile's
- *                              descriptors loaded a tile ahead (default 0: one
- *                              tile per wave)
+ *                              (default); 1 = off; k >= 2 = k tiles per wave
  *   INGOT_TUNE_CACHE_POLICY    0 = measured default (non-temporal record
  *                              stores; the ring kernel: non-temporal staging
  *                              loads and, for 16-B records, device-scope
@@ -498,56 +500,35 @@ int ingot_gpu_stream_delay(ingot_gpu_ctx* ctx, uint32_t ns, void* stream);
  *                              0 / 16 = 16-bit entries when bins <= 65,536
  *                              and no full hash is requested (default), 32 =
  *                              always 32-bit entries (same flow bins)
- *   INGOT_TUNE_SLOW_PATH       bytes past the staged window (indexed frames,
- *                              16-B records, default windows): 0 = read per
- *                              lane from L2/HBM (default), 1 = ballot the
- *                              lanes whose chain outruns the window, re-stage
- *                              a window twice as large for just those frames
- *                              (compacted) and walk them again; 2 = fetch
- *                              only the (up to 4) chunks right after those
- *                              lanes' windows into image slots no lane needs
- *                              any more (ballot + prefix scan) and re-walk
- *                              them from LDS (resume-style)
- *   INGOT_TUNE_READ_PLAN       ingot_gpu_parse_read (16-B records): 16-B
- *                              pieces staged in LDS for each of a packet's
- *                              first four chunks (a packet's last chunk, the
- *                              payload, is never staged): 0 / 11 = chunk 0
- *                              in a line-completing window of 3 to 5 pieces
+ *   INGOT_TUNE_SLOW_PATH       bytes past the staged window: 0 = read per
+ *                              lane from L2/HBM (the only value; the
+ *                              compacted re-stage and resume-style variants
+ *                              lost and were removed: EINVAL)
+ *   INGOT_TUNE_READ_PLAN       ingot_gpu_parse_read / _read_first (16-B
+ *                              records): 0 / 11 = chunk 0 staged in a
+ *                              line-completing window of 3 to 5 16-B pieces
  *                              (to the end of the 128-B line its third piece
- *                              lies in; default), 1 = {4,0,0,0}, 2 =
- *                              {2,2,2,0}, 3 = {4,2,2,0}, 4 = {4,1,1,0},
- *                              5 = {3,0,0,0}, 6 = {2,0,0,0}, 7 / 8 / 10 =
- *                              line-completing 2-8 / 4-8 / 2-5; 9 = no descriptor
- *                              prefetch: chunk 0 staged, later chunks'
- *                              descriptors and bytes read on demand;
- *                              12-14 = persistent grids with a descriptor
- *                              lookahead; 15 / 16 = the default window with
- *                              only chunk 1's / no later chunk's descriptor
- *                              loaded up front (fewer VGPRs).  Chunk
- *                              pools in mapped host memory (ingot_gpu_host_map)
- *                              default to 1, and ingot_gpu_parse_read_dense
- *                              always stages {4,0,0,0} (the knob is ignored)
- *   INGOT_TUNE_FLOW_KERNEL     ingot_gpu_flow_hist at the default windows:
- *                              0 = measured default: offset-addressed device
- *                              frames with the 16-bit table use 15, others
- *                              stage, walk, hash, store per tile (one tile
- *                              per wave with the 16-bit table, a persistent
- *                              grid with the 32-bit one); 1 = the next
- *                              tile's staging issued before the hash of this
- *                              one (persistent); 2 = that kernel on a
- *                              persistent grid; 3 = it with the address
- *                              block's source (LDS window or L2) chosen per
- *                              lane; 4-9 = the plain parse's window + the
- *                              5-tuple's missing chunks fetched by a
- *                              ballot / prefix-scan compacted LDS-DMA (4 / 5
- *                              / 7 EARLY, 6 / 8 / 9 LATE);
- *                              10-13 = the table copied into each wave's
- *                              image per tile (8 blocks per CU; 10 / 11 / 12
- *                              windows of 4-5 / 2-5 / 3-5 chunks, 13 = 10
- *                              with per-lane address sources); 14 = the
- *                              round-3/4 kernel with a block-wide LDS table;
- *                              15 = 13 without a table (the hash bit by bit
- *                              from the key windows)
+ *                              lies in; default); 1 = 4 pieces (the default
+ *                              for chunk pools in mapped host memory,
+ *                              ingot_gpu_host_map); 17 = the default window
+ *                              with the chunk bounds loaded lazily, per lane,
+ *                              only by a walk that leaves chunk 0 or fails
+ *                              in it (ingot_gpu_parse_read_first only: one
+ *                              descriptor stream for header-split packets;
+ *                              elsewhere it means 0).  Field blocks stage 4
+ *                              pieces, and ingot_gpu_parse_read_dense always
+ *                              stages 4 pieces (the knob is ignored there).
+ *                              Other values: EINVAL
+ *   INGOT_TUNE_FLOW_KERNEL     ingot_gpu_flow_hist: 0 / 15 = the measured
+ *                              default (the only values; EINVAL otherwise):
+ *                              offset-addressed device frames with bins <=
+ *                              65,536, no full hash, no explicit window and
+ *                              not the tunnel chain run k_flows_bits (the
+ *                              plain parse's 4-to-5-chunk window, the
+ *                              Toeplitz hash bit by bit from the key windows,
+ *                              no LDS table); everything else runs k_parse's
+ *                              flows mode (LDS table: 16-bit entries one tile
+ *                              per wave, 32-bit entries on a persistent grid)
  *   INGOT_TUNE_RING_GRID       ingot_gpu_parse_ring: 256-thread blocks per
  *                              CU (1..8; 0 = measured default).  The ring's
  *                              tiles in flight per wave follow
@@ -704,8 +685,10 @@ int ingot_gpu_parse_read_dense(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
  * after them (one HBM round trip before the staging, not two).  The chunk
  * table is still read for chunks >= 1.  Records and chunk indices are those
  * of ingot_gpu_parse_read over the same chunks (the caller keeps d_first
- * consistent with the table).  16-B records; INGOT_TUNE_READ_PLAN is not
- * consulted (chunk 0 in the default line-completing 3-5-piece window).
+ * consistent with the table).  16-B records; chunk 0 in the default
+ * line-completing 3-5-piece window (INGOT_TUNE_READ_PLAN 1: 4 pieces; 17:
+ * the chunk bounds loaded only by walks that leave chunk 0 or fail in it —
+ * set it for header-split producers).
  */
 int ingot_gpu_parse_read_first(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
                                const uint64_t* d_seg_off, const uint16_t* d_seg_len,

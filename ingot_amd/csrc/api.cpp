@@ -385,8 +385,10 @@ int ingot_gpu_parse_ring(ingot_gpu_ctx* ctx, const ingot_ring_batch* batches, ui
     if (nbatches > INGOT_RING_MAX_BATCHES) return INGOT_GPU_ERANGE;
     if (stride < 64u || stride % 16u != 0 || stride > 65535u) return INGOT_GPU_ERANGE;
     if (db && (timeout_ms == 0 || timeout_ms > 60000u)) return INGOT_GPU_ERANGE;
-    // the kernel compares the word with db_first + b in 32 bits: no wrap
-    if (db && (uint64_t)db_first + nbatches > 0xffffffffull) return INGOT_GPU_ERANGE;
+    // the kernel compares the word with db_first + b (b < nbatches) in 32
+    // bits: the largest, db_first + nbatches - 1, must not wrap
+    if (db && nbatches && (uint64_t)db_first + nbatches - 1u > 0xffffffffull)
+        return INGOT_GPU_ERANGE;
     if (db && db->device != ctx->device) return INGOT_GPU_EINVAL;
     if (nbatches == 0 || n == 0) return INGOT_GPU_SUCCESS;
     if (!batches) return INGOT_GPU_EINVAL;

@@ -11,7 +11,7 @@ namespace ingot_gpu {
 
 // STRIDED: frame i at i*stride; INDEXED: (off[i], len[i]); SEGMENTED: packet i
 // is the chunks pkt_seg[i] .. pkt_seg[i+1] of (off, len) = (seg_off, seg_len),
-// walked with parse_read's chunk semantics.
+// walked with parse_read's chunk semantics (read.hip).
 // PACKED: frames back to back with only a length array; `off` holds one u64
 // base per group of tiles and `tile_local` each tile's prefix in its group
 // (packed.hip); the frame offsets come from a wavefront prefix scan of the
@@ -61,7 +61,6 @@ struct FlowArgs {
     ParseArgs p;
     uint32_t* flow;  // per-packet bin or INGOT_FLOW_NONE
     uint32_t bin_mask;
-    uint32_t addr_lanes;  // 1: address block read per lane (INGOT_TUNE_FLOW_KERNEL 3)
     uint32_t* hash;  // optional
     uint32_t w[FLOW_INPUT_BITS];
     alignas(16) uint32_t tab16[FLOW_TAB16_DW];  // entry (p, v) at half-word 16p + v
@@ -150,10 +149,10 @@ struct Tuning {
     int writeback = 0;     // ring rewrite kernel: write-back unit (0 = measured default)
     int cache_policy = 0;  // bit 0: nt staging loads; bit 1: nt record stores
     int flow_table = 0;    // flows: 0 = auto (16-bit table when it suffices), 32 = 32-bit
-    int slow_path = 0;     // bytes past the window: 0 = per-lane loads, 1 = compacted re-stage
-    int read_plan = 0;     // parse_read: LDS pieces per staged chunk (see launch_parse)
-    int flow_kernel = 0;   // flows: 0 = k_parse (16-bit table: one tile per wave), 1 = hash
-                           // overlapped with the next tile (k_flows), 2 = k_parse persistent
+    int slow_path = 0;     // bytes past the window: per-lane loads (0, the only value left)
+    int read_plan = 0;     // parse_read: 0 / 11 line-completing chunk-0 window, 1 = 4 pieces,
+                           // 17 = chunk bounds loaded lazily (parse_read_first)
+    int flow_kernel = 0;   // flows: 0 / 15 = the measured default (k_flows_bits when it applies)
     int ring_grid = 0;     // ring consumer: blocks per CU (0 = measured default)
     int ring_groups = 0;   // ring consumer: batches in flight at once (0 = measured default)
     int xcd_remap = 0;     // slot ring: 1 = each XCD's blocks take a contiguous share of tiles
@@ -166,11 +165,10 @@ hipError_t launch_parse(const ParseArgs& a, int layout_kind, int chain, int mode
 hipError_t launch_flows(const FlowArgs& a, int layout_kind, int chain, const Tuning& t,
                         hipStream_t s);
 hipError_t launch_ring(const RingArgs& a, int chain, int mode, const Tuning& t, hipStream_t s);
-// Flow classification with the 5-tuple's chunks past the plain parse's
-// window fetched by a compacted LDS-DMA pass (tuple.hip): offset-addressed
-// device frames, 16-bit table, not the tunnel chain.
-hipError_t launch_flows_tuple(const FlowArgs& a, int chain, int variant, const Tuning& t,
-                              hipStream_t s);
+// Flow classification over the plain parse's window with the table-free
+// Toeplitz hash (tuple.hip, k_flows_bits): offset-addressed device frames,
+// 16-bit bins, not the tunnel chain.
+hipError_t launch_flows_tuple(const FlowArgs& a, int chain, const Tuning& t, hipStream_t s);
 // launch_parse's branches in their own files: parse_read over chunk lists
 // (read.hip; `a` with its cache policy set, `g` the one-tile-per-wave grid)
 // and the slot-ring kernels (ring.hip).

@@ -32,15 +32,8 @@
 namespace ingot_gpu {
 namespace {
 
-// PF (INGOT_TUNE_PIPELINE >= 2 on frames addressed by offset, 16-B records):
-// a grid of fewer waves, each walking several tiles, with the next tile's
-// descriptors loaded while this tile is walked — its (offset, length) are
-// in registers when the next staging starts, one HBM round trip fewer per
-// tile after the first.
-template <uint32_t NCH, int LAYOUT, int CHAIN, int MODE, class ARGS, int SLOW = 0,
-          bool PF = false>
+template <uint32_t NCH, int LAYOUT, int CHAIN, int MODE, class ARGS>
 __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
-    static_assert(!PF || LAYOUT == LAYOUT_INDEXED, "descriptor prefetch: offset-addressed frames");
     const ParseArgs& a = base_args(args);
     constexpr bool TUN = CHAIN == INGOT_CHAIN_GENEVE_OVER_V6;
     constexpr uint32_t WIN = NCH * 16u;
@@ -74,33 +67,17 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
     constexpr uint32_t SKIP =
         NCH == 0 ? 0u
         : FLOWS && LAYOUT == LAYOUT_INDEXED && !TUN ? INGOT_FLOW_SKIP
-        : RECM && SLOW != 1 && (LAYOUT == LAYOUT_INDEXED || LAYOUT == LAYOUT_PACKED) ? INGOT_REC_SKIP
+        : RECM && (LAYOUT == LAYOUT_INDEXED || LAYOUT == LAYOUT_PACKED) ? INGOT_REC_SKIP
                                                                                   : 0u;
     static_assert(SKIP <= 12u, "the walk reads the ethertype at frame byte 12");
 
     const uint64_t tstep = (uint64_t)gridDim.x * WAVES;
-    uint64_t pf_off = 0;  // PF: the next tile's descriptors, loaded a tile ahead
-    uint32_t pf_len = 0;
-    if constexpr (PF) {
-        const uint64_t i0 = ((uint64_t)blockIdx.x * WAVES + wave) * WAVE + lane;
-        if (i0 < a.n) {
-            pf_off = a.off[i0];
-            pf_len = (uint32_t)a.len[i0];
-        }
-    }
     for (uint64_t t = (uint64_t)blockIdx.x * WAVES + wave; t < ntiles; t += tstep) {
         const uint64_t i = t * WAVE + lane;
         const bool valid = i < a.n;
         uint64_t off;
         uint32_t len;
-        uint32_t s0 = 0, nseg = 0;
-        if constexpr (LAYOUT == LAYOUT_SEGMENTED) {
-            // chunk 0 is staged like a frame; the rest is read on demand
-            s0 = valid ? a.pkt_seg[i] : 0u;
-            nseg = valid ? a.pkt_seg[i + 1] - s0 : 0u;
-            off = nseg ? a.off[s0] : 0u;
-            len = nseg ? (uint32_t)a.len[s0] : 0u;
-        } else if constexpr (LAYOUT == LAYOUT_STRIDED) {
+        if constexpr (LAYOUT == LAYOUT_STRIDED) {
             off = i * a.stride;
             len = valid ? (a.len ? (uint32_t)a.len[i] : a.stride) : 0u;
             if (len > a.stride) len = a.stride;  // a slot holds at most one frame
@@ -116,9 +93,6 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
             }
             off = a.off[t / PACKED_GROUP] + a.tile_local[t] + (x - len);
             if (valid && a.off_out) a.off_out[i] = off;
-        } else if constexpr (PF) {
-            off = pf_off;  // zero for a lane past the batch
-            len = pf_len;
         } else {
             off = valid ? a.off[i] : 0u;
             len = valid ? (uint32_t)a.len[i] : 0u;
@@ -175,36 +149,8 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
             if (c < np) stage16p(a.arena + bp + 16u * c, wimg + k * WAVE * 4u, a.policy);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if constexpr (PF) {
-            // behind the staging wait: in flight during this tile's walk
-            const uint64_t in = (t + tstep) * WAVE + lane;
-            pf_off = 0u;
-            pf_len = 0u;
-            if (in < a.n) {
-                pf_off = a.off[in];
-                pf_len = (uint32_t)a.len[in];
-            }
-        }
 
-        static_assert(!SLOW || (LAYOUT == LAYOUT_INDEXED && MODE == OUT_REC16),
-                      "the compacted slow path is built for indexed 16-B records");
-        using FR = typename std::conditional<LAYOUT == LAYOUT_SEGMENTED, SegFrame<NCH>,
-                                             Frame<NCH, SLOW == 1>>::type;
-        FR fr;
-        fr.win = (const lds_u32*)wimg;
-        fr.p = lane;
-        fr.sh = sh - SKIP;
-        fr.avail = take;
-        fr.len = len;
-        fr.g = a.arena + off;
-        if constexpr (LAYOUT == LAYOUT_SEGMENTED) {
-            fr.arena = a.arena;
-            fr.seg_off = a.off;
-            fr.seg_len = a.len;
-            fr.s0 = s0;
-            fr.k = 0;
-            fr.nseg = nseg;
-        }
+        Frame<NCH> fr{(const lds_u32*)wimg, lane, sh - SKIP, take, len, a.arena + off};
         Rec r;
         if constexpr (MODE == OUT_FIELDS) {
             // ingot_fields, or ingot_geneve_fields (inner + outer) for the tunnel.
@@ -255,148 +201,23 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
         } else if constexpr (FLOWS) {
             walk<CHAIN, false>(fr, r, nullptr, nullptr);
             uint32_t h;
-            const bool counted = valid && flow_hash<H16>(fr, r, s_tab, h, args.addr_lanes != 0u);
+            const bool counted = valid && flow_hash<H16>(fr, r, s_tab, h);
             if (valid) {
                 args.flow[i] = counted ? (h & args.bin_mask) : INGOT_FLOW_NONE;
                 if (args.hash) args.hash[i] = h;
             }
-        } else if constexpr (SLOW == 2) {
-            ext_walk<NCH, CHAIN>(valid, wimg, lane, a.arena, base, nch, sh - SKIP, take, len,
-                                 a.arena + off, static_cast<uint4*>(a.out) + i, a.policy);
         } else {
             walk<CHAIN, false>(fr, r, nullptr, nullptr);
-            if constexpr (SLOW == 1)
-                slow_rewalk<NCH, CHAIN>(fr, r, valid, wimg, lane, a.arena, base, sh, len);
             if (valid) store_rec(static_cast<uint4*>(a.out) + i, pack(r), a.policy);
-        }
-        if constexpr (LAYOUT == LAYOUT_SEGMENTED) {
-            if (valid && a.chunk) a.chunk[i] = (uint16_t)fr.k;
         }
         // The next tile's LDS-DMA overwrites this image: every lane's reads
         // above have returned (their values were consumed by the store).
     }
 }
 
-// Flow classification with the hash overlapped (INGOT_TUNE_FLOW_KERNEL = 1):
-// the persistent k_parse<…, OUT_FLOWS*> loop stages a tile, waits, walks,
-// hashes and stores, so the ~72 LDS table lookups per packet run while no
-// HBM request of that wave is in flight.  Here a wave reads its tile's hash
-// input words out of the LDS image into registers right after the walk,
-// issues the next tile's LDS-DMA into the same image (its descriptors were
-// loaded during the walk), and only then computes the Toeplitz hash from
-// the table — the next tile's HBM latency covers the hash.  One LDS image
-// per wave, as in k_parse.
-template <uint32_t NCH, int LAYOUT, int CHAIN, bool H16>
-__global__ __launch_bounds__(BLOCK) void k_flows(FlowArgs args) {
-    static_assert(LAYOUT == LAYOUT_INDEXED || LAYOUT == LAYOUT_STRIDED, "indexed or slots");
-    const ParseArgs& a = args.p;
-    constexpr bool TUN = CHAIN == INGOT_CHAIN_GENEVE_OVER_V6;
-    constexpr uint32_t WIN = NCH * 16u;
-    constexpr uint32_t WAVE_DW = WAVE * NCH * 4u;
-    constexpr uint32_t SKIP = LAYOUT == LAYOUT_INDEXED && !TUN ? INGOT_FLOW_SKIP : 0u;
-    __shared__ __attribute__((aligned(16))) uint32_t s_win[WAVES * WAVE_DW + 16];
-    __shared__ __attribute__((aligned(64))) uint32_t s_tab[H16 ? FLOW_TAB16 : FLOW_TAB];
-    if constexpr (H16) load_flow_table16(s_tab, args.tab16);
-    else build_flow_table(s_tab, args.w);
-    __syncthreads();
-
-    const uint32_t lane = threadIdx.x & (WAVE - 1u);
-    const uint32_t wave = threadIdx.x / WAVE;
-    uint32_t* wimg = s_win + wave * WAVE_DW;
-    const uint64_t ntiles = (a.n + WAVE - 1u) / WAVE;
-    const uint64_t step = (uint64_t)gridDim.x * WAVES;
-    const uint32_t mis = (uint32_t)((uintptr_t)a.arena & 31u);
-
-    // this lane's frame of tile tt: offset and length
-    auto desc = [&](uint64_t tt, uint64_t& off, uint32_t& len) {
-        const uint64_t i = tt * WAVE + lane;
-        const bool valid = i < a.n;
-        if constexpr (LAYOUT == LAYOUT_STRIDED) {
-            off = i * a.stride;
-            len = valid ? (a.len ? (uint32_t)a.len[i] : a.stride) : 0u;
-            if (len > a.stride) len = a.stride;
-        } else {
-            off = valid ? a.off[i] : 0u;
-            len = valid ? (uint32_t)a.len[i] : 0u;
-        }
-    };
-    // the window of a frame (as k_parse): staged bytes and chunk count
-    auto window = [&](uint64_t off, uint32_t len, uint32_t& sh, int64_t& base, uint32_t& take,
-                      uint32_t& nch) {
-        sh = (uint32_t)((off + SKIP + mis) & 15u);
-        base = (int64_t)off + (int64_t)SKIP - (int64_t)sh;
-        if constexpr (SKIP == 0) {
-            take = len < WIN - sh ? len : WIN - sh;
-            nch = (sh + take + 15u) >> 4;
-        } else {
-            const uint32_t wend = SKIP + WIN - sh;
-            take = len < wend ? len : wend;
-            const int32_t staged = (int32_t)take - ((int32_t)SKIP - (int32_t)sh);
-            nch = staged > 0 ? ((uint32_t)staged + 15u) >> 4 : 0u;
-        }
-    };
-    auto stage = [&](uint64_t tt, int64_t base, uint32_t nch) {
-#pragma unroll
-        for (uint32_t k = 0; k < NCH; ++k) {
-            const uint32_t q = k * WAVE + lane;
-            const uint32_t pp = q / NCH;
-            const uint32_t c = (q - pp * NCH) ^ swz<NCH>(pp);
-            const uint32_t np = (uint32_t)__shfl((int)nch, (int)pp);
-            int64_t bp;
-            if constexpr (LAYOUT == LAYOUT_STRIDED) bp = (int64_t)((tt * WAVE + pp) * a.stride);
-            else bp = (int64_t)__shfl((long long)base, (int)pp);
-            if (c < np) stage16(a.arena + bp + 16u * c, wimg + k * WAVE * 4u, false);
-        }
-    };
-
-    uint64_t t = (uint64_t)blockIdx.x * WAVES + wave;
-    if (t >= ntiles) return;
-    uint64_t off;
-    uint32_t len, sh, take, nch;
-    int64_t base;
-    desc(t, off, len);
-    window(off, len, sh, base, take, nch);
-    stage(t, base, nch);
-    for (;;) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t staged
-        const uint64_t tn = t + step;
-        const bool more = tn < ntiles;
-        uint64_t offn = 0;
-        uint32_t lenn = 0;
-        if (more) desc(tn, offn, lenn);  // in flight during the walk
-        const uint64_t i = t * WAVE + lane;
-        const bool valid = i < a.n;
-        Frame<NCH> fr{(const lds_u32*)wimg, lane, sh - SKIP, take, len, a.arena + off};
-        Rec r;
-        walk<CHAIN, false>(fr, r, nullptr, nullptr);
-        FlowWords x;
-        const bool counted = valid && flow_words(fr, r, x);
-        // every lane's reads of the image have returned before the next
-        // tile's LDS-DMA overwrites it
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (more) {
-            window(offn, lenn, sh, base, take, nch);
-            stage(tn, base, nch);
-        }
-        uint32_t h = 0;
-        if (counted) {
-            if constexpr (H16) h = toeplitz9_16(x, s_tab);
-            else h = toeplitz9(x, s_tab);
-        }
-        if (valid) {
-            args.flow[i] = counted ? (h & args.bin_mask) : INGOT_FLOW_NONE;
-            if (args.hash) args.hash[i] = h;
-        }
-        if (!more) break;
-        t = tn;
-        off = offn;
-        len = lenn;
-    }
-}
-
 // persist_cus != 0: a persistent grid, capped at the blocks the device holds
 // at once (cus x resident_per_cu), so no CU runs a second partial round.
-template <uint32_t NCH, int LAYOUT, int MODE, class ARGS, int SLOW = 0, bool PF = false>
+template <uint32_t NCH, int LAYOUT, int MODE, class ARGS>
 hipError_t launch_chain(const ARGS& a, int chain, uint32_t grid, hipStream_t s,
                         uint32_t persist_cus = 0) {
     auto go = [&](auto kernel) {
@@ -409,19 +230,19 @@ hipError_t launch_chain(const ARGS& a, int chain, uint32_t grid, hipStream_t s,
     };
     switch (chain) {
     case INGOT_CHAIN_UDP_PARSER:
-        go(k_parse<NCH, LAYOUT, INGOT_CHAIN_UDP_PARSER, MODE, ARGS, SLOW, PF>);
+        go(k_parse<NCH, LAYOUT, INGOT_CHAIN_UDP_PARSER, MODE, ARGS>);
         break;
     case INGOT_CHAIN_GENERIC_ULP:
-        go(k_parse<NCH, LAYOUT, INGOT_CHAIN_GENERIC_ULP, MODE, ARGS, SLOW, PF>);
+        go(k_parse<NCH, LAYOUT, INGOT_CHAIN_GENERIC_ULP, MODE, ARGS>);
         break;
     case INGOT_CHAIN_VLAN_ULP:
-        go(k_parse<NCH, LAYOUT, INGOT_CHAIN_VLAN_ULP, MODE, ARGS, SLOW, PF>);
+        go(k_parse<NCH, LAYOUT, INGOT_CHAIN_VLAN_ULP, MODE, ARGS>);
         break;
     default:
         if constexpr (MODE == OUT_REC8) {
             return hipErrorInvalidValue;  // not offered for the tunnel (api.cpp)
         } else {
-            go(k_parse<NCH, LAYOUT, INGOT_CHAIN_GENEVE_OVER_V6, MODE, ARGS, SLOW, PF>);
+            go(k_parse<NCH, LAYOUT, INGOT_CHAIN_GENEVE_OVER_V6, MODE, ARGS>);
         }
         break;
     }
@@ -463,15 +284,7 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
     if (t.cache_policy == 0) a.policy = mode == OUT_FIELDS ? 0u : ring ? (mode == OUT_REC16 ? 11u : 3u) : 2u;
     else a.policy = (uint32_t)t.cache_policy & 0x1fbu;
     const uint32_t g = grid_for(a.n, t.max_blocks);
-    if (layout_kind == LAYOUT_SEGMENTED) {
-        // INGOT_TUNE_READ_PLAN 9: the round-1 parse_read kernel (chunk 0
-        // staged, later descriptors and bytes on demand) is k_parse over
-        // SegFrame; every other plan is k_parse_read (read.hip)
-        if (a.len && t.read_plan == 9 && (mode == OUT_FIELDS || mode == OUT_REC16))
-            return mode == OUT_FIELDS ? launch_chain<4, LAYOUT_SEGMENTED, OUT_FIELDS>(a, chain, g, s)
-                                      : launch_chain<4, LAYOUT_SEGMENTED, OUT_REC16>(a, chain, g, s);
-        return launch_segmented(a, chain, mode, t, g, s);
-    }
+    if (layout_kind == LAYOUT_SEGMENTED) return launch_segmented(a, chain, mode, t, g, s);
     // Staged window (16-B chunks per frame); defaults measured on MI355X with
     // interleaved A/B in one process (tools/abtune.py):
     //  * packed frames: 3 chunks (C3 595-598 us/step at 2-3 chunks, 614 at 4,
@@ -532,28 +345,6 @@ hipError_t launch_parse(const ParseArgs& args, int layout_kind, int chain, int m
         default: return launch_mode<5, LAYOUT_PACKED>(a, chain, mode, g, s);
         }
     }
-    // INGOT_TUNE_PIPELINE = k >= 2 (16-B records, device arenas, default
-    // windows, not the tunnel): k tiles per wave with the next tile's
-    // descriptors prefetched (k_parse<..., PF>)
-    if (t.pipeline >= 2 && mode == OUT_REC16 && !host && !t.window_indexed && !tun &&
-        t.slow_path != 1 && layout_kind == LAYOUT_INDEXED) {
-        const uint64_t tiles = (a.n + WAVE - 1) / WAVE;
-        const uint64_t waves = (tiles + (uint64_t)t.pipeline - 1) / (uint64_t)t.pipeline;
-        const uint64_t blocks = (waves + WAVES - 1) / WAVES;
-        return launch_chain<5, LAYOUT_INDEXED, OUT_REC16, ParseArgs, 0, true>(
-            a, chain, (uint32_t)(blocks ? blocks : 1), s);
-    }
-    // The compacted slow path (INGOT_TUNE_SLOW_PATH = 1, 16-B records,
-    // device arenas): default windows only.
-    if (t.slow_path == 1 && mode == OUT_REC16 && !host && !t.window_indexed)
-        return tun ? launch_chain<8, LAYOUT_INDEXED, OUT_REC16, ParseArgs, 1>(a, chain, g, s)
-                   : launch_chain<3, LAYOUT_INDEXED, OUT_REC16, ParseArgs, 1>(a, chain, g, s);
-    // The resume-style slow path (INGOT_TUNE_SLOW_PATH = 2): the default
-    // line-completing windows, then only the missing chunks (ext_rewalk)
-    if (t.slow_path == 2 && mode == OUT_REC16 && !host && !t.window_indexed &&
-        layout_kind == LAYOUT_INDEXED)
-        return tun ? launch_chain<9, LAYOUT_INDEXED, OUT_REC16, ParseArgs, 2>(a, chain, g, s)
-                   : launch_chain<5, LAYOUT_INDEXED, OUT_REC16, ParseArgs, 2>(a, chain, g, s);
     switch (wi ? wi : tun ? 8 : host ? 5 : 3) {
     case 100: return launch_mode<0, LAYOUT_INDEXED>(a, chain, mode, g, s);
     case 2: return launch_mode<2, LAYOUT_INDEXED>(a, chain, mode, g, s);
@@ -592,26 +383,6 @@ hipError_t launch_modify(const ModifyArgs& args, int layout_kind, int chain, con
 // its default window is 5 chunks from the chunk holding byte 12 (SKIP in
 // k_parse: 392 -> 384 us per C5 flow_hist vs 5 chunks from the frame start;
 // 4 chunks from byte 12: 387); the same tuning knobs override the size.
-template <uint32_t NCH, int LAYOUT, bool H16>
-hipError_t launch_flows_pipe(const FlowArgs& a, int chain, uint32_t grid, hipStream_t s,
-                             uint32_t cus) {
-    auto go = [&](auto kernel) {
-        uint32_t g = grid;
-        if (cus) {
-            const uint32_t cap = cus * resident_per_cu(kernel);
-            if (g > cap) g = cap;
-        }
-        hipLaunchKernelGGL(kernel, dim3(g), dim3(BLOCK), 0, s, a);
-    };
-    switch (chain) {
-    case INGOT_CHAIN_UDP_PARSER: go(k_flows<NCH, LAYOUT, INGOT_CHAIN_UDP_PARSER, H16>); break;
-    case INGOT_CHAIN_GENERIC_ULP: go(k_flows<NCH, LAYOUT, INGOT_CHAIN_GENERIC_ULP, H16>); break;
-    case INGOT_CHAIN_VLAN_ULP: go(k_flows<NCH, LAYOUT, INGOT_CHAIN_VLAN_ULP, H16>); break;
-    default: go(k_flows<NCH, LAYOUT, INGOT_CHAIN_GENEVE_OVER_V6, H16>); break;
-    }
-    return hipGetLastError();
-}
-
 template <int MODE>
 hipError_t launch_flows_mode(const FlowArgs& a, int layout_kind, int chain, const Tuning& t,
                              hipStream_t s) {
@@ -625,35 +396,22 @@ hipError_t launch_flows_mode(const FlowArgs& a, int layout_kind, int chain, cons
     // built per block (1,152 entries from the key windows), so its grid is
     // persistent; INGOT_TUNE_FLOW_KERNEL = 2 makes the 16-bit one persistent
     // too.  Fixed max_blocks: grid-stride over that many blocks.
-    // Offset-addressed device frames, 16-bit table (the C5 case): the
-    // default (0) is k_flows_bits (tuple.hip, variant 15): the plain parse's
-    // staging and walk, the address block's source chosen per lane, and the
-    // Toeplitz hash bit by bit from the key windows in SGPRs — no table, so
-    // the 5-chunk images fit 8 blocks per CU like the plain parse.  Measured
-    // on C5 in six interleaved runs: 1.3-2.2% faster than the table-in-image
-    // kernel (13, the default before it; itself 6-7% faster than the
-    // round-3/4 kernel, 14 below), 1.07-1.09x the plain parse
-    // (profiles/r04_c5_table_free_hash_ab.json, r04_c5_flows_variants_ab.json).
-    // 4..13: the other tuple.hip variants.
+    // Offset-addressed device frames, 16-bit table (the C5 case):
+    // k_flows_bits (tuple.hip): the plain parse's staging and walk, the
+    // address block's source chosen per lane, and the Toeplitz hash bit by
+    // bit from the key windows in SGPRs — no table, so the 5-chunk images fit
+    // 8 blocks per CU like the plain parse.  Measured on C5 in six
+    // interleaved runs: 1.3-2.2% faster than a table-in-image kernel, itself
+    // 6-7% faster than this file's k_parse flows mode; 1.07-1.09x the plain
+    // parse (profiles/r04_c5_table_free_hash_ab.json; the losing variants
+    // are in git history).
     const bool tuple_ok = H16 && layout_kind == LAYOUT_INDEXED && !t.host_arena &&
                           !t.window_indexed && chain != INGOT_CHAIN_GENEVE_OVER_V6;
-    if (tuple_ok && (t.flow_kernel == 0 || (t.flow_kernel >= 4 && t.flow_kernel <= 13) ||
-                     t.flow_kernel == 15))
-        return launch_flows_tuple(a, chain, t.flow_kernel ? t.flow_kernel : 15, t, s);
-    // 14: the round-3/4 k_parse flows kernel (block-wide LDS table)
-    const uint32_t pc =
-        t.max_blocks || (H16 && (t.flow_kernel == 0 || t.flow_kernel == 3 || t.flow_kernel == 14))
-            ? 0u : t.cus;
-    // INGOT_TUNE_FLOW_KERNEL = 1: the hash-overlapped kernel (k_flows) at the
-    // default windows.  Measured on C5 (tools/abtune.py, us per step incl.
-    // the histogram): 360.7 vs 363.6 on one stream, 350.2 vs
-    // 337.3 on the bench's two — not the default.
-    if (t.flow_kernel == 1 && !t.window_indexed && !t.window_strided) {
-        if (layout_kind == LAYOUT_STRIDED)
-            return a.p.stride <= 64u ? launch_flows_pipe<4, LAYOUT_STRIDED, H16>(a, chain, g, s, pc)
-                                     : launch_flows_pipe<5, LAYOUT_STRIDED, H16>(a, chain, g, s, pc);
-        return launch_flows_pipe<5, LAYOUT_INDEXED, H16>(a, chain, g, s, pc);
-    }
+    if (tuple_ok) return launch_flows_tuple(a, chain, t, s);
+    // Otherwise k_parse's flows mode (the full 32-bit hash, the tunnel chain,
+    // slots, host arenas, explicit windows): one tile per wave with the
+    // 16-bit table, a persistent grid with the 32-bit one (built per block).
+    const uint32_t pc = t.max_blocks || H16 ? 0u : t.cus;
     if (layout_kind == LAYOUT_STRIDED) {
         switch (t.window_strided ? t.window_strided : (a.p.stride <= 64u ? 4 : 5)) {
         case 3: return launch_chain<3, LAYOUT_STRIDED, MODE>(a, chain, g, s, pc);
@@ -695,7 +453,6 @@ hipError_t launch_flows(const FlowArgs& args, int layout_kind, int chain, const 
                         hipStream_t s) {
     if (args.p.n == 0) return hipSuccess;
     FlowArgs a = args;
-    a.addr_lanes = t.flow_kernel == 3 ? 1u : 0u;
     // With a table built per block, the grid is persistent: exactly the
     // blocks the device holds at once (resident_per_cu, per kernel instance),
     // each wave walking tiles.  Measured on C5 (round 1, 32-bit table built
@@ -740,12 +497,12 @@ bool tuning_valid(int key, int value) {
         return value == 0 || value == 16 || value == 32 || value == 64;
     case INGOT_TUNE_FLOW_TABLE:
         return value == 0 || value == 16 || value == 32;
-    case INGOT_TUNE_SLOW_PATH:
-        return value >= 0 && value <= 2;
+    case INGOT_TUNE_SLOW_PATH:  // per-lane loads past the window only (the others: git history)
+        return value == 0;
     case INGOT_TUNE_READ_PLAN:
-        return (value >= 0 && value <= 17);
-    case INGOT_TUNE_FLOW_KERNEL:
-        return value >= 0 && value <= 15;
+        return value == 0 || value == 1 || value == 11 || value == 17;
+    case INGOT_TUNE_FLOW_KERNEL:  // 15 = the default, k_flows_bits
+        return value == 0 || value == 15;
     default:
         return false;
     }

@@ -6,25 +6,18 @@
 namespace ingot_gpu {
 namespace {
 
-// parse_read over chunk lists with the header chunks staged (SegFrameP): per
-// tile, the packets' chunk bounds and the first four chunks' descriptors are
-// loaded together (independent loads), chunk 0 is staged packet-major like a
-// frame window, the later non-final chunks plane by plane, then the walk —
-// no dependent descriptor or byte load for headers inside staged pieces.
-// One 64-packet tile per wave.
+// parse_read over chunk lists with chunk 0 staged (SegFrameP): per tile, the
+// packets' chunk bounds and the first four chunks' descriptors are loaded
+// together (independent loads), chunk 0 is staged packet-major like a frame
+// window (with any later non-final chunk that lies inside that window), then
+// the walk — no dependent descriptor or byte load for headers inside staged
+// pieces.  One 64-packet tile per wave.  (Staging later chunks in planes, a
+// persistent grid with a descriptor lookahead and fewer prefetched
+// descriptors all measured slower — DESIGN.md §1b; git history, round 4.)
 //
-// PIPE (persistent grid, INGOT_TUNE_READ_PLAN 12-14): the chain pkt_seg ->
-// chunk-0 descriptor -> staging is three dependent HBM round trips per tile,
-// and one tile per wave left them exposed.  A persistent wave instead keeps
-// the next tiles' lookups in flight while it walks the current one: tile
-// t + W's chunk-0 descriptor and tile t + 2W's chunk bounds are issued right
-// after tile t's staging: the staging and the lookahead loads are in flight
-// together and the wave waits for both (one round trip instead of three).
-//
-// NPRE (0..3): descriptors of chunks 1..NPRE loaded with chunk 0's (when not
-// the packet's last); later chunks are looked up when the walk reaches them.
-// Each prefetched descriptor holds 3 VGPRs through the walk: NPRE 3 is 68
-// VGPRs (7 waves per SIMD), NPRE 1 is 63 and NPRE 0 is 59 (8 waves).
+// NPRE (0 or 3): descriptors of chunks 1..NPRE loaded with chunk 0's (when
+// not the packet's last); later chunks are looked up when the walk reaches
+// them.
 //
 // FIRST (ingot_gpu_parse_read_first): chunk 0's descriptor comes from the
 // per-packet array a.first, indexed by the packet like pkt_seg, so it is
@@ -35,16 +28,12 @@ namespace {
 // loaded per tile at all — chunk 0 comes from a.first — but by the walk, per
 // lane, only when it needs them (SegFrameP::bounds): one descriptor stream
 // (8 B per packet) instead of two for packets whose headers lie in chunk 0.
-template <int CS0, int CS1, int CS2, int CS3, int CHAIN, int MODE, bool DENSE = false,
-          bool PIPE = false, int NPRE = 3, bool FIRST = false, bool LAZY = false>
+template <int CS0, int CHAIN, int MODE, bool DENSE = false, int NPRE = 3, bool FIRST = false,
+          bool LAZY = false>
 __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
-    static_assert(!(FIRST && PIPE), "the lookahead kernel loads chunk 0 from the table");
     static_assert(!LAZY || (FIRST && NPRE == 0), "lazy bounds: chunk 0 per packet, no prefetch");
-    using FR = SegFrameP<CS0, CS1, CS2, CS3, DENSE, NPRE, LAZY>;
-    static_assert((CS1 == 0 || NPRE >= 1) && (CS2 == 0 || NPRE >= 2) && (CS3 == 0 || NPRE >= 3),
-                  "a chunk staged in planes needs its descriptor up front");
-    constexpr uint32_t P = CS0 + CS1 + CS2 + CS3;
-    constexpr uint32_t WAVE_DW = WAVE * P * 4u;
+    using FR = SegFrameP<CS0, DENSE, NPRE, LAZY>;
+    constexpr uint32_t WAVE_DW = WAVE * CS0 * 4u;
     constexpr bool TUN = CHAIN == INGOT_CHAIN_GENEVE_OVER_V6;
     // no slack past the last image: SegFrameP::be clamps the second dword of
     // a pair to the current chunk's staged pieces (a 5-piece image is then
@@ -93,13 +82,12 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
         o = ns ? v >> 16 : 0u;  // (LAZY: ns is kUnknown for every packet of the batch)
         l = ns ? (uint32_t)(v & 0xffffu) : 0u;
     };
-    uint32_t s0, nseg, s0n = 0, nsn = 0;
+    uint32_t s0, nseg;
     uint64_t o0;
     uint32_t l0;
     load_pkt(t, s0, nseg);
     if constexpr (FIRST) load_first(t, nseg, o0, l0);
     else load_d0(s0, nseg, o0, l0);
-    if constexpr (PIPE) load_pkt(t + W < ntiles ? t + W : t, s0n, nsn);
 
     for (;;) {
         const uint64_t i = t * WAVE + lane;
@@ -152,11 +140,11 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
         // (nothing when chunk 0 ends before byte SKIP)
         const int64_t e0 = (int64_t)sh0 + (int64_t)fr.l0 - (int64_t)SKIP;
         uint32_t ext = nseg && e0 > 0 ? (e0 < (int64_t)wlim ? (uint32_t)e0 : wlim) : 0u;
-        // a later non-last chunk without planes that starts inside chunk 0's
-        // window: stage the window's pieces up to its end (or the window's)
+        // a later non-last chunk that starts inside chunk 0's window: stage
+        // the window's pieces up to its end (or the window's)
         auto widen = [&](uint32_t e, uint64_t o, uint32_t l) {
             const int64_t d = (int64_t)o - base0;
-            if (FR::cs(e) == 0 && e + 1 < nseg && d >= 0 && d < (int64_t)wlim) {
+            if (e + 1 < nseg && d >= 0 && d < (int64_t)wlim) {
                 const uint32_t end = (uint32_t)d + l < wlim ? (uint32_t)d + l : wlim;
                 ext = end > ext ? end : ext;
             }
@@ -174,30 +162,6 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
             const int64_t bp = (int64_t)__shfl((long long)base0, (int)pp);
             if (c < np) stage16(a.arena + bp + 16u * c, wimg + k * WAVE * 4u, false);
         }
-        // chunks 1..3 unless last: piece j of chunk e into plane CS0 + pb(e) + j
-        auto stage_chunk = [&](uint32_t e, uint64_t o, uint32_t l) {
-            const uint32_t sh = (uint32_t)((uintptr_t)(a.arena + o) & 15u);
-            const uint32_t c = FR::staged(e, nseg);
-            for (uint32_t j = 0; j < FR::cs(e); ++j)
-                if (j < c && 16u * j < sh + l)
-                    stage16(a.arena + o - sh + 16u * j,
-                            wimg + (CS0 + FR::pb(e) + j) * WAVE * 4u, false);
-        };
-        if constexpr (CS1 > 0) stage_chunk(1, fr.o1, fr.l1);
-        if constexpr (CS2 > 0) stage_chunk(2, fr.o2, fr.l2);
-        if constexpr (CS3 > 0) stage_chunk(3, fr.o3, fr.l3);
-        uint32_t s0nn = 0, nsnn = 0;
-        uint64_t o0n = 0;
-        uint32_t l0n = 0;
-        if constexpr (PIPE) {
-            // lookahead, issued behind the staging (the compiler may not
-            // hoist loads across the barrier): tile t+W's chunk-0
-            // descriptor, tile t+2W's bounds
-            asm volatile("" ::: "memory");
-            load_d0(s0n, nsn, o0n, l0n);
-            const uint64_t t2 = t + 2u * W;
-            load_pkt(t2 < ntiles ? t2 : t, s0nn, nsnn);
-        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
         fr.win = (const lds_u32*)wimg;
@@ -213,7 +177,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
         fr.L = 0;
         fr.b0 = base0;
         fr.span0 = 16u * n0;
-        fr.enter(fr.o0, fr.l0, 0u, nseg ? want : 0u);
+        fr.enter(fr.o0, fr.l0, nseg ? want : 0u);
         if constexpr (SKIP != 0) {
             // chunk-0 byte i >= SKIP is staged byte i + sh0 - SKIP (mod 2^32);
             // bytes [0, avail) count as staged (those below SKIP are never read)
@@ -250,47 +214,32 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         t += W;
         if (t >= ntiles) break;
-        if constexpr (PIPE) {
-            s0 = s0n;
-            nseg = nsn;
-            o0 = o0n;
-            l0 = l0n;
-            s0n = s0nn;
-            nsn = nsnn;
-        } else {
-            load_pkt(t, s0, nseg);
-            if constexpr (FIRST) load_first(t, nseg, o0, l0);
-            else load_d0(s0, nseg, o0, l0);
-        }
+        load_pkt(t, s0, nseg);
+        if constexpr (FIRST) load_first(t, nseg, o0, l0);
+        else load_d0(s0, nseg, o0, l0);
     }
 }
 
-// persist_cus != 0 (the PIPE kernels): a persistent grid of the blocks the
-// device holds at once.
-template <int CS0, int CS1, int CS2, int CS3, int MODE, bool DENSE = false, bool PIPE = false,
-          int NPRE = 3, bool FIRST = false, bool LAZY = false>
-hipError_t launch_read(const ParseArgs& a, int chain, uint32_t grid, hipStream_t s,
-                       uint32_t persist_cus = 0) {
-    auto go = [&](auto kernel) {
-        uint32_t g = grid;
-        if (persist_cus) {
-            const uint32_t cap = persist_cus * resident_per_cu(kernel);
-            if (g > cap) g = cap;
-        }
-        hipLaunchKernelGGL(kernel, dim3(g), dim3(BLOCK), 0, s, a);
-    };
+template <int CS0, int MODE, bool DENSE = false, int NPRE = 3, bool FIRST = false,
+          bool LAZY = false>
+hipError_t launch_read(const ParseArgs& a, int chain, uint32_t g, hipStream_t s) {
     switch (chain) {
     case INGOT_CHAIN_UDP_PARSER:
-        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_UDP_PARSER, MODE, DENSE, PIPE, NPRE, FIRST, LAZY>);
+        hipLaunchKernelGGL((k_parse_read<CS0, INGOT_CHAIN_UDP_PARSER, MODE, DENSE, NPRE, FIRST, LAZY>),
+                           dim3(g), dim3(BLOCK), 0, s, a);
         break;
     case INGOT_CHAIN_GENERIC_ULP:
-        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENERIC_ULP, MODE, DENSE, PIPE, NPRE, FIRST, LAZY>);
+        hipLaunchKernelGGL((k_parse_read<CS0, INGOT_CHAIN_GENERIC_ULP, MODE, DENSE, NPRE, FIRST, LAZY>),
+                           dim3(g), dim3(BLOCK), 0, s, a);
         break;
     case INGOT_CHAIN_VLAN_ULP:
-        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_VLAN_ULP, MODE, DENSE, PIPE, NPRE, FIRST, LAZY>);
+        hipLaunchKernelGGL((k_parse_read<CS0, INGOT_CHAIN_VLAN_ULP, MODE, DENSE, NPRE, FIRST, LAZY>),
+                           dim3(g), dim3(BLOCK), 0, s, a);
         break;
     default:
-        go(k_parse_read<CS0, CS1, CS2, CS3, INGOT_CHAIN_GENEVE_OVER_V6, MODE, DENSE, PIPE, NPRE, FIRST, LAZY>);
+        hipLaunchKernelGGL(
+            (k_parse_read<CS0, INGOT_CHAIN_GENEVE_OVER_V6, MODE, DENSE, NPRE, FIRST, LAZY>), dim3(g),
+            dim3(BLOCK), 0, s, a);
         break;
     }
     return hipGetLastError();
@@ -298,95 +247,44 @@ hipError_t launch_read(const ParseArgs& a, int chain, uint32_t grid, hipStream_t
 
 }  // namespace
 
-// parse_read over chunk lists: chunk 0 staged in a 4-chunk (64-B) window
-// (first mblk-style chunks are short header blocks), the rest from L2/HBM.
+// parse_read over chunk lists.  Measured (tools/abtune.py, us per launch,
+// DESIGN.md §1b): the reference's one-header-per-chunk shape (c2r, 1 M) 33.3
+// with descriptors and bytes on demand / 25.1 with chunk 0 in 4 pieces /
+// 24.2 with later chunks in planes {2,2,2,0}; header + payload chunks (c3r,
+// 16.7 M) 651 / 667 / 681 — extra planes cost occupancy on the
+// gather-bound shape.  Default (round 2): chunk 0 in a line-completing window
+// of 3 to 5 pieces (to the end of the 128-B line its third piece lies in;
+// k_parse's windows): c3r 676 -> 651 us, c2r 23.05 -> 23.24.
+// INGOT_TUNE_READ_PLAN 1 = the round-1 4-piece window (the default for chunk
+// pools in mapped host memory, where every staged piece is a PCIe read).
 hipError_t launch_segmented(const ParseArgs& a, int chain, int mode, const Tuning& t,
                             uint32_t g, hipStream_t s) {
     if (mode != OUT_FIELDS && mode != OUT_REC16) return hipErrorInvalidValue;
-    // dense chunk table (ingot_gpu_parse_read_dense): no length array,
-    // one (offset << 16) | length entry per chunk
-    if (!a.len) {
-        if (mode == OUT_REC16 && t.read_plan >= 12)
-            return launch_read<4, 0, 0, 0, OUT_REC16, true, true>(a, chain, g, s, t.cus);
-        return mode == OUT_FIELDS ? launch_read<4, 0, 0, 0, OUT_FIELDS, true>(a, chain, g, s)
-                                  : launch_read<4, 0, 0, 0, OUT_REC16, true>(a, chain, g, s);
-    }
-    // INGOT_TUNE_READ_PLAN: 16-B pieces staged per chunk of the first four.
-    // Measured (tools/abtune.py, us per launch): the
-    // reference's one-header-per-chunk shape (c2r, 1 M) 33.3 on demand
-    // (9) / 25.1 {4,0,0,0} / 24.2 {2,2,2,0} / 27.0 {4,2,2,0}; header +
-    // payload chunks (c3r, 16.7 M) 651 / 667 / 681 / 769 — extra planes
-    // cost occupancy on the gather-bound shape.  Default (round 2): chunk
-    // 0 in a line-completing window of 3 to 5 pieces (to the end of the
-    // 128-B line its third piece lies in; k_parse's windows, DESIGN.md
-    // §4): c3r 676 -> 651 us, c2r 23.05 -> 23.24; 3 to 8 pieces reads 15%
-    // fewer bytes but loses occupancy (724 us).  1 = the round-1 {4,0,0,0}.
-    // (9, the round-1 kernel without descriptor prefetch, is k_parse over
-    // SegFrame: launch_parse runs it.)
-    // chunk 0's descriptor per packet (ingot_gpu_parse_read_first): the
-    // default window (3-5 pieces, line-completing; fields: 4 pieces; host
-    // pools: 4) with chunk 0 loaded beside the bounds; the staging plans of
-    // INGOT_TUNE_READ_PLAN other than these do not apply
+    // dense chunk table (ingot_gpu_parse_read_dense): no length array, one
+    // (offset << 16) | length entry per chunk; 4 pieces of chunk 0 (the
+    // knob does not apply)
+    if (!a.len)
+        return mode == OUT_FIELDS ? launch_read<4, OUT_FIELDS, true>(a, chain, g, s)
+                                  : launch_read<4, OUT_REC16, true>(a, chain, g, s);
+    // chunk 0's descriptor per packet (ingot_gpu_parse_read_first): loaded
+    // beside the bounds; 17 = the bounds loaded lazily by the walk
     if (a.first) {
         if (mode == OUT_FIELDS)
-            return launch_read<4, 0, 0, 0, OUT_FIELDS, false, false, 3, true>(a, chain, g, s);
-        if (t.host_arena)
-            return launch_read<4, 0, 0, 0, OUT_REC16, false, false, 3, true>(a, chain, g, s);
+            return launch_read<4, OUT_FIELDS, false, 3, true>(a, chain, g, s);
+        if (t.host_arena || t.read_plan == 1)
+            return launch_read<4, OUT_REC16, false, 3, true>(a, chain, g, s);
         ParseArgs b = a;
         b.linewin = 3u;
-        if (t.read_plan == 17)  // chunk bounds loaded lazily by the walk
-            return launch_read<5, 0, 0, 0, OUT_REC16, false, false, 0, true, true>(b, chain, g, s);
-        return launch_read<5, 0, 0, 0, OUT_REC16, false, false, 3, true>(b, chain, g, s);
+        if (t.read_plan == 17)
+            return launch_read<5, OUT_REC16, false, 0, true, true>(b, chain, g, s);
+        return launch_read<5, OUT_REC16, false, 3, true>(b, chain, g, s);
     }
-    if (mode == OUT_FIELDS) return launch_read<4, 0, 0, 0, OUT_FIELDS>(a, chain, g, s);
-    // chunk pools in mapped host memory keep the round-1 window (every
-    // staged piece is a PCIe read there)
-    switch (t.read_plan ? t.read_plan : t.host_arena ? 1 : 11) {
-    case 2: return launch_read<2, 2, 2, 0, OUT_REC16>(a, chain, g, s);
-    case 3: return launch_read<4, 2, 2, 0, OUT_REC16>(a, chain, g, s);
-    case 4: return launch_read<4, 1, 1, 0, OUT_REC16>(a, chain, g, s);
-    case 5: return launch_read<3, 0, 0, 0, OUT_REC16>(a, chain, g, s);
-    case 6: return launch_read<2, 0, 0, 0, OUT_REC16>(a, chain, g, s);
-    case 7:  // line-completing chunk-0 windows of 2 / 4 to 8 pieces
-    case 8: {
-        ParseArgs b = a;
-        b.linewin = t.read_plan == 7 ? 2u : 4u;
-        return launch_read<8, 0, 0, 0, OUT_REC16>(b, chain, g, s);
-    }
-    case 10: {  // ... of 2 to 5 pieces (11, the default: 3 to 5)
-        ParseArgs b = a;
-        b.linewin = 2u;
-        return launch_read<5, 0, 0, 0, OUT_REC16>(b, chain, g, s);
-    }
-    case 1: return launch_read<4, 0, 0, 0, OUT_REC16>(a, chain, g, s);
-    // 12-14: the persistent kernel with the descriptor lookahead (PIPE)
-    case 12: {
-        ParseArgs b = a;
-        b.linewin = 3u;
-        return launch_read<5, 0, 0, 0, OUT_REC16, false, true>(b, chain, g, s, t.cus);
-    }
-    case 13: return launch_read<4, 0, 0, 0, OUT_REC16, false, true>(a, chain, g, s, t.cus);
-    case 14: {
-        ParseArgs b = a;
-        b.linewin = 2u;
-        return launch_read<5, 0, 0, 0, OUT_REC16, false, true>(b, chain, g, s, t.cus);
-    }
-    // 15 / 16: the default window with only chunk 1's / no later descriptor
-    // prefetched (NPRE 1 / 0: 63 / 59 VGPRs, 8 waves per SIMD)
-    case 15:
-    case 16: {
-        ParseArgs b = a;
-        b.linewin = 3u;
-        return t.read_plan == 15
-                   ? launch_read<5, 0, 0, 0, OUT_REC16, false, false, 1>(b, chain, g, s)
-                   : launch_read<5, 0, 0, 0, OUT_REC16, false, false, 0>(b, chain, g, s);
-    }
-    default: {  // 11
-        ParseArgs b = a;
-        b.linewin = 3u;
-        return launch_read<5, 0, 0, 0, OUT_REC16>(b, chain, g, s);
-    }
-    }
+    if (mode == OUT_FIELDS) return launch_read<4, OUT_FIELDS>(a, chain, g, s);
+    if (t.read_plan == 1 || (t.read_plan == 0 && t.host_arena))
+        return launch_read<4, OUT_REC16>(a, chain, g, s);
+    ParseArgs b = a;  // 0 / 11 / 17 (17 applies to parse_read_first only)
+    b.linewin = 3u;
+    return launch_read<5, OUT_REC16>(b, chain, g, s);
 }
 
 }  // namespace ingot_gpu

@@ -1,6 +1,6 @@
 // walk.h — the device side shared by the parse kernels (parse.hip,
 // read.hip, ring.hip): LDS-DMA staging and record stores, the lane's frame
-// views (Frame, SegFrame, SegFrameP), the chain walk `walk<CHAIN>()` that
+// views (Frame, SegFrameP), the chain walk `walk<CHAIN>()` that
 // restates ingot's generated parse_slice / parse_read (see parse.hip's
 // header for the reference map), the setters' and the flow hash's helpers,
 // and the grid helpers.  Internal; every definition is in an anonymous
@@ -104,20 +104,15 @@ __device__ __forceinline__ uint32_t slot_of(uint32_t p, uint32_t c) {
 }
 
 // One lane's view of its frame: LDS window for the first bytes, HBM beyond.
-// PROBE (the compacted slow path, INGOT_TUNE_SLOW_PATH = 1): a read past the
-// window loads nothing — it sets `miss` and yields 0, and the walk's loops
-// stop; the lane is walked again over a larger, re-staged window.
-template <uint32_t NCH, bool PROBE = false>
+template <uint32_t NCH>
 struct Frame {
     static constexpr bool kRead = false;
-    static constexpr bool kProbe = PROBE;
     const lds_u32* win;  // this wave's LDS image
     uint32_t p;          // packet index within the wave (== lane)
     uint32_t sh;         // frame start inside its first staged chunk (0..15)
     uint32_t avail;      // frame bytes [0, avail) are staged in LDS
     uint32_t len;        // frame length
     const uint8_t* g;    // frame start in HBM
-    mutable uint32_t miss = 0;  // PROBE: a read fell past the window
 
     __device__ __forceinline__ uint32_t dw(uint32_t b) const {
         return win[slot_of<NCH>(p, b >> 4) * 4u + ((b >> 2) & 3u)];
@@ -138,9 +133,6 @@ struct Frame {
             const uint32_t d1 = ((b & 3u) + n > 4u) ? dw(a1) : 0u;
             const uint32_t x = __builtin_amdgcn_alignbyte(d1, d0, b & 3u);  // bytes b.. little-endian
             v = __builtin_bswap32(x) >> (32u - 8u * n);
-        } else if constexpr (PROBE) {
-            miss = 1u;
-            v = 0u;
         } else {
             v = beyond(i, n);
         }
@@ -238,58 +230,30 @@ struct Frame {
     }
 };
 
-// parse_read's view of a multi-chunk packet (parse.rs:511-537): offsets are
-// logical (the chunks concatenated); `len` is the end of the current chunk, so
-// every bounds check in the walk is a chunk bound.  Chunk 0 is staged in LDS
-// like a single frame; later chunks are read from L2/HBM.
-template <uint32_t NCH>
-struct SegFrame : Frame<NCH> {
-    static constexpr bool kRead = true;
-    const uint8_t* arena;
-    const uint64_t* seg_off;
-    const uint16_t* seg_len;
-    uint32_t s0, k, nseg;  // first chunk's index, current chunk, chunk count
-
-    // Frame::be serves reads: bytes below `avail` (chunk 0's window) from LDS,
-    // the rest through g, which advance() rebases so that g[i] is logical
-    // byte i of the current chunk.
-    __device__ __forceinline__ bool more() const { return k + 1 < nseg; }
-    // next_chunk(): the next chunk starts at logical offset `len`.
-    __device__ __forceinline__ void advance() {
-        ++k;
-        const uint32_t l = seg_len[s0 + k];
-        this->g = arena + seg_off[s0 + k] - this->len;
-        const uint32_t e = this->len + l;
-        this->len = e > 65535u ? 65535u : e;  // record offsets are u16
-    }
-};
-
-// parse_read with the header chunks staged (k_parse_read): the descriptors
-// of the first four chunks, except a packet's last, are loaded up front; chunk 0 gets CS0 16-B slots per
-// packet (packet-major, like a frame's window: a packet's pieces sit side by
-// side, so the wave's requests for one frame coalesce) and each later chunk
-// e < 4 that is not the packet's last one gets CS_e pieces in planes (plane
-// π holds that piece of all 64 packets: one LDS-DMA instruction per piece
-// for the whole wave).  A packet's last chunk is taken to hold the payload
-// (an mblk chain's tail) and is read on demand like chunks past the fourth.
-// A chunk without planes of its own that lies inside chunk 0's window (chunks
-// cut from one buffer, like the reference bench's one chunk per header) is
-// staged with chunk 0's pieces and read from there.
-// Offsets are logical as in SegFrame; `len` is the current chunk's end.
+// parse_read's view of a multi-chunk packet (k_parse_read, parse.rs:511-537):
+// offsets are logical (the chunks concatenated) and `len` is the end of the
+// current chunk, so every bounds check in the walk is a chunk bound.  Chunk
+// 0 gets CS0 16-B slots per packet in LDS (packet-major, like a frame's
+// window: a packet's pieces sit side by side, so the wave's requests for one
+// frame coalesce).  A later chunk that lies inside chunk 0's staged window
+// (chunks cut from one buffer, like the reference bench's one chunk per
+// header) is read from there; other chunks are read from L2/HBM.  The
+// descriptors of chunks 1..NPRE, unless a packet's last, are loaded with
+// chunk 0's; the last chunk (an mblk chain's payload) and chunks past NPRE
+// are looked up when the walk reaches them.
 // LAZY (ingot_gpu_parse_read_first with INGOT_TUNE_READ_PLAN 17): the
 // packet's chunk bounds (pkt_seg[pi], pkt_seg[pi + 1]) are not loaded up
 // front — chunk 0 comes per packet — but on the first more() / advance(),
 // i.e. only by a walk that leaves chunk 0 or fails in it (NPRE = 0: no later
 // descriptor is prefetched, since they are found through the bounds).
-template <int CS0, int CS1, int CS2, int CS3, bool DENSE = false, int NPRE = 3, bool LAZY = false>
+template <int CS0, bool DENSE = false, int NPRE = 3, bool LAZY = false>
 struct SegFrameP {
     static_assert(!LAZY || NPRE == 0, "lazy bounds: no descriptor prefetch");
     static constexpr bool kRead = true;
-    static constexpr bool kProbe = false;
-    const lds_u32* win;  // this wave's image: 64 x CS0 slots, then the planes
+    const lds_u32* win;  // this wave's image: 64 x CS0 slots
     uint32_t p;          // lane
     uint32_t L, len;     // current chunk: logical [L, len)
-    uint32_t plane, sh, avail;  // its first plane (chunks >= 1), start in it, staged bytes
+    uint32_t sh, avail;  // its start in chunk 0's window, its bytes staged there
     const uint8_t* g;    // g[i] = logical byte i of the current chunk
     const uint8_t* arena;
     const uint64_t* seg_off;
@@ -311,20 +275,10 @@ struct SegFrameP {
     uint32_t l0, l1, l2, l3;
     int64_t b0;      // chunk 0's window: arena bytes [b0, b0 + span0) staged
     uint32_t span0;
-    static constexpr uint32_t kW0 = 0xffffffffu;  // `plane` of a chunk read from that window
 
-    static constexpr uint32_t cs(uint32_t e) {
-        return e == 0 ? CS0 : e == 1 ? CS1 : e == 2 ? CS2 : e == 3 ? CS3 : 0;
-    }
-    static constexpr uint32_t pb(uint32_t e) {  // first plane of chunk e >= 1
-        return e == 1 ? 0 : e == 2 ? CS1 : CS1 + CS2;
-    }
-    // staged chunk-relative byte b of the current chunk: a dword of the image
+    // staged byte b (window coordinates): a dword of the image
     __device__ __forceinline__ uint32_t dw(uint32_t b) const {
-        const uint32_t c = b >> 4;
-        const uint32_t slot =
-            k == 0 || plane == kW0 ? slot_of<CS0>(p, c) : WAVE * (CS0 + plane + c) + p;
-        return win[slot * 4u + ((b >> 2) & 3u)];
+        return win[slot_of<CS0>(p, b >> 4) * 4u + ((b >> 2) & 3u)];
     }
     __device__ __forceinline__ uint32_t be(uint32_t i, uint32_t n) const {
         const uint32_t x0 = i - L;
@@ -333,10 +287,9 @@ struct SegFrameP {
             const uint32_t a = b & ~3u;
             const uint32_t d0 = dw(a);
             // the second dword only when the bytes straddle it (then it lies
-            // in the current chunk's staged pieces); clamped to them so that
-            // a speculated read stays inside this packet's slots / planes
-            const uint32_t lim = k == 0 || plane == kW0 ? 16u * CS0 : 16u * cs(k);
-            const uint32_t a1 = a + 4u < lim ? a + 4u : a;
+            // in the staged pieces); clamped to them so that a speculated
+            // read stays inside this packet's slots
+            const uint32_t a1 = a + 4u < 16u * CS0 ? a + 4u : a;
             const uint32_t d1 = ((b & 3u) + n > 4u) ? dw(a1) : 0u;
             return __builtin_bswap32(__builtin_amdgcn_alignbyte(d1, d0, b & 3u)) >> (32u - 8u * n);
         }
@@ -351,21 +304,18 @@ struct SegFrameP {
         bounds();
         return k + 1 < nseg;
     }
-    // chunk e's staged pieces: chunk 0 always; later ones unless last
-    __device__ __forceinline__ static uint32_t staged(uint32_t e, uint32_t nseg) {
-        return e == 0 ? CS0 : (e + 1 < nseg ? cs(e) : 0u);
-    }
-    __device__ __forceinline__ void enter(uint64_t o, uint32_t l, uint32_t pl, uint32_t c) {
+    // Step into a chunk at arena offset o, length l; c = chunk 0's staged
+    // pieces (k == 0), else 0: the chunk's bytes are staged only if it lies
+    // in chunk 0's window.
+    __device__ __forceinline__ void enter(uint64_t o, uint32_t l, uint32_t c) {
         g = arena + o - L;
         const uint32_t e = L + l;
         len = e > 65535u ? 65535u : e;  // record offsets are u16
-        plane = pl;
         sh = (uint32_t)((uintptr_t)(arena + o) & 15u);
         avail = c ? (l < 16u * c - sh ? l : 16u * c - sh) : 0u;
-        if (k != 0 && c == 0) {
+        if (k != 0) {
             const int64_t d = (int64_t)o - b0;
             if (d >= 0 && d < (int64_t)span0) {
-                plane = kW0;
                 sh = (uint32_t)d;
                 avail = l < span0 - sh ? l : span0 - sh;
             }
@@ -375,17 +325,14 @@ struct SegFrameP {
         bounds();
         ++k;
         L = len;
-        // chunks 1..NPRE that are not the packet's last had their
-        // descriptors loaded with chunk 0's; the last chunk (the payload) and
-        // the others are looked up when the walk reaches them
-        if (NPRE >= 1 && k + 1 < nseg && k == 1) enter(o1, l1, pb(1), staged(1, nseg));
-        else if (NPRE >= 2 && k + 1 < nseg && k == 2) enter(o2, l2, pb(2), staged(2, nseg));
-        else if (NPRE >= 3 && k + 1 < nseg && k == 3) enter(o3, l3, pb(3), staged(3, nseg));
+        if (NPRE >= 1 && k + 1 < nseg && k == 1) enter(o1, l1, 0u);
+        else if (NPRE >= 2 && k + 1 < nseg && k == 2) enter(o2, l2, 0u);
+        else if (NPRE >= 3 && k + 1 < nseg && k == 3) enter(o3, l3, 0u);
         else if constexpr (DENSE) {
             const uint64_t v = seg_off[s0 + k];  // (offset << 16) | length
-            enter(v >> 16, (uint32_t)(v & 0xffffu), 0u, 0u);
+            enter(v >> 16, (uint32_t)(v & 0xffffu), 0u);
         } else {
-            enter(seg_off[s0 + k], seg_len[s0 + k], 0u, 0u);
+            enter(seg_off[s0 + k], seg_len[s0 + k], 0u);
         }
     }
 };
@@ -449,9 +396,6 @@ template <bool FIELDS, class FR>
 __device__ __forceinline__ bool v6_ext_chain(const FR& f, uint32_t len, uint32_t& q, uint32_t& h,
                                              uint32_t& n_eh, ingot_v6eh* eh) {
     while (q < len) {
-        if constexpr (FR::kProbe) {
-            if (f.miss) break;  // walked again over a larger window
-        }
         const uint32_t c = eh_class(h);
         if (c == EH_NONE) break;  // Err(Unwanted) => break
         uint32_t used, nh, x = 0;
@@ -651,9 +595,6 @@ __device__ __forceinline__ void walk(FR& f, Rec& r, ingot_fields* F, ingot_tunne
         uint32_t read = 0, n_opt = 0, crit = 0;
         bool opt_bad = false;
         while (read < span) {
-            if constexpr (FR::kProbe) {
-                if (f.miss) break;
-            }
             const uint32_t o = p + geneve::LEN + read, rem = span - read;
             if (rem < geneve_opt::LEN) { opt_bad = true; break; }
             const uint32_t ow = f.be(o, 4);
@@ -1055,7 +996,7 @@ struct FlowWords {
 // holding it from L2 — instead of a bounds check, two reads and a wait (or 4
 // byte loads) per word.  The port word: LDS, or aligned dwords past the
 // window (IPv6 EH chains).
-// lanes (INGOT_TUNE_FLOW_KERNEL 3): the path is chosen per lane — a lane
+// lanes (k_flows_bits): the path is chosen per lane — a lane
 // whose block lies past its window reads it from L2 while the others read
 // LDS (a split wave runs both paths, each under its lanes' mask) — so that a
 // window ending before some lanes' IPv6 addresses does not send every lane
@@ -1185,226 +1126,6 @@ __device__ __forceinline__ bool flow_hash(const FR& f, const Rec& r, const uint3
     if constexpr (H16) h = ok ? toeplitz9_16(x, tab) : 0u;
     else h = ok ? toeplitz9(x, tab) : 0u;
     return ok;
-}
-
-// Index of the j-th set bit of m (j < popcount(m)): binary search on
-// popcounts, 6 steps.
-__device__ __forceinline__ uint32_t nth_set_bit(uint64_t m, uint32_t j) {
-    uint32_t pos = 0;
-#pragma unroll
-    for (uint32_t w = 32; w; w >>= 1) {
-        const uint64_t lo = (1ull << w) - 1ull;
-        const uint32_t c = (uint32_t)__popcll(m & lo);
-        if (j >= c) {
-            j -= c;
-            m >>= w;
-            pos += w;
-        } else {
-            m &= lo;
-        }
-    }
-    return pos;
-}
-
-// The compacted slow path (INGOT_TUNE_SLOW_PATH = 1; A/B against per-lane
-// byte loads).  After a PROBE walk over the NCH-chunk window,
-// the lanes whose chain ran past it are balloted and ranked (prefix count of
-// the ballot); in batches of B = 64 NCH / NCH2 lanes the wave re-stages the
-// first NCH2 = 2 NCH chunks of just those frames into its LDS image,
-// compacted (rank-major, lane-linear per LDS-DMA instruction: every
-// instruction fills 64 slots of the batch), and walks those lanes again over
-// the larger window; bytes past it are read per lane from L2/HBM.  This is
-// the GPU form of the reference's unbounded EH loop (util.rs:206-216) and
-// long IPv4/TCP options (ip.rs:91, tcp.rs:28).
-template <uint32_t NCH, int CHAIN>
-__device__ __forceinline__ void slow_rewalk(const Frame<NCH, true>& fr, Rec& r, bool valid,
-                                            uint32_t* wimg, uint32_t lane, const uint8_t* arena,
-                                            int64_t base, uint32_t sh, uint32_t len) {
-    constexpr uint32_t NCH2 = 2u * NCH;
-    constexpr uint32_t B = WAVE * NCH / NCH2;
-    const bool miss = valid && fr.miss;
-    const uint64_t m = __ballot(miss);
-    if (!m) return;
-    const uint32_t K = (uint32_t)__popcll(m);
-    const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-    const uint32_t take2 = len < 16u * NCH2 - sh ? len : 16u * NCH2 - sh;
-    const uint32_t nch2 = (sh + take2 + 15u) >> 4;
-    for (uint32_t b0 = 0; b0 < K; b0 += B) {
-        // every lane's reads of the image have returned (their values were
-        // consumed by the walk) before LDS-DMA overwrites it
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (uint32_t k = 0; k < NCH; ++k) {
-            const uint32_t q = k * WAVE + lane;
-            const uint32_t cp = q / NCH2, c = q - cp * NCH2;
-            const uint32_t j = b0 + cp;
-            const uint32_t src = nth_set_bit(m, j < K ? j : K - 1u);
-            const uint32_t np = (uint32_t)__shfl((int)nch2, (int)src);
-            const int64_t bp = (int64_t)__shfl((long long)base, (int)src);
-            if (j < K && c < np) stage16(arena + bp + 16u * c, wimg + k * WAVE * 4u, false);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (miss && rank >= b0 && rank < b0 + B) {
-            Frame<NCH2> f2{(const lds_u32*)wimg, rank - b0, sh, take2, len, fr.g};
-            walk<CHAIN, false>(f2, r, nullptr, nullptr);
-        }
-    }
-}
-
-// A lane's frame over its window plus up to EXT_MAX extension chunks staged
-// in other slots of the wave's image (ext_walk): staged chunk c < nch is the
-// lane's own slot_of(p, c), chunk nch + e is image slot q[e].  Bytes past
-// `avail` are read from L2/HBM as in Frame.
-constexpr uint32_t EXT_MAX = 4;
-template <uint32_t NCH>
-struct FrameExt {
-    static constexpr bool kRead = false;
-    static constexpr bool kProbe = false;
-    const lds_u32* win;
-    uint32_t p, sh, avail, len;  // as Frame; avail covers the extension too
-    const uint8_t* g;
-    uint32_t nch, q0, q1, q2, q3;  // window chunks; the extension's image slots
-
-    __device__ __forceinline__ uint32_t dw(uint32_t b) const {
-        const uint32_t c = b >> 4;
-        const uint32_t e = c - nch;
-        const uint32_t slot = c < nch ? slot_of<NCH>(p, c)
-                              : e == 0u ? q0 : e == 1u ? q1 : e == 2u ? q2 : q3;
-        return win[slot * 4u + ((b >> 2) & 3u)];
-    }
-    __device__ __forceinline__ uint32_t be(uint32_t i, uint32_t n) const {
-        if (i + n <= avail) {
-            const uint32_t b = sh + i;
-            const uint32_t a = b & ~3u;
-            const uint32_t d0 = dw(a);
-            const uint32_t d1 = ((b & 3u) + n > 4u) ? dw(a + 4u) : 0u;
-            return __builtin_bswap32(__builtin_amdgcn_alignbyte(d1, d0, b & 3u)) >> (32u - 8u * n);
-        }
-        uint32_t v = 0;
-        for (uint32_t k = 0; k < n; ++k) v = (v << 8) | g[i + k];
-        return v;
-    }
-    __device__ __forceinline__ uint32_t get(uint32_t hdr, Field f) const {
-        return (be(hdr + f.byte0(), f.nbytes()) >> f.rshift()) & f.mask();
-    }
-};
-
-// The resume-style slow path (INGOT_TUNE_SLOW_PATH = 2).
-// Pass 1 walks every lane over its window, probing.  The lanes whose chain
-// ran past it (ballot) need the chunks right after their window: up to
-// EXT_MAX, not past the frame.  Those chunks only are fetched (the window is
-// not re-staged) into image slots nobody needs any more — every slot of a
-// lane whose walk finished, and a missing lane's own slots past its window:
-// row k of the image is ballot-scanned for free slots (running count of the
-// earlier rows + popcount of the row's ballot below the lane = the slot's
-// rank among free slots), and free slot F receives extension chunk F of the
-// wave (owner lane: binary search over the inclusive prefix scan of the
-// lanes' chunk counts).  One LDS-DMA instruction per image row.  Pass 2
-// re-walks the missing lanes from LDS (window + extension), bytes past both
-// from L2/HBM.
-template <uint32_t NCH, int CHAIN>
-__device__ __forceinline__ void ext_walk(bool valid, uint32_t* wimg, uint32_t lane,
-                                         const uint8_t* arena, int64_t base, uint32_t nch,
-                                         uint32_t sh, uint32_t take, uint32_t len,
-                                         const uint8_t* g, uint4* out, uint32_t pol) {
-    bool miss;
-    {   // pass 1: probe the window; a lane done walking stores its record
-        // now, so no record stays live across the fetch and pass 2
-        Frame<NCH, true> f{(const lds_u32*)wimg, lane, sh, take, len, g};
-        Rec r;
-        walk<CHAIN, false>(f, r, nullptr, nullptr);
-        miss = valid && f.miss;
-        if (valid && !miss) store_rec(out, pack(r), pol);
-    }
-    const uint64_t M = __ballot(miss);
-    if (!M) return;
-    uint32_t m = 0;
-    if (miss) {
-        const uint32_t last = (sh + len - 1u) >> 4;  // staged chunk of the frame's last byte
-        const uint32_t rest = last + 1u > nch ? last + 1u - nch : 0u;
-        m = rest < EXT_MAX ? rest : EXT_MAX;
-    }
-    uint32_t x = m;  // inclusive prefix scan of the counts
-#pragma unroll
-    for (uint32_t d = 1; d < WAVE; d <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, d);
-        if (lane >= d) x += y;
-    }
-    const uint32_t S = x - m;
-    const uint32_t TOT = (uint32_t)__shfl((int)x, (int)(WAVE - 1u));
-    // every lane's reads of the image have returned before LDS-DMA reuses it
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    const uint64_t lt = (1ull << lane) - 1ull;
-    uint64_t rowB[NCH];     // free-slot ballot of each image row (wave-uniform)
-    uint32_t cum[NCH + 1];  // free slots in the rows before k (wave-uniform)
-    cum[0] = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < NCH; ++k) {
-        const uint32_t q = k * WAVE + lane;
-        const uint32_t pp = q / NCH;
-        const uint32_t c = (q - pp * NCH) ^ swz<NCH>(pp);
-        const uint32_t np = (uint32_t)__shfl((int)nch, (int)pp);
-        const bool free = !((M >> pp) & 1ull) || c >= np;
-        const uint64_t B = __ballot(free);
-        rowB[k] = B;
-        const uint32_t F = cum[k] + (uint32_t)__popcll(B & lt);
-        cum[k + 1] = cum[k] + (uint32_t)__popcll(B);
-        if (cum[k] < TOT) {  // wave-uniform
-            uint32_t j = 0;  // owner: the first lane whose inclusive count exceeds F
-#pragma unroll
-            for (uint32_t s2 = WAVE / 2; s2; s2 >>= 1) {
-                const uint32_t v = (uint32_t)__shfl((int)x, (int)(j + s2 - 1u));
-                if (v <= F) j += s2;
-            }
-            j = j < WAVE ? j : WAVE - 1u;
-            const uint32_t sj = (uint32_t)__shfl((int)S, (int)j);
-            const uint32_t nj = (uint32_t)__shfl((int)nch, (int)j);
-            const int64_t bj = (int64_t)__shfl((long long)base, (int)j);
-            if (free && F < TOT)
-                stage16(arena + bj + 16u * (nj + F - sj), wimg + k * WAVE * 4u, false);
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!miss) return;
-    // chunks placed for this lane (all of them unless the free slots ran out)
-    const uint32_t placed = S + m <= cum[NCH] ? m : (cum[NCH] > S ? cum[NCH] - S : 0u);
-    // image slot of free slot S + e: its row (by cum) and its set bit in the
-    // row's ballot (fully unrolled, constant indices: the arrays stay in
-    // registers)
-    uint32_t qv[EXT_MAX];
-#pragma unroll
-    for (uint32_t e = 0; e < EXT_MAX; ++e) {
-        const uint32_t t = S + e;
-        uint32_t k = 0, c0 = 0;
-        uint64_t B = rowB[0];
-#pragma unroll
-        for (uint32_t kk = 1; kk < NCH; ++kk) {
-            const bool in = t >= cum[kk];
-            k = in ? kk : k;
-            B = in ? rowB[kk] : B;
-            c0 = in ? cum[kk] : c0;
-        }
-        qv[e] = e < placed ? k * WAVE + nth_set_bit(B, t - c0) : 0u;
-    }
-    FrameExt<NCH> f;
-    f.win = (const lds_u32*)wimg;
-    f.p = lane;
-    f.sh = sh;
-    f.len = len;
-    f.g = g;
-    f.nch = nch;
-    f.q0 = qv[0];
-    f.q1 = qv[1];
-    f.q2 = qv[2];
-    f.q3 = qv[3];
-    const uint32_t end = 16u * (nch + placed) - sh;  // staged byte sh + i = frame byte i
-    f.avail = end < len ? end : len;
-    // pass 2: the missing lanes, from the window and the extension
-    Rec r;
-    walk<CHAIN, false>(f, r, nullptr, nullptr);
-    store_rec(out, pack(r), pol);
 }
 
 // Blocks of `kernel` one CU holds at once (its LDS / VGPR footprint), queried

@@ -9,7 +9,8 @@ import pytest
 
 import ingot_amd
 from ingot_amd import Chain, GenProfile, _lib
-from ingot_amd.abi import TUNE_PIPE_DEPTH, TUNE_WINDOW_INDEXED, TUNE_WINDOW_STRIDED
+from ingot_amd.abi import (TUNE_FLOW_KERNEL, TUNE_PIPE_DEPTH, TUNE_READ_PLAN, TUNE_SLOW_PATH,
+                           TUNE_WINDOW_INDEXED, TUNE_WINDOW_STRIDED)
 
 pytestmark = pytest.mark.gpu
 
@@ -91,8 +92,12 @@ def test_modify_and_flow_argument_errors(env):
 def test_tuning_errors_and_defaults(env):
     torch, ctx, lib, *_ = env
     c = ingot_amd.Context(0)
-    for key, val in ((TUNE_WINDOW_INDEXED, 7), (TUNE_WINDOW_STRIDED, 6), (TUNE_PIPE_DEPTH, 1),
-                     (99, 0)):
+    # the variants that lost were removed: their values are EINVAL
+    pruned = [(TUNE_SLOW_PATH, v) for v in (1, 2)] + \
+        [(TUNE_READ_PLAN, v) for v in (2, 3, 4, 5, 6, 7, 8, 9, 10, 12, 13, 14, 15, 16, 18)] + \
+        [(TUNE_FLOW_KERNEL, v) for v in range(1, 15)] + [(TUNE_FLOW_KERNEL, 16)]
+    for key, val in [(TUNE_WINDOW_INDEXED, 7), (TUNE_WINDOW_STRIDED, 6), (TUNE_PIPE_DEPTH, 1),
+                     (99, 0)] + pruned:
         assert lib.ingot_gpu_ctx_set_tuning(c._h, key, val) == EINVAL, (key, val)
     assert c.get_tuning(TUNE_WINDOW_INDEXED) == 0  # untouched by the rejected calls
     c.set_tuning(TUNE_WINDOW_INDEXED, 5)

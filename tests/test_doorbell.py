@@ -120,10 +120,10 @@ def test_held_queue_blocks_its_streams(env):
     assert all(e.query() for e in evs)
     db.close()
     # How HIP maps streams onto hardware queues is the runtime's, not the
-    # library's: only checked when the queue count is known and below the
-    # stream count
-    hwq = os.environ.get("GPU_MAX_HW_QUEUES")
-    if hwq is None or not hwq.isdigit() or int(hwq) >= len(streams):
+    # library's: checked whenever the queue count (GPU_MAX_HW_QUEUES, HIP's
+    # default 4 when unset) is below the stream count
+    hwq = os.environ.get("GPU_MAX_HW_QUEUES", "4")
+    if not hwq.isdigit() or int(hwq) >= len(streams):
         return
     assert any(ran), "no stream ran beside the held one"
     assert not all(ran), ("every stream ran beside the held queue: more hardware queues than "

@@ -153,12 +153,10 @@ def test_flow_hist_bit_exact(profile, chain, stride):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("tune", [{}, {"win": 3}, {"win": 4}, {"win": 5}, {"win": 8},
-                                  {"blocks": 7}, {"blocks": 1, "win": 3}, {"fk": 1},
-                                  {"fk": 1, "blocks": 3}, {"fk": 2}, {"fk": 2, "win": 4},
-                                  {"fk": 2, "blocks": 3}, {"win": 25}, {"win": 26}, {"win": 28},
-                                  {"fk": 2, "win": 25}, {"win": 25, "blocks": 3}, {"win": 1045},
-                                  {"win": 1058}, {"fk": 3}, {"fk": 3, "win": 1025},
-                                  {"fk": 3, "win": 1035}, {"fk": 3, "win": 3}])
+                                  {"blocks": 7}, {"blocks": 1, "win": 3}, {"blocks": 3},
+                                  {"win": 25}, {"win": 26}, {"win": 28},
+                                  {"win": 25, "blocks": 3}, {"win": 1045}, {"win": 1056},
+                                  {"win": 1058}, {"win": 1025}, {"win": 1035}, {"fk": 15}])
 @pytest.mark.parametrize("profile,chain,stride", [
     ("FLOWS", "VlanUlp", None), ("ADVERSARIAL", "GenericUlp", None),
     ("GENEVE_ADVERSARIAL", "GeneveOverV6Tunnel", None), ("VLAN_V6EH", "VlanUlp", 256),
@@ -203,11 +201,8 @@ def test_flow_kernels_every_setting(tune, profile, chain, stride):
 @pytest.mark.gpu
 @pytest.mark.parametrize("table", [0, 32])
 @pytest.mark.parametrize("tune", [{}, {"win": 3}, {"win": 4}, {"win": 8}, {"blocks": 5},
-                                  {"fk": 1}, {"fk": 2}, {"win": 25}, {"fk": 3, "win": 1025},
-                                  {"fk": 4}, {"fk": 5}, {"fk": 6}, {"fk": 7}, {"fk": 8}, {"fk": 9},
-                                  {"fk": 10}, {"fk": 11}, {"fk": 12}, {"fk": 13}, {"fk": 14}, {"fk": 15},
-                                  {"fk": 10, "blocks": 3}, {"fk": 14, "blocks": 5},
-                                  {"fk": 4, "blocks": 3}, {"fk": 6, "blocks": 5}])
+                                  {"blocks": 3}, {"win": 25}, {"win": 1025}, {"win": 1056},
+                                  {"fk": 15}])
 @pytest.mark.parametrize("bins", [1 << 16, 1024])
 @pytest.mark.parametrize("profile,chain,stride", [
     ("FLOWS", "VlanUlp", None), ("ADVERSARIAL", "GenericUlp", None),
@@ -310,23 +305,24 @@ def test_flow_hist_many_slices():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fk", [0, 13, 15])
+@pytest.mark.parametrize("win", [0, 1056])
 @pytest.mark.parametrize("bins", [1, 2, 4096, 1 << 16])
-def test_flow_bins_extreme_bin_counts(fk, bins):
-    """The table-free default kernel at the bin-mask extremes (one bin, two
-    bins, the 16-bit maximum): flow ids and histogram equal the oracle's."""
+def test_flow_bins_extreme_bin_counts(win, bins):
+    """The table-free default kernel (win 0) and k_parse's flows mode (an
+    explicit window) at the bin-mask extremes (one bin, two bins, the 16-bit
+    maximum): flow ids and histogram equal the oracle's."""
     import torch
 
     import ingot_amd
     from ingot_amd import GenProfile
-    from ingot_amd.abi import TUNE_FLOW_KERNEL
+    from ingot_amd.abi import TUNE_WINDOW_INDEXED
 
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     n = 4097
     ctx = ingot_amd.Context(0)
-    ctx.set_tuning(TUNE_FLOW_KERNEL, fk)
-    arena, off, lens = ingot_amd.gen_frames(GenProfile.FLOWS, n, seed=bins + fk)
+    ctx.set_tuning(TUNE_WINDOW_INDEXED, win)
+    arena, off, lens = ingot_amd.gen_frames(GenProfile.FLOWS, n, seed=bins + win)
     hist = torch.zeros(bins, dtype=torch.int32, device="cuda")
     flow = ctx.flow_hist(arena, off, lens, Chain.VlanUlp, hist=hist, bins=bins, n=n,
                          workspace=ctx.flow_hist_workspace(n, bins))
@@ -338,21 +334,24 @@ def test_flow_bins_extreme_bin_counts(fk, bins):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fk", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
+@pytest.mark.parametrize("tune", [{}, {"win": 1056}, {"table": 32}, {"blocks": 3}])
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 4097, 262_145])
-def test_flow_ids_ragged_batches(n, fk):
-    """Ragged batch sizes on every flows grid (one tile per wave, the
-    hash-overlapped and the persistent kernel): flow ids equal the oracle's."""
+def test_flow_ids_ragged_batches(n, tune):
+    """Ragged batch sizes on every flows grid (k_flows_bits one tile per
+    wave, k_parse's flows mode with the 16-bit table, the 32-bit table's
+    persistent grid, a grid cap): flow ids equal the oracle's."""
     import torch
 
     import ingot_amd
     from ingot_amd import GenProfile
-    from ingot_amd.abi import TUNE_FLOW_KERNEL
+    from ingot_amd.abi import TUNE_FLOW_TABLE, TUNE_MAX_BLOCKS, TUNE_WINDOW_INDEXED
 
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     ctx = ingot_amd.Context(0)
-    ctx.set_tuning(TUNE_FLOW_KERNEL, fk)
+    ctx.set_tuning(TUNE_WINDOW_INDEXED, tune.get("win", 0))
+    ctx.set_tuning(TUNE_FLOW_TABLE, tune.get("table", 0))
+    ctx.set_tuning(TUNE_MAX_BLOCKS, tune.get("blocks", 0))
     arena, off, lens = ingot_amd.gen_frames(GenProfile.FLOWS, n, seed=n + 7)
     flow = ctx.flow_hist(arena, off, lens, Chain.VlanUlp, n=n)
     torch.cuda.synchronize()

@@ -251,36 +251,6 @@ def test_every_window_setting_is_bit_exact(torch):
             assert fs.cpu().numpy().tobytes() == want_s[chain][1].tobytes(), (w, chain)
 
 
-@pytest.mark.parametrize("slow", [1, 2])
-@pytest.mark.parametrize("profile,chains,seed", [
-    ("ADVERSARIAL", list(Chain), 41), ("VLAN_V6EH", [Chain.VlanUlp, Chain.GenericUlp], 42),
-    ("MIXED", [Chain.GenericUlp, Chain.UdpParser], 43),
-    ("GENEVE_ADVERSARIAL", [Chain.GeneveOverV6Tunnel], 44),
-    ("GENEVE", [Chain.GeneveOverV6Tunnel], 45),
-])
-def test_compacted_slow_path_is_bit_exact(torch, profile, chains, seed, slow):
-    """INGOT_TUNE_SLOW_PATH = 1: lanes whose chain outruns the window are
-    balloted, re-staged compacted into a window twice as large and walked
-    again; = 2 (resume-style): only the chunks past their window are fetched,
-    into the image slots no lane needs any more (ballot-scanned), and those
-    lanes re-walk from LDS.  The records equal the oracle's, ragged batch end
-    included."""
-    from ingot_amd.abi import TUNE_SLOW_PATH
-
-    n = 70_001
-    arena, off, lens = ingot_amd.gen_frames(GenProfile[profile], n, seed=seed)
-    c = ingot_amd.Context(0)
-    c.set_tuning(TUNE_SLOW_PATH, slow)
-    a_np, o_np, l_np = arena.cpu().numpy(), off.cpu().numpy(), lens.cpu().numpy()
-    for chain in chains:
-        r = c.parse(arena, off, lens, chain)
-        torch.cuda.synchronize()
-        want = oracle.parse_batch(a_np, o_np, l_np, chain, nthreads=8)
-        g = r.cpu().numpy().reshape(n, 16)
-        bad = np.nonzero((g != want.view(np.uint8).reshape(n, 16)).any(axis=1))[0]
-        assert bad.size == 0, (chain, bad[:5])
-
-
 @pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 1000])
 def test_small_and_ragged_batches(ctx, torch, n):
     arena, off, lens = ingot_amd.gen_frames(GenProfile.ADVERSARIAL, max(n, 1), seed=n + 1)

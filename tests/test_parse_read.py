@@ -163,10 +163,10 @@ def split_many(frames, seed):
     return out
 
 
-@pytest.mark.parametrize("plan", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16])
+@pytest.mark.parametrize("plan", [0, 1, 11, 17])
 def test_every_read_plan_is_bit_exact(torch, plan):
-    """INGOT_TUNE_READ_PLAN: how many 16-B pieces of each of the first four
-    chunks are staged in LDS never changes a record, a field block or the
+    """INGOT_TUNE_READ_PLAN: how chunk 0 is staged in LDS (line-completing
+    3-5 pieces, or 4) never changes a record, a field block or the
     remainder's chunk index (1-8 chunks per packet, every chain)."""
     from ingot_amd.abi import TUNE_READ_PLAN
 
@@ -231,11 +231,12 @@ def test_dense_chunk_table_matches(ctx, torch, chain):
     assert np.array_equal(c2.cpu().numpy().view(np.uint16), chunk)
     w_rec, _, w_chunk = oracle.parse_read_batch(*segs, chain)
     assert recs.tobytes() == w_rec.tobytes() and np.array_equal(chunk, w_chunk)
-    # the persistent lookahead kernel over the dense table (READ_PLAN >= 12)
+    # the dense call ignores INGOT_TUNE_READ_PLAN (17 once
+    # switched it to another kernel)
     from ingot_amd.abi import TUNE_READ_PLAN
 
     c = ingot_amd.Context(0)
-    c.set_tuning(TUNE_READ_PLAN, 12)
+    c.set_tuning(TUNE_READ_PLAN, 17)
     r3, c3 = c.parse_read_dense(*d, chain)
     torch.cuda.synchronize()
     assert r3.cpu().numpy().tobytes() == recs.tobytes()
@@ -275,12 +276,12 @@ def scatter(packets, seed):
             np.array(pkt, dtype=np.uint32))
 
 
-@pytest.mark.parametrize("plan", [0, 1, 2, 5, 6, 7, 8, 9, 12, 13, 15, 16])
+@pytest.mark.parametrize("plan", [0, 1])
 def test_scattered_and_aliased_chunks(torch, plan):
     """Chunks out of memory order, with gaps, partly inside chunk 0's staged
-    window and partly outside, and repeated chunks: the staged reads of later
-    chunks come from wherever their bytes are (INGOT_TUNE_READ_PLAN 0 / 2 /
-    9), records and chunk indices equal the oracle's."""
+    window and partly outside, and repeated chunks: the reads of later
+    chunks come from wherever their bytes are (chunk 0's window or L2/HBM),
+    records and chunk indices equal the oracle's."""
     from ingot_amd.abi import TUNE_READ_PLAN
 
     c = ingot_amd.Context(0)

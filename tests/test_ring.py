@@ -199,4 +199,30 @@ def test_ring_doorbell_argument_checks(torch):
                        db_first=0xFFFFFFFF, timeout_ms=100)
     torch.cuda.synchronize()
     assert all(bool((o == 0xAB).all()) for o in outs)
+    # the exact boundary: the last batch's value db_first + 1 == 0x1_0000_0000
+    # wraps (ERANGE); db_first + 1 == 0xFFFFFFFF does not
+    with pytest.raises(RuntimeError, match=r"\(-?\d+\)"):
+        ctx.parse_ring(arenas, 64, n, Chain.UdpParser, outs, doorbell=db,
+                       db_first=0xFFFFFFFF, timeout_ms=100)
+    db.ring(0xFFFFFFFF)  # publishes both batches from db_first 0xFFFFFFFE
+    torch.cuda.synchronize()
+    ctx.parse_ring(arenas, 64, n, Chain.UdpParser, outs, doorbell=db, db_first=0xFFFFFFFE,
+                   timeout_ms=2000)
+    torch.cuda.synchronize()
+    for a, o in zip(arenas, outs):
+        assert o.cpu().numpy().tobytes() == _want(a, Chain.UdpParser, 64, n).tobytes()
+    db.close()
+
+
+def test_ring_doorbell_other_device_is_einval(torch):
+    """A doorbell of another device's context is EINVAL (needs two GPUs)."""
+    if torch.cuda.device_count() < 2:
+        pytest.skip("one GPU: the cross-device EINVAL path needs a second context device")
+    ctx0, ctx1 = ingot_amd.Context(0), ingot_amd.Context(1)
+    n = 4096
+    arenas = _batches(torch, GenProfile.V4UDP64, n, 64, 1, seed=6)
+    outs = [torch.zeros((n, 16), dtype=torch.uint8, device="cuda")]
+    db = ingot_amd.Doorbell(ctx1)
+    with pytest.raises(RuntimeError, match="EINVAL|invalid"):
+        ctx0.parse_ring(arenas, 64, n, Chain.UdpParser, outs, doorbell=db, timeout_ms=100)
     db.close()

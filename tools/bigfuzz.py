@@ -4,9 +4,9 @@ the sizes the pytest suite uses.  For every chain: records and every getter
 over N adversarial frames (every truncation / ihl / data_offset / EH / Geneve
 defect path), in the packed layout and in 256-B slots; flow ids and hashes
 for the VLAN chain.  Prints one JSON line with the mismatch counts (all must
-be 0) and writes it to gpurun_out/bigfuzz.json.  Round 2 adds the compacted
-slow path, parse_read over random 4-chunk splits with every staging plan, and
-flow bins from the 16-bit table.
+be 0) and writes it to gpurun_out/bigfuzz.json.  Also parse_read over random
+4-chunk splits (every staging plan kept, parse_read_first, lazy bounds),
+flow bins from k_flows_bits and from k_parse's flows mode, and the slot ring.
 
     python tools/bigfuzz.py [--frames 4000000] [--seed 1234]
 """
@@ -73,26 +73,14 @@ def main():
             print(chain.name, layout, res[f"{chain.name}/{layout}"], flush=True)
             del arena, off, lens, recs, flds
             torch.cuda.empty_cache()
-    # round 2 kernels: the compacted slow path, parse_read over random chunk
-    # splits with every staging plan, flow bins from the 16-bit table
-    from ingot_amd.abi import TUNE_READ_PLAN, TUNE_SLOW_PATH
+    # parse_read over random chunk splits with every staging plan
+    from ingot_amd.abi import TUNE_READ_PLAN
 
     for chain in Chain:
         prof = (GenProfile.GENEVE_ADVERSARIAL if chain == Chain.GeneveOverV6Tunnel
                 else GenProfile.ADVERSARIAL)
         arena, off, lens = ingot_amd.gen_frames(prof, n, seed=args.seed + 10 + int(chain))
         a, o, ln = arena.cpu().numpy(), off.cpu().numpy(), lens.cpu().numpy()
-        w_rec = oracle.parse_batch(a, o, ln, chain, nthreads=16)
-        for sp in (1, 2):  # round 2: re-stage compacted; round 4: resume-style
-            c1 = ingot_amd.Context(0)
-            c1.set_tuning(TUNE_SLOW_PATH, sp)
-            g = c1.parse(arena, off, lens, chain)
-            torch.cuda.synchronize()
-            bad = int((g.cpu().numpy().reshape(n, -1) != w_rec.view(np.uint8).reshape(n, -1))
-                      .any(axis=1).sum())
-            key = f"{chain.name}/slow_path" + ("" if sp == 1 else str(sp))
-            res[key] = {"record_mismatches": bad}
-            print(chain.name, key, res[key], flush=True)
         # 4 chunks per packet at 3 sorted random cuts (empty chunks included)
         rng = np.random.default_rng(args.seed + int(chain))
         cuts = np.sort(rng.integers(0, ln.astype(np.int64)[:, None] + 1, size=(n, 3)), axis=1)
@@ -106,7 +94,7 @@ def main():
         d_so = torch.from_numpy(seg_off).cuda()
         d_sl = torch.from_numpy(seg_len.view(np.int16)).cuda()
         d_ps = torch.from_numpy(pkt_seg.view(np.int32)).cuda()
-        for plan in (0, 1, 2, 3, 7, 8, 9, 10, 15, 16):
+        for plan in (0, 1):
             c2 = ingot_amd.Context(0)
             c2.set_tuning(TUNE_READ_PLAN, plan)
             r, ch = c2.parse_read(arena, d_so, d_sl, d_ps, chain)
@@ -148,30 +136,18 @@ def main():
         "flow_mismatches": int((flow.cpu().numpy().view(np.uint32) != w_flow).sum()),
         "flow16_mismatches": int((flow16.cpu().numpy().view(np.uint32) != w_flow).sum())}
     print("flows", res["flows/VlanUlp"], flush=True)
-    # round 3: flow bins with the address block read per lane (FLOW_KERNEL 3)
-    # at the 2-to-5-chunk window; the C2 ring kernel (64-B slots, no lengths:
-    # k_parse_pipe with its cache policy compiled in) over adversarial bytes,
-    # 16- and 8-B records
-    from ingot_amd.abi import TUNE_FLOW_KERNEL, TUNE_WINDOW_INDEXED
+    # k_parse's flows mode (explicit windows) beside the default k_flows_bits,
+    # on the FLOWS frames and on adversarial frames
+    from ingot_amd.abi import TUNE_WINDOW_INDEXED
 
-    c3 = ingot_amd.Context(0)
-    c3.set_tuning(TUNE_FLOW_KERNEL, 3)
-    c3.set_tuning(TUNE_WINDOW_INDEXED, 1025)
-    f3 = c3.flow_hist(arena, off, lens, Chain.VlanUlp)
-    torch.cuda.synchronize()
-    res["flows/VlanUlp/lane_addr_1025"] = {
-        "flow_mismatches": int((f3.cpu().numpy().view(np.uint32) != w_flow).sum())}
-    print("flows fk3", res["flows/VlanUlp/lane_addr_1025"], flush=True)
-    # round 4: the compacted 5-tuple kernels (tuple.hip, FLOW_KERNEL 4-9) and
-    # the default window, on the FLOWS frames and on adversarial frames
-    for fk in (0, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 15):
+    for fk in (0, 1025, 1056):  # 0: k_flows_bits; else k_parse flows with that window
         c4 = ingot_amd.Context(0)
-        c4.set_tuning(TUNE_FLOW_KERNEL, fk)
+        c4.set_tuning(TUNE_WINDOW_INDEXED, fk)
         f4 = c4.flow_hist(arena, off, lens, Chain.VlanUlp)
         torch.cuda.synchronize()
-        res[f"flows/VlanUlp/fk{fk}"] = {
+        res[f"flows/VlanUlp/win{fk}"] = {
             "flow_mismatches": int((f4.cpu().numpy().view(np.uint32) != w_flow).sum())}
-        print("flows", fk, res[f"flows/VlanUlp/fk{fk}"], flush=True)
+        print("flows", fk, res[f"flows/VlanUlp/win{fk}"], flush=True)
     del arena, off, lens
     torch.cuda.empty_cache()
     for chain in (Chain.GenericUlp, Chain.VlanUlp):
@@ -179,16 +155,18 @@ def main():
                                                 seed=args.seed + 40 + int(chain))
         oracle.flow_hist(arena.cpu().numpy(), off.cpu().numpy(), lens.cpu().numpy(), chain)
         w_adv = oracle.flow_hist.last_flows
-        for fk in (0, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 15):
+        for fk in (0, 1025, 1056):
             c4 = ingot_amd.Context(0)
-            c4.set_tuning(TUNE_FLOW_KERNEL, fk)
+            c4.set_tuning(TUNE_WINDOW_INDEXED, fk)
             f4 = c4.flow_hist(arena, off, lens, chain)
             torch.cuda.synchronize()
-            key = f"flows_adversarial/{chain.name}/fk{fk}"
+            key = f"flows_adversarial/{chain.name}/win{fk}"
             res[key] = {"flow_mismatches": int((f4.cpu().numpy().view(np.uint32) != w_adv).sum())}
             print(key, res[key], flush=True)
         del arena, off, lens
         torch.cuda.empty_cache()
+    # the C2 slot-ring kernel (64-B slots, no lengths) over adversarial
+    # bytes, 16- and 8-B records
     for chain in (Chain.UdpParser, Chain.GenericUlp, Chain.VlanUlp):
         arena, _, _ = ingot_amd.gen_frames(GenProfile.ADVERSARIAL, n, seed=args.seed + 20 +
                                            int(chain), stride=64)

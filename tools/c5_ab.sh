@@ -2,7 +2,7 @@
 # C5 flows-kernel A/B on the GPU box: the flows variants beside the plain
 # parse over the same FLOWS frames (tools/c5_same_run.py), then per-kernel
 # HBM bytes (tools/pmc_kernels.py).  Usage: tools/c5_ab.sh TAG VARIANT...
-# (VARIANT = KEY=VALUE[,KEY=VALUE], e.g. flow_kernel=4)
+# (VARIANT = KEY=VALUE[,KEY=VALUE], e.g. window_indexed=1056)
 set -eo pipefail
 tag=$1; shift
 args=()
