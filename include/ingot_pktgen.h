@@ -67,6 +67,18 @@ int ingot_pktgen_fill(int profile, uint64_t seed, uint64_t first, uint64_t n,
                       const uint64_t* d_off, uint32_t stride, const uint16_t* d_len,
                       uint8_t* d_arena, uint64_t arena_bytes, void* stream);
 
+/*
+ * The same generator on the host (libingot_pktgen_host.so, no HIP): the
+ * same bytes as the device calls for the same arguments, into host memory
+ * (h_arena 16-B aligned); `threads` > 1 splits the work.  bench.py builds its
+ * CPU baseline's sample with these before the process touches the GPU.
+ */
+int ingot_pktgen_lengths_host(int profile, uint64_t seed, uint64_t first, uint64_t n,
+                              uint16_t* h_len, int threads);
+int ingot_pktgen_fill_host(int profile, uint64_t seed, uint64_t first, uint64_t n,
+                           const uint64_t* h_off, uint32_t stride, const uint16_t* h_len,
+                           uint8_t* h_arena, uint64_t arena_bytes, int threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -129,6 +129,15 @@ SIGNATURES = {
         [ctypes.c_int, c_u64, c_u64, c_u64, c_u8p, ctypes.c_uint32, c_u8p, c_u8p, c_u64,
          ctypes.c_void_p],
     ),
+    # the host build of the generator (also in libingot_pktgen_host.so, no HIP)
+    "ingot_pktgen_lengths_host": (
+        ctypes.c_int, [ctypes.c_int, c_u64, c_u64, c_u64, c_u8p, ctypes.c_int],
+    ),
+    "ingot_pktgen_fill_host": (
+        ctypes.c_int,
+        [ctypes.c_int, c_u64, c_u64, c_u64, c_u8p, ctypes.c_uint32, c_u8p, c_u8p, c_u64,
+         ctypes.c_int],
+    ),
 }
 
 _lib: ctypes.CDLL | None = None

@@ -20,7 +20,8 @@ ROOT = PKG.parent
 CSRC = PKG / "csrc"
 BUILD = PKG / "build"
 LIB = PKG / "lib" / "libingot_gpu.so"
-SOURCES = ["parse.hip", "read.hip", "ring.hip", "flow.hip", "tuple.hip", "header.hip", "packed.hip", "pktgen.hip", "stream.hip", "api.cpp"]
+SOURCES = ["parse.hip", "read.hip", "ring.hip", "flow.hip", "tuple.hip", "header.hip", "packed.hip",
+           "pktgen.hip", "pktgen_host.cpp", "stream.hip", "api.cpp"]
 ARCH = "gfx950"
 
 
@@ -89,6 +90,29 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     return LIB
 
 
+HOST_PKTGEN = PKG / "lib" / "libingot_pktgen_host.so"
+
+
+def build_host_pktgen(force: bool = False, verbose: bool = False) -> Path:
+    """The synthetic traffic generator for the host (csrc/pktgen_host.cpp,
+    g++, no HIP): bench.py builds its CPU baseline's sample with it before
+    the process touches the GPU."""
+    src = CSRC / "pktgen_host.cpp"
+    deps = [src, CSRC / "pktgen_core.h", ROOT / "include" / "ingot_pktgen.h",
+            ROOT / "include" / "ingot_gpu.h"]
+    HOST_PKTGEN.parent.mkdir(exist_ok=True)
+    if force or _stale(HOST_PKTGEN, deps):
+        cmd = [shutil.which("g++") or "g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread",
+               "-Wall", f"-I{ROOT / 'include'}", str(src), "-o", str(HOST_PKTGEN)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            HOST_PKTGEN.unlink(missing_ok=True)
+            raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if verbose:
+        print(f"built {HOST_PKTGEN}")
+    return HOST_PKTGEN
+
+
 CPP_TESTS = ROOT / "tests" / "cpp"
 
 
@@ -117,4 +141,5 @@ def build_cpp_tests(verbose: bool = False) -> list[Path]:
 
 if __name__ == "__main__":
     build(force="--force" in sys.argv, verbose=True)
+    build_host_pktgen(force="--force" in sys.argv, verbose=True)
     build_cpp_tests(verbose=True)

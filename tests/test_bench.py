@@ -459,3 +459,75 @@ def test_physical_core_pick_stays_in_one_socket(monkeypatch):
     assert info["sockets_available"] == 2 and info["l3_domains_used"] == 2
     picked, info = bench.physical_core_pick(list(range(6, 16)), 6)  # socket 0 has 2 cores here
     assert all(c >= 8 for c in picked) and info["socket"] == "1"
+
+
+def _fake_line(value, cpu_label="clean", variants=None, ratio=1.3):
+    return {"metric": bench.METRIC, "value": value, "ms_per_step": 0.0118,
+            "config": {"workload": "x"},
+            "roofline": {"frac": 0.72, "pipelined_read_frac": 0.71,
+                         "traffic_detail": {"ratio_to_algorithmic": ratio, "pad": "p" * 900}},
+            "variants": variants or {},
+            "cpu_baseline": {"value": 800.0, "cores": 15, "kind": "port",
+                             "sample": f"{cpu_label}: median of ...", "detail": {"runs": [1] * 500}},
+            "pad": "q" * 3000}
+
+
+def test_compact_line_ends_in_a_summary_of_every_config(tmp_path, monkeypatch):
+    """The driver keeps the line's last ~1,800 characters: the
+    line drops each cpu_baseline's detail and ends in a summary that names
+    C2 (and its 1 GiB record-ring read share), C3, C4 and C5 with their
+    value, step time, kernel roofline fraction, traffic ratio and CPU
+    baseline (clean / contended)."""
+    import json
+
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+    main = _fake_line(88_000, variants={"streams2_rec16_records64": {
+        "us_per_step": 12.5, "read_frac": 0.667}})
+    subs = {"c3": _fake_line(29_000, "contended"), "c4": _fake_line(29_100),
+            "c5": _fake_line(26_000, variants={"plain_parse_streams1_rec16": {
+                "flows_over_plain": 1.07}})}
+    out = bench.compact_line({**main, "sublines": subs, "wall_s_command": 20.0}, "c2")
+    text = json.dumps(out)
+    tail = text[-1800:]
+    for key in ('"c2"', '"c2_records_1GiB_ring"', '"c3"', '"c4"', '"c5"', '"over_plain_parse"',
+                '"traffic_ratio"', '"kernel_frac"', 'contended"'):
+        assert key in tail, key
+    assert "\"detail\"" not in text
+    assert json.loads((tmp_path / "gpurun_out" / "bench_full.json").read_text())[
+        "cpu_baseline"]["detail"]
+    s = out["summary"]
+    assert s["c3"]["cpu"].endswith("contended") and s["c4"]["cpu"].endswith("clean")
+    assert s["c2_records_1GiB_ring"]["step_read_frac"] == 0.667
+
+
+def test_read_chunks_np_equals_read_chunks():
+    """The host chunk tables of the CPU baseline's sample equal the device
+    path's (read_chunks, run here on CPU tensors)."""
+    import torch
+
+    frames = build_frames(3000, seed=5, broken=0.2)
+    arena, off, lens = pack(frames)
+    recs = oracle.parse_batch(arena, off, lens, Chain.GenericUlp)
+    for kind in ("split2", "per_header"):
+        a = bench.read_chunks_np(off, None, lens, recs, kind)
+        b = bench.read_chunks(torch, torch.from_numpy(off.astype(np.int64)), None,
+                              torch.from_numpy(lens.astype(np.int32)), recs, kind, "cpu")
+        assert (a[0] == b[0].numpy().astype(np.uint64)).all()
+        assert (a[1] == b[1].numpy().view(np.uint16)).all() if b[1].dtype != torch.int32 else True
+        assert (a[2] == b[2].numpy().astype(np.uint32)).all()
+
+
+def test_cpu_baseline_labels_what_it_measured():
+    """cpu_baseline names its placements, says clean or contended in the
+    first words of `sample`, and names the measured cause of a low share."""
+    from ingot_amd.hostgen import gen_frames_host
+    from ingot_amd import GenProfile
+
+    arena, off, lens = gen_frames_host(GenProfile.MIXED, 20_000)
+    c = bench.cpu_baseline(arena, off, lens, 0, 20_000, Chain.GenericUlp, budget_s=0.06,
+                           workers=2)
+    assert c["sample"].split(":")[0] in ("clean", "contended")
+    assert c["value"] > 0 and c["cores"] in (1, 2) and c["kind"] == "port"
+    assert {p["placement"].split()[1] for p in c["placements"]} >= {"pinned", "free"}
+    assert isinstance(c["contention"], str) and c["contention"]
+    assert len(c["sample"]) < 200

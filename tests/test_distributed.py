@@ -134,3 +134,155 @@ def test_rank_report_world_one():
     f = torch.tensor([0, -1, 0, 2], dtype=torch.int32)
     r = idist.flow_hist_check(h, f, 3, 3)
     assert r["ok"] and r["hist_total"] == 3
+
+
+class _CpuTorch:
+    """torch for bench.FlowRunner / bench._timed on CPU: streams and events
+    are no-ops; the histograms are real CPU tensors reduced over gloo."""
+
+    class cuda:  # noqa: N801
+        class Event:
+            def __init__(self, enable_timing=False):
+                pass
+
+            def record(self, s=None):
+                pass
+
+            def elapsed_time(self, other):
+                return 1.0
+
+        @staticmethod
+        def synchronize():
+            pass
+
+        class stream:  # noqa: N801
+            def __init__(self, s):
+                pass
+
+            def __enter__(self):
+                return self
+
+            def __exit__(self, *a):
+                return False
+
+    uint8 = torch.uint8
+    empty = staticmethod(torch.empty)
+
+
+class _CpuStream:
+    cuda_stream = 0
+
+    def wait_event(self, ev):
+        pass
+
+
+class _Ptr:
+    def __init__(self, i):
+        self.i = i
+
+    def data_ptr(self):
+        return self.i
+
+
+def _c5_subline_worker(rank, world, port, q):
+    """The C5 sub-line's distributed plumbing at world 4 over gloo: the
+    rank's shard (bench.frames_for_rank), the gate policy RCCL would get,
+    bench.FlowRunner with the real async all-reduce (ingot_amd.dist) — the
+    flows kernel stood in for by the oracle's flow ids over the first frames
+    of the rank's own shard (the host generator, same bytes) — and the
+    line's flow_hist_check, world info and max-over-ranks time."""
+    import bench
+    from ingot_amd import GenProfile
+    from ingot_amd.hostgen import gen_frames_host
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        first, n, total = bench.frames_for_rank("c5", "weak", rank, world)
+        policy = bench.gate_policy(True, world, "nccl", False)
+        m, bins = 4096, bench.FLOW_BINS
+        arena, off, lens = gen_frames_host(GenProfile.FLOWS, m, first=first)
+        hist_np, _ = oracle.flow_hist(arena, off, lens, Chain.VlanUlp, bins=bins)
+        fids = torch.from_numpy(oracle.flow_hist.last_flows.view(np.int32).copy())
+        recs = oracle.parse_batch(arena, off, lens, Chain.VlanUlp).view(REC_DTYPE)
+        ok_l3 = int(((recs["status"] == 0) & (recs["l3_kind"] != 0)).sum())
+        reps = 4
+        hists = [torch.zeros(bins, dtype=torch.int32) for _ in range(reps)]
+        by_ptr = {h.data_ptr(): h for h in hists}
+        log = []
+
+        class _Lib:  # the flows kernel: this rank's histogram into `hist`
+            def ingot_gpu_flow_hist_workspace_size(self, n, bins):
+                return 0
+
+            def ingot_gpu_flow_hist_ws(self, h, arena, optr, lptr, stride, n, c, key, nbins,
+                                       flow, hashes, hist, work, wbytes, stream):
+                log.append("kernel")
+                if hist:
+                    by_ptr[hist].copy_(torch.from_numpy(hist_np.view(np.int32)))
+                return 0
+
+        class _Ctx:
+            _h = None
+
+        class _Gate:
+            def arm(self, streams):
+                log.append("arm")
+
+            def open(self):
+                log.append("open")
+
+        def reduce_fn(h):
+            log.append("reduce")
+            return idist.reduce_histogram_async(h)
+
+        r = bench.FlowRunner(_CpuTorch, _Lib(), _Ctx(), Chain.VlanUlp, m,
+                             [_Ptr(i + 1) for i in range(reps)], _Ptr(0), _Ptr(0), hists,
+                             [_Ptr(0)] * reps, [_CpuStream(), _CpuStream()], reduce_fn,
+                             open_before_collective=policy == "until_collective")
+        steps = 6
+        r.run(steps, gate=_Gate())
+        # the last step's histogram, all-reduced, against every rank's flow ids
+        check = idist.flow_hist_check(hists[(steps - 1) % reps], fids, ok_l3, bins)
+        first_reduce = log.index("reduce")
+        res = {"rank": rank, "first": first, "n": n, "total": total, "policy": policy,
+               "open_before_first_reduce": "open" in log[:first_reduce],
+               "reduces": log.count("reduce"), "check": check, "info": idist.world_info(),
+               "slowest": idist.max_over_ranks(0.1 * (rank + 1))}
+        out = [None] * world
+        dist.all_gather_object(out, res)
+        if rank == 0:
+            q.put(out)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_c5_subline_plumbing_world4_gloo():
+    """before SCALE runs, the N>1 C5 path on the CPU side
+    at world 4 — equal 8,388,608-frame shards, the until_collective gate
+    opened before any all-reduce is enqueued, flow_hist_check ok on the
+    all-reduced histogram, world size 4 in the line's distributed block."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 4
+    procs = [ctx.Process(target=_c5_subline_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [o["n"] for o in out] == [8_388_608] * world
+    assert [o["first"] for o in out] == [r * 8_388_608 for r in range(world)]
+    assert all(o["total"] == 8_388_608 * world for o in out)
+    assert all(o["policy"] == "until_collective" for o in out)
+    assert all(o["open_before_first_reduce"] and o["reduces"] == 6 for o in out)
+    assert all(o["check"]["ok"] and o["check"]["bins_equal_allreduced_bincount"] for o in out)
+    assert out[0]["check"]["hist_total"] == out[0]["check"]["ok_l3_packets_all_ranks"] > 0
+    assert all(o["info"] == {"world_size": 4, "backend": "gloo", "process_group": True}
+               for o in out)
+    assert all(o["slowest"] == pytest.approx(0.4) for o in out)
