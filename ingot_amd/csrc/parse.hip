@@ -159,7 +159,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
             if (valid) {
                 uint4* z = reinterpret_cast<uint4*>(G);
 #pragma unroll
-                for (int k = 0; k < (int)(sizeof(OutT) / 16); ++k) z[k] = make_uint4(0, 0, 0, 0);
+                for (int k = 0; k < (int)(sizeof(OutT) / 16); ++k) st_global(z + k, make_uint4(0, 0, 0, 0));
                 ingot_fields* F;
                 ingot_tunnel_fields* T = nullptr;
                 if constexpr (TUN) {
@@ -169,7 +169,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
                     F = G;
                 }
                 walk<CHAIN, true>(fr, r, F, T);
-                reinterpret_cast<uint4*>(F)[0] = pack(r);
+                st_global(reinterpret_cast<uint4*>(F), pack(r));
             }
         } else if constexpr (MODE == OUT_REC8) {
             walk<CHAIN, false>(fr, r, nullptr, nullptr);
@@ -192,10 +192,10 @@ __global__ __launch_bounds__(BLOCK) void k_parse(ARGS args) {
                 for (uint32_t d = sink.dirty; d; d &= d - 1u) {
                     const uint32_t c = __builtin_ctz(d);
 #pragma unroll
-                    for (uint32_t q = 0; q < WB_BYTES / 16u; ++q) dst[c + q] = fr.chunk(c + q);
+                    for (uint32_t q = 0; q < WB_BYTES / 16u; ++q) st_global(dst + c + q, fr.chunk(c + q));
                 }
             }
-            if (valid && a.out) static_cast<uint4*>(a.out)[i] = pack(r);
+            if (valid && a.out) st_global(static_cast<uint4*>(a.out) + i, pack(r));
             // the window writes must land before the next tile's LDS-DMA
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         } else if constexpr (FLOWS) {

@@ -192,7 +192,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
             if (valid) {
                 uint4* z = reinterpret_cast<uint4*>(G);
 #pragma unroll
-                for (int k = 0; k < (int)(sizeof(OutT) / 16); ++k) z[k] = make_uint4(0, 0, 0, 0);
+                for (int k = 0; k < (int)(sizeof(OutT) / 16); ++k) st_global(z + k, make_uint4(0, 0, 0, 0));
                 ingot_fields* F;
                 ingot_tunnel_fields* T = nullptr;
                 if constexpr (TUN) {
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse_read(ParseArgs a) {
                     F = G;
                 }
                 walk<CHAIN, true>(fr, r, F, T);
-                reinterpret_cast<uint4*>(F)[0] = pack(r);
+                st_global(reinterpret_cast<uint4*>(F), pack(r));
             }
         } else {
             walk<CHAIN, false>(fr, r, nullptr, nullptr);

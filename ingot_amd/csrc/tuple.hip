@@ -13,41 +13,6 @@
 namespace ingot_gpu {
 namespace {
 
-// EARLY: the 5-tuple's frame-byte span [start, end) as far as the window's
-// first bytes tell — the addresses, and the ports when the L4 header follows
-// the L3 header directly (IPv4 after its options, IPv6 without extension
-// headers).  Only a fetch hint: the hash reads whatever it needs wherever it
-// lies, so a span that turns out wrong costs bytes, never results.
-template <int CHAIN, class FR>
-__device__ __forceinline__ void tuple_span_early(const FR& f, uint32_t& start, uint32_t& end) {
-    start = end = 0;
-    const uint32_t len = f.len;
-    if (len < eth::LEN) return;
-    uint32_t et = f.get(0, eth::ethertype);
-    uint32_t p = eth::LEN;
-    if constexpr (CHAIN == INGOT_CHAIN_VLAN_ULP) {
-        for (uint32_t v = 0; v < 2u && (et == ET_VLAN || et == ET_QINQ); ++v) {
-            if (len - p < vlan::LEN) return;
-            et = f.get(p, vlan::ethertype);
-            p += vlan::LEN;
-        }
-    }
-    if (et == ET_IPV4) {
-        if (len - p < ipv4::LEN) return;
-        const uint32_t ihl = f.get(p, ipv4::ihl);
-        const uint32_t hl = ihl * 4u > ipv4::LEN ? ihl * 4u : ipv4::LEN;
-        const uint32_t proto = f.get(p, ipv4::protocol);
-        start = p + 12u;
-        end = proto == IPP_TCP || proto == IPP_UDP ? p + hl + 4u : p + ipv4::LEN;
-    } else if (et == ET_IPV6) {
-        if (len - p < ipv6::LEN) return;
-        const uint32_t nh = f.get(p, ipv6::next_header);
-        start = p + ipv6::SOURCE_BYTE;
-        end = nh == IPP_TCP || nh == IPP_UDP ? p + ipv6::LEN + 4u : p + ipv6::LEN;
-    }
-    if (end > len) end = len;
-}
-
 // The table-free flows kernel: the plain parse's staging and walk, the
 // address block's source chosen per lane (flow_words `lanes`), and the hash
 // computed bit by bit from the key windows in SGPRs (toeplitz9_bits16): no
@@ -123,16 +88,16 @@ template <uint32_t NCH>
 hipError_t go_bits(const FlowArgs& a, int chain, uint32_t g, hipStream_t s) {
     switch (chain) {
     case INGOT_CHAIN_UDP_PARSER:
-        hipLaunchKernelGGL((k_flows_bits<NCH, INGOT_CHAIN_UDP_PARSER>), dim3(g), dim3(BLOCK), 0,
-                           s, a);
+        hipLaunchKernelGGL((k_flows_bits<NCH, INGOT_CHAIN_UDP_PARSER>), dim3(g),
+                           dim3(BLOCK), 0, s, a);
         break;
     case INGOT_CHAIN_GENERIC_ULP:
-        hipLaunchKernelGGL((k_flows_bits<NCH, INGOT_CHAIN_GENERIC_ULP>), dim3(g), dim3(BLOCK), 0,
-                           s, a);
+        hipLaunchKernelGGL((k_flows_bits<NCH, INGOT_CHAIN_GENERIC_ULP>), dim3(g),
+                           dim3(BLOCK), 0, s, a);
         break;
     default:
-        hipLaunchKernelGGL((k_flows_bits<NCH, INGOT_CHAIN_VLAN_ULP>), dim3(g), dim3(BLOCK), 0, s,
-                           a);
+        hipLaunchKernelGGL((k_flows_bits<NCH, INGOT_CHAIN_VLAN_ULP>), dim3(g),
+                           dim3(BLOCK), 0, s, a);
         break;
     }
     return hipGetLastError();

@@ -29,6 +29,20 @@ constexpr uint32_t BLOCK = WAVE * WAVES;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) void lds_void;
 
+// Global-address-space views of device pointers.  A load through a generic
+// pointer compiles to a FLAT load, which counts in lgkmcnt as well as vmcnt:
+// every LDS read issued after it then waits (s_waitcnt lgkmcnt(0)) for the
+// HBM round trip too.  The walk reads frame bytes past the window, chunk
+// descriptors and the 5-tuple past the window through these instead.
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* gbl(const T* p) {
+    return (const __attribute__((address_space(1))) T*)p;
+}
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gbl_mut(T* p) {
+    return (__attribute__((address_space(1))) T*)p;
+}
+
 // HBM -> LDS staging of one 16-B chunk per lane (LDS-DMA).  `nt` (uniform,
 // INGOT_TUNE_CACHE_POLICY bit 0) marks the frame bytes non-temporal: they are
 // read once per launch.
@@ -65,6 +79,14 @@ __device__ __forceinline__ void stage16p(const uint8_t* src, uint32_t* dst, uint
 // hazard recognizer cannot see in asm.)
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+// Plain stores through the global address space (HIP's vector types have no
+// assignment in address space 1; clang's ext vectors do).
+__device__ __forceinline__ void st_global(uint4* dst, const uint4& v) {
+    *(__attribute__((address_space(1))) u32x4*)dst = u32x4{v.x, v.y, v.z, v.w};
+}
+__device__ __forceinline__ void st_global(uint2* dst, const uint2& v) {
+    *(__attribute__((address_space(1))) u32x2*)dst = u32x2{v.x, v.y};
+}
 #define INGOT_ST(op, bits) asm volatile(op " %0, %1, off " bits "\n\ts_nop 1" ::"v"(dst), "v"(x) : "memory")
 #define INGOT_ST_SWITCH(op)                                    \
     switch ((pol >> 3) & 7u) {                                 \
@@ -78,12 +100,12 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void store_rec(uint4* dst, const uint4& v, uint32_t pol) {
     const u32x4 x{v.x, v.y, v.z, v.w};
     INGOT_ST_SWITCH("global_store_dwordx4")
-    *dst = v;
+    st_global(dst, v);
 }
 __device__ __forceinline__ void store_rec(uint2* dst, const uint2& v, uint32_t pol) {
     const u32x2 x{v.x, v.y};
     INGOT_ST_SWITCH("global_store_dwordx2")
-    *dst = v;
+    st_global(dst, v);
 }
 #undef INGOT_ST_SWITCH
 #undef INGOT_ST
@@ -166,13 +188,13 @@ struct Frame {
     __device__ __forceinline__ void be_words_global8(uint32_t i, uint32_t nw,
                                                      uint32_t* out) const {
         const uintptr_t at = (uintptr_t)(g + i);
-        const uint4* q = reinterpret_cast<const uint4*>(at & ~(uintptr_t)15);
+        const auto* q = (const __attribute__((address_space(1))) u32x4*)(at & ~(uintptr_t)15);
         const uint32_t r = (uint32_t)(at & 15u);
         const uint32_t end = r + 4u * nw;
-        const uint4 z = make_uint4(0, 0, 0, 0);
-        const uint4 c0 = q[0];
-        const uint4 c1 = end > 16u ? q[1] : z;
-        const uint4 c2 = end > 32u ? q[2] : z;
+        const u32x4 z = {0u, 0u, 0u, 0u};
+        const u32x4 c0 = q[0];
+        const u32x4 c1 = end > 16u ? q[1] : z;
+        const u32x4 c2 = end > 32u ? q[2] : z;
         const uint32_t d[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y,
                                 c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
         const uint32_t s = r >> 2;
@@ -190,7 +212,7 @@ struct Frame {
     __device__ __forceinline__ uint32_t be32(uint32_t i) const {
         if (i + 4u <= avail) return be(i, 4);
         const uintptr_t at = (uintptr_t)(g + i);
-        const uint32_t* d = reinterpret_cast<const uint32_t*>(at & ~(uintptr_t)3);
+        const auto* d = gbl(reinterpret_cast<const uint32_t*>(at & ~(uintptr_t)3));
         const uint32_t r = (uint32_t)(at & 3u);
         const uint32_t d0 = d[0];
         const uint32_t d1 = r ? d[1] : 0u;
@@ -204,7 +226,8 @@ struct Frame {
     // for the same one DRAM sector.
     __device__ __forceinline__ uint32_t beyond(uint32_t i, uint32_t n) const {
         uint32_t v = 0;
-        for (uint32_t k = 0; k < n; ++k) v = (v << 8) | g[i + k];
+        const auto* gg = gbl(g);
+        for (uint32_t k = 0; k < n; ++k) v = (v << 8) | gg[i + k];
         return v;
     }
 
@@ -266,8 +289,8 @@ struct SegFrameP {
     __device__ __forceinline__ void bounds() const {
         if constexpr (LAZY) {
             if (nseg == kUnknown) {
-                s0 = pkt_seg[pi];
-                nseg = pkt_seg[pi + 1] - s0;
+                s0 = gbl(pkt_seg)[pi];
+                nseg = gbl(pkt_seg)[pi + 1] - s0;
             }
         }
     }
@@ -294,7 +317,8 @@ struct SegFrameP {
             return __builtin_bswap32(__builtin_amdgcn_alignbyte(d1, d0, b & 3u)) >> (32u - 8u * n);
         }
         uint32_t v = 0;
-        for (uint32_t j = 0; j < n; ++j) v = (v << 8) | g[i + j];
+        const auto* gg = gbl(g);
+        for (uint32_t j = 0; j < n; ++j) v = (v << 8) | gg[i + j];
         return v;
     }
     __device__ __forceinline__ uint32_t get(uint32_t hdr, Field f) const {
@@ -329,10 +353,10 @@ struct SegFrameP {
         else if (NPRE >= 2 && k + 1 < nseg && k == 2) enter(o2, l2, 0u);
         else if (NPRE >= 3 && k + 1 < nseg && k == 3) enter(o3, l3, 0u);
         else if constexpr (DENSE) {
-            const uint64_t v = seg_off[s0 + k];  // (offset << 16) | length
+            const uint64_t v = gbl(seg_off)[s0 + k];  // (offset << 16) | length
             enter(v >> 16, (uint32_t)(v & 0xffffu), 0u);
         } else {
-            enter(seg_off[s0 + k], seg_len[s0 + k], 0u);
+            enter(gbl(seg_off)[s0 + k], gbl(seg_len)[s0 + k], 0u);
         }
     }
 };
@@ -898,7 +922,7 @@ __device__ __forceinline__ void put_byte(const FR& f, EditSink& k, uint32_t i, u
         s + WB_BYTES <= k.base + 16 * (int64_t)k.staged) {
         k.dirty |= 1u << (uint32_t)((s - k.base) >> 4);
     } else {
-        k.frame[i] = v;
+        gbl_mut(k.frame)[i] = v;
     }
 }
 
