@@ -25,11 +25,11 @@ for cfg in $cfgs; do
     # per-launch time that run's JSON line (gpurun_out/prof_<cfg>.log) reports
     (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
         -d $R/gpurun_out/prof_$cfg -o run -- python3 $R/bench.py --config $cfg --streams 1 \
-        --steps $s --warmup 20 --no-cpu-baseline --no-variants --no-host-path \
+        --steps $s --warmup 20 --no-cpu-baseline --no-variants --no-host-path --no-sublines \
         > $R/gpurun_out/prof_$cfg.log 2>&1) || exit $?
     f=$(find $R/gpurun_out/prof_$cfg -name "*kernel_stats.csv" | head -1)
     cp "$f" $R/gpurun_out/${tag}_${cfg}_streams1_kernel_stats.csv
-    $S 300 bench_$cfg python bench.py --config $cfg --steps $s --warmup 20 || exit $?
+    $S 300 bench_$cfg python bench.py --config $cfg --steps $s --warmup 20 --no-sublines || exit $?
     # raw rocprofv3 output: the JSON / summary above hold the results, and
     # gpurun copies gpurun_out/ back only below 64 MiB
     rm -rf gpurun_out/pmc_$cfg gpurun_out/prof_$cfg
