@@ -757,6 +757,76 @@ int ingot_gpu_parse_modify(ingot_gpu_ctx* ctx, uint8_t* d_arena,
                            const ingot_edit* edits, uint32_t n_edits,
                            ingot_rec* d_out, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Batched Emit: ingot's `Emit` (ingot-types/src/emit.rs:8-120; the generated
+ * owned `emit_raw`, ingot-macros/src/packet/mod.rs:2097-2255) of one owned
+ * header stack per packet, followed by the packet's own bytes — the tuple
+ * `(headers, &payload[..])` emitted for every packet of a batch, e.g. OPTE's
+ * outbound Geneve encapsulation (outer Ethernet / IPv6 / UDP / Geneve + options
+ * in front of the inner frame, ingot-examples/src/packets.rs:27-40).
+ *
+ * The owned headers are serialised ONCE, on the host, by the caller (ingot's
+ * own `(eth, v6, udp, geneve).emit_vec()`, or ingot_amd.emit_headers in the
+ * Python mirror): `hdr`, hdr_len <= INGOT_MAX_EMIT_HDR bytes of host memory.
+ * The device then writes them in front of every packet and applies the
+ * per-packet setters `sets` (<= INGOT_MAX_EMIT_SETS; host memory) to that
+ * packet's copy, in order: the field `field` (enum ingot_field) of the header
+ * that starts at byte `at` of `hdr` is set (bitfield.rs:188-315 set paths,
+ * neighbouring bits kept, big-endian) to
+ *   INGOT_EMIT_LENGTH  the packet's emitted bytes from `at` to its end, + add
+ *                      (IPv6 payload_len: at = the IPv6 header, add = -40;
+ *                      UDP / IPv4 length: add = 0);
+ *   INGOT_EMIT_U16     ((const uint16_t*)d_values)[i] + add  (device array);
+ *   INGOT_EMIT_U32     ((const uint32_t*)d_values)[i] + add  (device array);
+ *   INGOT_EMIT_VALUE   add (the same value for every packet);
+ * wrapping modulo 2^width.  The field must lie inside hdr (EINVAL).
+ *
+ * ingot_gpu_emit_packets: packet i (hdr_len + d_len[i] bytes) is written at
+ * d_dst + d_dst_off[i]: the headers, then d_src[d_off[i] .. + d_len[i]).
+ * hdr_len 0 is a plain gather-copy (decapsulation: the inner frames at their
+ * parsed offsets).  Sources are read in aligned 16-B blocks (the arena must be
+ * readable to the 16-B boundary past each packet); destinations are written
+ * exactly (packets may be packed back to back); source and destination must
+ * not overlap.
+ *
+ * ingot_gpu_emit_headers: only the header blocks, packet i's at d_out +
+ * (d_out_off ? d_out_off[i] : i * out_stride); LENGTH counts hdr_len +
+ * d_len[i] (the payload that will follow).  With d_out_off[i] = off[i] -
+ * hdr_len into the frames' own arena this is `emit_suffix` into headroom (the
+ * packet becomes contiguous in place); into separate slots it is the header
+ * chunk of a two-chunk packet that ingot_gpu_parse_read parses as is.
+ * ------------------------------------------------------------------------- */
+enum ingot_emit_source {
+    INGOT_EMIT_LENGTH = 0,
+    INGOT_EMIT_U16 = 1,
+    INGOT_EMIT_U32 = 2,
+    INGOT_EMIT_VALUE = 3
+};
+#define INGOT_MAX_EMIT_SETS 8
+#define INGOT_MAX_EMIT_HDR 256
+
+typedef struct ingot_emit_set {
+    uint16_t at;           /* byte offset in hdr of the header holding the field */
+    uint8_t field;         /* enum ingot_field */
+    uint8_t source;        /* enum ingot_emit_source */
+    int32_t add;           /* added to the value (VALUE: the value) */
+    const void* d_values;  /* U16 / U32: n per-packet values (device memory) */
+} ingot_emit_set;
+
+#ifdef __cplusplus
+static_assert(sizeof(ingot_emit_set) == 16, "ingot_emit_set is 16 bytes");
+#endif
+
+int ingot_gpu_emit_packets(ingot_gpu_ctx* ctx, const uint8_t* hdr, uint32_t hdr_len,
+                           const ingot_emit_set* sets, uint32_t n_sets,
+                           const uint8_t* d_src, const uint64_t* d_off,
+                           const uint16_t* d_len, uint64_t n, uint8_t* d_dst,
+                           const uint64_t* d_dst_off, void* stream);
+int ingot_gpu_emit_headers(ingot_gpu_ctx* ctx, const uint8_t* hdr, uint32_t hdr_len,
+                           const ingot_emit_set* sets, uint32_t n_sets,
+                           const uint16_t* d_len, uint64_t n, uint8_t* d_out,
+                           const uint64_t* d_out_off, uint32_t out_stride, void* stream);
+
 /*
  * Flow classification + per-flow histogram (config 5; build-defined, ingot
  * has no flow hash).  For every packet that parses Ok as `chain` with an

@@ -46,9 +46,11 @@ from .abi import (  # noqa: F401  (re-exports)
     L3Kind,
     L4Kind,
     EditOp,
+    EmitSource,
     Field,
     ParseError,
     edits_array,
+    emit_sets_array,
     rec16_to_rec8,
 )
 
@@ -464,6 +466,61 @@ class Context:
             self._h, _ptr(arena), _ptr(off), _ptr(lens), int(stride), n, int(chain),
             e.ctypes.data_as(ctypes.c_void_p), len(e), _ptr(out), _stream(stream, self.device)),
             "ingot_gpu_parse_modify")
+        return out
+
+    def _emit_sets(self, sets, n: int):
+        """[(at, Field, EmitSource, add[, per-packet cuda tensor]), ...] ->
+        (ingot_emit_set array, tensors kept alive for the call)."""
+        rows, keep = [], []
+        for e in sets:
+            vals = e[4] if len(e) > 4 else None
+            if vals is not None:
+                want = _U16 if int(e[2]) == EmitSource.U16 else _U32
+                self._arg("set values", vals, want, n)
+                self._on_device(values=vals)
+                keep.append(vals)
+            rows.append((e[0], e[1], e[2], e[3], None if vals is None else vals.data_ptr()))
+        return emit_sets_array(rows), keep
+
+    def emit_packets(self, hdr: bytes, sets, src, off, lens, dst, dst_off, stream=None):
+        """Batched Emit (ingot_gpu_emit_packets): packet i = the header block
+        `hdr` (owned headers serialised once on the host, e.g. by emit_headers
+        below) with the per-packet setters `sets` applied, then src[off[i] ..
+        + lens[i]), written at dst + dst_off[i].  sets = [(at, Field,
+        EmitSource, add[, per-packet u16/u32 cuda tensor]), ...]."""
+        n = off.numel()
+        hdr = bytes(hdr)
+        self._arg("src", src, _U8)
+        self._arg("off", off, _U64, n)
+        self._arg("lens", lens, _U16, n)
+        self._arg("dst", dst, _U8)
+        self._arg("dst_off", dst_off, _U64, n)
+        self._on_device(src=src, off=off, lens=lens, dst=dst, dst_off=dst_off)
+        s, keep = self._emit_sets(sets, n)
+        h = (ctypes.c_uint8 * max(len(hdr), 1)).from_buffer_copy(hdr or b"\0")
+        _lib.check(self._lib.ingot_gpu_emit_packets(
+            self._h, ctypes.addressof(h), len(hdr), s.ctypes.data_as(ctypes.c_void_p), len(s),
+            _ptr(src), _ptr(off), _ptr(lens), n, _ptr(dst), _ptr(dst_off),
+            _stream(stream, self.device)), "ingot_gpu_emit_packets")
+        return dst
+
+    def emit_header_blocks(self, hdr: bytes, sets, lens, out, out_off=None, stride: int = 0,
+                           stream=None):
+        """ingot_gpu_emit_headers: only the header blocks, packet i's at
+        out + (out_off[i] if out_off is given else i * stride); LENGTH sets
+        count len(hdr) + lens[i]."""
+        n = lens.numel()
+        hdr = bytes(hdr)
+        self._arg("lens", lens, _U16, n)
+        self._arg("out", out, _U8)
+        self._arg("out_off", out_off, _U64, n, optional=True)
+        self._on_device(lens=lens, out=out, out_off=out_off)
+        s, keep = self._emit_sets(sets, n)
+        h = (ctypes.c_uint8 * max(len(hdr), 1)).from_buffer_copy(hdr or b"\0")
+        _lib.check(self._lib.ingot_gpu_emit_headers(
+            self._h, ctypes.addressof(h), len(hdr), s.ctypes.data_as(ctypes.c_void_p), len(s),
+            _ptr(lens), n, _ptr(out), _ptr(out_off), int(stride), _stream(stream, self.device)),
+            "ingot_gpu_emit_headers")
         return out
 
     def flow_hist(self, arena, off, lens, chain: Chain, hist=None, bins: Optional[int] = None,

@@ -106,6 +106,16 @@ SIGNATURES = {
         [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, ctypes.c_uint32, c_u64, ctypes.c_int, c_u8p,
          ctypes.c_uint32, c_u8p, ctypes.c_void_p],
     ),
+    "ingot_gpu_emit_packets": (
+        ctypes.c_int,
+        [ctypes.c_void_p, c_u8p, ctypes.c_uint32, c_u8p, ctypes.c_uint32, c_u8p, c_u8p, c_u8p,
+         c_u64, c_u8p, c_u8p, ctypes.c_void_p],
+    ),
+    "ingot_gpu_emit_headers": (
+        ctypes.c_int,
+        [ctypes.c_void_p, c_u8p, ctypes.c_uint32, c_u8p, ctypes.c_uint32, c_u8p, c_u64, c_u8p,
+         c_u8p, ctypes.c_uint32, ctypes.c_void_p],
+    ),
     "ingot_gpu_flow_hist": (
         ctypes.c_int,
         [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, ctypes.c_uint32, c_u64, ctypes.c_int, c_u8p,

@@ -347,6 +347,38 @@ def edits_array(edits) -> np.ndarray:
     return a
 
 
+class EmitSource(enum.IntEnum):
+    """enum ingot_emit_source: where a per-packet setter's value comes from."""
+
+    LENGTH = 0  # the packet's emitted bytes from the header's start to its end, + add
+    U16 = 1     # a u16 per packet (device array) + add
+    U32 = 2     # a u32 per packet (device array) + add
+    VALUE = 3   # `add` for every packet
+
+
+MAX_EMIT_SETS = 8
+MAX_EMIT_HDR = 256
+
+
+class IngotEmitSet(ctypes.Structure):
+    _fields_ = [("at", U16), ("field", U8), ("source", U8), ("add", ctypes.c_int32),
+                ("d_values", ctypes.c_void_p)]
+
+
+assert ctypes.sizeof(IngotEmitSet) == 16
+EMIT_SET_DTYPE = np.dtype(IngotEmitSet)
+
+
+def emit_sets_array(sets) -> np.ndarray:
+    """[(at, Field, EmitSource, add[, values pointer]), ...] -> ingot_emit_set
+    array (values: a device address for U16 / U32 sources, else 0)."""
+    a = np.zeros(len(sets), dtype=EMIT_SET_DTYPE)
+    for k, e in enumerate(sets):
+        a[k]["at"], a[k]["field"], a[k]["source"], a[k]["add"] = e[0], int(e[1]), int(e[2]), e[3]
+        a[k]["d_values"] = e[4] if len(e) > 4 and e[4] is not None else 0
+    return a
+
+
 class GenProfile(enum.IntEnum):
     """Synthetic traffic profiles (include/ingot_pktgen.h)."""
 

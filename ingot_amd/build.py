@@ -21,7 +21,7 @@ CSRC = PKG / "csrc"
 BUILD = PKG / "build"
 LIB = PKG / "lib" / "libingot_gpu.so"
 SOURCES = ["parse.hip", "read.hip", "ring.hip", "flow.hip", "tuple.hip", "header.hip", "packed.hip",
-           "pktgen.hip", "pktgen_host.cpp", "stream.hip", "api.cpp"]
+           "pktgen.hip", "pktgen_host.cpp", "stream.hip", "emit.hip", "api.cpp"]
 ARCH = "gfx950"
 
 

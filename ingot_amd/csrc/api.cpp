@@ -554,6 +554,81 @@ int ingot_gpu_parse_modify(ingot_gpu_ctx* ctx, uint8_t* d_arena, const uint64_t*
                                              (hipStream_t)stream));
 }
 
+}  // extern "C"
+
+namespace {
+
+// The header block and its setters -> EmitArgs (shared by both emit calls).
+int emit_args(const uint8_t* hdr, uint32_t hdr_len, const ingot_emit_set* sets,
+              uint32_t n_sets, ingot_gpu::EmitArgs& a) {
+    if (hdr_len > INGOT_MAX_EMIT_HDR || (hdr_len && !hdr) || n_sets > INGOT_MAX_EMIT_SETS ||
+        (n_sets && !sets))
+        return INGOT_GPU_EINVAL;
+    if (hdr_len) std::memcpy(a.hdr, hdr, hdr_len);  // the rest stays zero
+    a.hdr_len = hdr_len;
+    for (uint32_t k = 0; k < n_sets; ++k) {
+        const ingot_emit_set& e = sets[k];
+        if (e.field >= INGOT_F_COUNT || e.source > INGOT_EMIT_VALUE) return INGOT_GPU_EINVAL;
+        if ((e.source == INGOT_EMIT_U16 || e.source == INGOT_EMIT_U32) && !e.d_values)
+            return INGOT_GPU_EINVAL;
+        const FieldGeo g = kFieldGeo[e.field];
+        ingot_gpu::EmitSet& d = a.sets[k];
+        d.pos = (uint16_t)(e.at + g.bit / 8u);
+        d.nbytes = (uint8_t)((g.bit % 8u + g.bits + 7u) / 8u);
+        if ((uint32_t)d.pos + d.nbytes > hdr_len) return INGOT_GPU_EINVAL;  // field inside hdr
+        d.rshift = (uint8_t)((8u - ((g.bit + g.bits) % 8u)) % 8u);
+        d.bits = g.bits;
+        d.source = e.source;
+        d.at = e.at;
+        d.add = e.add;
+        d.values = e.d_values;
+    }
+    a.n_sets = n_sets;
+    return INGOT_GPU_SUCCESS;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ingot_gpu_emit_packets(ingot_gpu_ctx* ctx, const uint8_t* hdr, uint32_t hdr_len,
+                           const ingot_emit_set* sets, uint32_t n_sets, const uint8_t* d_src,
+                           const uint64_t* d_off, const uint16_t* d_len, uint64_t n,
+                           uint8_t* d_dst, const uint64_t* d_dst_off, void* stream) {
+    if (!ctx) return INGOT_GPU_EINVAL;
+    ingot_gpu::EmitArgs a{};
+    if (int e = emit_args(hdr, hdr_len, sets, n_sets, a)) return e;
+    if (n == 0) return INGOT_GPU_SUCCESS;
+    if (!d_src || !d_off || !d_len || !d_dst || !d_dst_off) return INGOT_GPU_EINVAL;
+    if (int e = enter(ctx)) return e;
+    a.src = d_src;
+    a.off = d_off;
+    a.len = d_len;
+    a.dst = d_dst;
+    a.dst_off = d_dst_off;
+    a.n = n;
+    return from_hip(ingot_gpu::launch_emit(a, (hipStream_t)stream));
+}
+
+int ingot_gpu_emit_headers(ingot_gpu_ctx* ctx, const uint8_t* hdr, uint32_t hdr_len,
+                           const ingot_emit_set* sets, uint32_t n_sets, const uint16_t* d_len,
+                           uint64_t n, uint8_t* d_out, const uint64_t* d_out_off,
+                           uint32_t out_stride, void* stream) {
+    if (!ctx) return INGOT_GPU_EINVAL;
+    ingot_gpu::EmitArgs a{};
+    if (int e = emit_args(hdr, hdr_len, sets, n_sets, a)) return e;
+    if (!d_out_off && out_stride < hdr_len) return INGOT_GPU_ERANGE;  // blocks would overlap
+    if (n == 0) return INGOT_GPU_SUCCESS;
+    if (!d_len || !d_out || hdr_len == 0) return INGOT_GPU_EINVAL;
+    if (int e = enter(ctx)) return e;
+    a.len = d_len;
+    a.dst = d_out;
+    a.dst_off = d_out_off;
+    a.stride = out_stride;
+    a.n = n;
+    return from_hip(ingot_gpu::launch_emit(a, (hipStream_t)stream));
+}
+
 int ingot_gpu_flow_hist_ws(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
                            const uint16_t* d_len, uint32_t stride, uint64_t n, int chain,
                            const uint8_t* key, uint32_t bins, uint32_t* d_flow, uint32_t* d_hash,

@@ -128,6 +128,32 @@ struct HeaderArgs {
 };
 hipError_t launch_header(const HeaderArgs& a, hipStream_t s);
 
+// Batched Emit (ingot_gpu_emit_packets / _headers, emit.hip).  api.cpp
+// resolves each ingot_emit_set to the covering bytes of its field in the
+// header block, so the kernel needs no tables.
+struct EmitSet {
+    uint16_t pos;      // first covering byte of the field in the header block
+    uint16_t at;       // INGOT_EMIT_LENGTH counts the packet's bytes from here
+    uint8_t nbytes, rshift, bits, source;
+    int32_t add;
+    const void* values;  // U16 / U32 sources: n per-packet values
+};
+struct EmitArgs {
+    const uint8_t* src;      // NULL: header blocks only
+    const uint64_t* off;     // source offsets (whole packets)
+    const uint16_t* len;     // payload bytes per packet
+    uint8_t* dst;
+    const uint64_t* dst_off; // NULL: i * stride
+    uint32_t stride;
+    uint32_t hdr_len;
+    uint64_t n;
+    uint32_t n_sets;
+    EmitSet sets[INGOT_MAX_EMIT_SETS];
+    uint32_t hdr[INGOT_MAX_EMIT_HDR / 4];  // the header block, zero-padded
+};
+static_assert(sizeof(EmitArgs) <= 4096, "EmitArgs exceeds the 4 KiB kernel-argument limit");
+hipError_t launch_emit(const EmitArgs& a, hipStream_t s);
+
 // Lengths-only packed frames (packed.hip): tile base = u64 base of its group
 // of PACKED_GROUP tiles (at the start of `work`, >= packed_workspace(n)
 // bytes) + the tile's u32 prefix within the group (after the group bases).

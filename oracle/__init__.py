@@ -15,7 +15,7 @@ from pathlib import Path
 import numpy as np
 
 from ingot_amd.abi import (FIELDS_DTYPE, GENEVE_FIELDS_DTYPE, REC_DTYPE, Chain,  # ABI layouts only
-                           edits_array)
+                           edits_array, emit_sets_array)
 
 HERE = Path(__file__).resolve().parent
 LIB_PATH = HERE / "build" / "libingot_oracle.so"
@@ -222,6 +222,36 @@ def parse_modify(frame: bytes, chain: Chain, edits):
     rec = parse_modify_batch(buf, np.array([0], dtype=np.uint64),
                              np.array([len(frame)], dtype=np.uint16), chain, edits)
     return buf[:len(frame)].tobytes(), rec[0]
+
+
+def emit_batch(hdr: bytes, sets, src, off, lens, dst, dst_off=None, stride: int = 0,
+               copy: bool = True):
+    """ingot_gpu_emit_packets (copy) / ingot_gpu_emit_headers semantics into
+    the numpy u8 array `dst`, in place.  sets = [(at, Field, EmitSource, add[,
+    per-packet numpy u16/u32 array]), ...]."""
+    lib = load()
+    vp = ctypes.c_void_p
+    lib.oracle_emit_batch.argtypes = [vp, ctypes.c_uint32, vp, ctypes.c_uint32, vp, vp, vp,
+                                      ctypes.c_uint64, vp, vp, ctypes.c_uint32, ctypes.c_int]
+    lens = np.ascontiguousarray(lens, dtype=np.uint16)
+    keep = []
+    rows = []
+    for e in sets:
+        vals = e[4] if len(e) > 4 else None
+        if vals is not None:
+            vals = np.ascontiguousarray(vals)
+            keep.append(vals)
+        rows.append((e[0], e[1], e[2], e[3], None if vals is None else vals.ctypes.data))
+    a = emit_sets_array(rows)
+    hb = np.frombuffer(bytes(hdr) + b"\0", dtype=np.uint8)
+    if off is not None:
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+    if dst_off is not None:
+        dst_off = np.ascontiguousarray(dst_off, dtype=np.uint64)
+    if lib.oracle_emit_batch(_p(hb), len(bytes(hdr)), _p(a), len(a), _p(src), _p(off), _p(lens),
+                             len(lens), _p(dst), _p(dst_off), stride, int(copy)) != 0:
+        raise ValueError("oracle_emit_batch: bad arguments")
+    return dst
 
 
 def be_bits(hdr: bytes, first_bit: int, n_bits: int) -> int:

@@ -926,6 +926,50 @@ int oracle_parse_modify_batch(uint8_t* arena, const uint64_t* off, const uint16_
 }
 
 /* ------------------------------------------------------------------------
+ * Batched Emit (ingot_gpu_emit_packets / _headers semantics): per packet the
+ * owned header block as given (Emit::emit_raw of the caller's header stack,
+ * ingot-types/src/emit.rs:8-120), then each setter in order through the BE
+ * set path (packet/mod.rs:2097-2255, bitfield.rs:188-315), then the payload
+ * bytes (a `&[u8]` member of the emitted tuple: a plain copy).  U16 / U32
+ * sources read host arrays here.  copy = 0: header blocks only, at
+ * dst_off[i] or i * stride.
+ * ---------------------------------------------------------------------- */
+int oracle_emit_batch(const uint8_t* hdr, uint32_t hdr_len, const ingot_emit_set* sets,
+                      uint32_t n_sets, const uint8_t* src, const uint64_t* off,
+                      const uint16_t* len, uint64_t n, uint8_t* dst, const uint64_t* dst_off,
+                      uint32_t stride, int copy) {
+    uint8_t buf[INGOT_MAX_EMIT_HDR];
+    if (hdr_len > INGOT_MAX_EMIT_HDR || n_sets > INGOT_MAX_EMIT_SETS) return -1;
+    for (uint32_t k = 0; k < n_sets; ++k) {
+        const ingot_emit_set* e = &sets[k];
+        if (e->field >= INGOT_F_COUNT || e->source > INGOT_EMIT_VALUE) return -1;
+        const uint32_t bit = FIELD_GEO[e->field].bit, bits = FIELD_GEO[e->field].bits;
+        if (e->at + (bit + bits + 7u) / 8u > hdr_len) return -1;
+    }
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t total = hdr_len + len[i];
+        memcpy(buf, hdr, hdr_len);
+        for (uint32_t k = 0; k < n_sets; ++k) {
+            const ingot_emit_set* e = &sets[k];
+            uint32_t v;
+            switch (e->source) {
+            case INGOT_EMIT_LENGTH: v = total - e->at + (uint32_t)e->add; break;
+            case INGOT_EMIT_U16: v = (uint32_t)((const uint16_t*)e->d_values)[i] + (uint32_t)e->add; break;
+            case INGOT_EMIT_U32: v = ((const uint32_t*)e->d_values)[i] + (uint32_t)e->add; break;
+            default: v = (uint32_t)e->add; break;
+            }
+            const uint32_t bits = FIELD_GEO[e->field].bits;
+            const uint64_t m = bits >= 32 ? 0xffffffffull : ((1ull << bits) - 1u);
+            oracle_be_set_bits(buf + e->at, FIELD_GEO[e->field].bit, bits, v & m);
+        }
+        uint8_t* d = dst + (dst_off ? dst_off[i] : i * (uint64_t)stride);
+        memcpy(d, buf, hdr_len);
+        if (copy) memcpy(d + hdr_len, src + off[i], len[i]);
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------
  * Batch driver (pthreads, static contiguous partition).
  * ---------------------------------------------------------------------- */
 typedef struct {

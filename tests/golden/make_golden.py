@@ -646,6 +646,89 @@ def modify_kats():
     return out
 
 
+def emit_kats():
+    """Batched Emit vectors (ingot_gpu_emit_packets / _headers): an owned
+    header stack (`stack`: header name + the owned struct's field values, as
+    ingot_amd.emit takes them), the bytes ingot's Emit writes for it (`hdr`,
+    written out by hand from the layouts here, not computed), a payload, the
+    per-packet setters and the emitted packet (`after`)."""
+    out = []
+    # ingot/src/tests.rs:503-527 easy_tuple_emit: (Udp, Geneve) emitted.
+    out.append(dict(
+        name="easy_tuple_emit", source="ingot/src/tests.rs:503-527",
+        stack=[["udp", dict(source=1234, destination=5678, length=77, checksum=0xFFFF)],
+               ["geneve", dict(vni=7777, flags=0x40, protocol_type=0x6558)]],
+        hdr=hexs(u16(1234) + u16(5678) + u16(77) + u16(0xFFFF)
+                 + [0x00, 0x40, 0x65, 0x58, 0x00, 0x1E, 0x61, 0x00]),
+        payload="", sets=[], after=None,
+        note="GeneveFlags::CRITICAL_OPTS = 0x40 (geneve.rs:47-53); vni 7777 = 0x001E61"))
+    # ingot/src/tests.rs:462-501 roundtrip_emit_parse_unchanged: the Udp and
+    # the Ipv6 with one RFC 6564 extension header.
+    v6 = ([0x60, 0x21, 0xE2, 0x40]  # version 6 | dscp 0 | ecn Capable1 = 2 | flow 123456
+          + u16(77) + [0x00, 128] + [0] * 15 + [1] + [0] * 16
+          + [59, 0] + [0] * 6)      # IpV6Ext6564 {next_header NO_NH, ext_len 0, 6 B}
+    out.append(dict(
+        name="roundtrip_emit_parse_unchanged_v6", source="ingot/src/tests.rs:474-500",
+        stack=[["ipv6", dict(source=[0] * 15 + [1], destination=[0] * 16, next_header=0,
+                             payload_len=77, hop_limit=128, ecn=2, flow_label=123456,
+                             v6ext=[["ipv6_ext_6564", dict(next_header=59, data=[0] * 6)]])]],
+        hdr=hexs(v6), payload="", sets=[], after=None,
+        note="Ecn::Capable1.to_network() == 2 (ip.rs:105-110)"))
+    out.append(dict(
+        name="roundtrip_emit_parse_unchanged_udp", source="ingot/src/tests.rs:464-472",
+        stack=[["udp", dict(source=1234, destination=5678, length=77, checksum=0xFFFF)]],
+        hdr=hexs(u16(1234) + u16(5678) + u16(77) + u16(0xFFFF)), payload="", sets=[],
+        after=None))
+    # OPTE's outbound encapsulation of the reference tunnel frame
+    # (ingot-examples/src/tests.rs:189-268 / benches/packet.rs:59-128): the
+    # outer Eth / IPv6 / UDP / Geneve(+1 option) stack of that frame, emitted
+    # in front of its inner frame, reproduces it.
+    outer = dict(
+        stack=[["ethernet", dict(destination=OPTE_IN[0:6], source=OPTE_IN[6:12],
+                                 ethertype=0x86DD)],
+               ["ipv6", dict(source=V6_FD02, destination=V6_FD01, next_header=17,
+                             payload_len=0x10, hop_limit=0xF0)],
+               ["udp", dict(source=0x1E61, destination=6081, length=0x14, checksum=0)],
+               ["geneve", dict(vni=0x0004D2, options=[["geneve_opt", dict(opt_class=0x0129,
+                                                                            option_type=0)]])]],
+        hdr=hexs(OPTE_IN[:74]), payload=hexs(OPTE_IN[74:]))
+    out.append(dict(name="encap_reference_tunnel_frame", source="ingot-examples/src/tests.rs:189-268",
+                    sets=[], after=hexs(OPTE_IN), **outer))
+    # The same with the lengths OPTE fills in per packet: IPv6 payload_len =
+    # 124 - 14 - 40 = 70, UDP length = 124 - 54 = 70 (the frame carries 0x10 /
+    # 0x14 as written by the test), plus a per-packet flow-entropy source port
+    # and VNI.
+    after = list(OPTE_IN)
+    after[18:20] = u16(70)
+    after[58:60] = u16(70)
+    out.append(dict(name="encap_lengths_filled", source="ingot-examples/src/tests.rs:189-268",
+                    sets=[[14, "V6_PAYLOAD_LEN", "LENGTH", -40], [54, "UDP_LENGTH", "LENGTH", 0]],
+                    after=hexs(after), **outer))
+    after2 = list(after)
+    after2[54:56] = u16(0xC0DE)
+    after2[66:69] = [0x12, 0x34, 0x56]
+    out.append(dict(name="encap_per_packet_fields", source="ingot-examples/src/tests.rs:189-268",
+                    sets=[[14, "V6_PAYLOAD_LEN", "LENGTH", -40], [54, "UDP_LENGTH", "LENGTH", 0],
+                          [54, "UDP_SOURCE", "U16", 0, 0xC0DE],
+                          [62, "GENEVE_VNI", "U32", 0, 0x123456]],
+                    after=hexs(after2), **outer))
+    # Setters keep the neighbouring bits: flow_label in the IPv6 bitfield word
+    # and the Geneve version next to opt_len (bitfield.rs:188-315).
+    after3 = list(OPTE_IN)
+    after3[15:18] = [0x0A, 0xBC, 0xDE]  # flow label 0xABCDE under version 6 / dscp 0 / ecn 0
+    after3[62] = 0x81                   # version 2 | opt_len 1
+    out.append(dict(name="encap_bitfield_neighbours", source="ingot/src/ip.rs:159-170, geneve.rs:16-44",
+                    sets=[[14, "V6_FLOW_LABEL", "VALUE", 0xABCDE],
+                          [62, "GENEVE_VERSION", "VALUE", 2]],
+                    after=hexs(after3), **outer))
+    # Wrapping: a LENGTH below zero wraps modulo 2^16 (the u16 setter).
+    after4 = list(OPTE_IN)
+    after4[58:60] = u16((124 - 54 - 200) & 0xFFFF)
+    out.append(dict(name="encap_length_wraps", source="include/ingot_gpu.h (emit)",
+                    sets=[[54, "UDP_LENGTH", "LENGTH", -200]], after=hexs(after4), **outer))
+    return out
+
+
 def setter_kats():
     """ingot/src/tests.rs:118-164 (unaligned_bitfield_read_write, setters; BE
     members of TestFunFields, :27-55): the set sequence, then every getter."""
@@ -792,6 +875,7 @@ def main() -> None:
         read_kats=read_kats(),
         modify_kats=modify_kats(),
         setter_kats=setter_kats(),
+        emit_kats=emit_kats(),
         bitfield_kats=bitfield_kats(),
         rss_kats=rss_kats(),
     )
