@@ -374,7 +374,8 @@ def emit_sets_array(sets) -> np.ndarray:
     array (values: a device address for U16 / U32 sources, else 0)."""
     a = np.zeros(len(sets), dtype=EMIT_SET_DTYPE)
     for k, e in enumerate(sets):
-        a[k]["at"], a[k]["field"], a[k]["source"], a[k]["add"] = e[0], int(e[1]), int(e[2]), e[3]
+        add = ((int(e[3]) + (1 << 31)) % (1 << 32)) - (1 << 31)  # modulo 2^32, as the C int32
+        a[k]["at"], a[k]["field"], a[k]["source"], a[k]["add"] = e[0], int(e[1]), int(e[2]), add
         a[k]["d_values"] = e[4] if len(e) > 4 and e[4] is not None else 0
     return a
 

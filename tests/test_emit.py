@@ -326,7 +326,7 @@ def test_emit_argument_errors(ctx, torch):
     # header block too long, too many sets, field outside the block
     assert lib.ingot_gpu_emit_headers(ctx._h, a, 257, None, 0, p, 1, p, None, 512, None) == -1
     assert lib.ingot_gpu_emit_headers(ctx._h, a, 64, sp, 9, p, 1, p, None, 64, None) == -1
-    assert lib.ingot_gpu_emit_headers(ctx._h, a, 7, sp, 1, p, 1, p, None, 64, None) == -1
+    assert lib.ingot_gpu_emit_headers(ctx._h, a, 5, sp, 1, p, 1, p, None, 64, None) == -1
     # a U16 source without values; an unknown source / field
     bad = ingot_amd.emit_sets_array([(0, Field.UDP_SOURCE, EmitSource.U16, 0)])
     assert lib.ingot_gpu_emit_headers(ctx._h, a, 8, bad.ctypes.data_as(ctypes.c_void_p), 1, p,
