@@ -33,8 +33,12 @@
 namespace ingot_gpu {
 namespace {
 
-constexpr uint32_t BLOCK = 256;
+constexpr uint32_t BLOCK = 128;  // two waves: <= 40 KiB of LDS at the largest header block
 constexpr uint32_t WAVE = 64;
+#ifndef INGOT_EMIT_UNROLL
+#define INGOT_EMIT_UNROLL 4
+#endif
+constexpr uint32_t UNROLL = INGOT_EMIT_UNROLL;  // 64-chunk steps whose loads fly together
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -92,118 +96,160 @@ __device__ __forceinline__ uint32_t set_value(const EmitSet& e, uint64_t i, uint
     }
 }
 
-template <uint32_t G, bool COPY>
+// Per-wave LDS: the 64 packets' descriptors, the inclusive prefix of their
+// chunk counts, and each packet's patched header block at its destination's
+// 16-B alignment (RS bytes per packet).
+struct WaveDesc {
+    uint64_t dst[WAVE];   // destination address of packet j
+    uint64_t src[WAVE];   // source address of its payload
+    uint32_t pfx[WAVE];   // inclusive prefix of chunk counts
+    uint32_t len[WAVE];   // payload bytes
+    uint32_t mis[WAVE];   // dmis | s_mis << 8
+    uint32_t _pad[WAVE];
+};
+
+__host__ __device__ constexpr uint32_t region_bytes(uint32_t H) { return (H + 15u + 15u) / 16u * 16u; }
+
+template <bool COPY>
 __global__ __launch_bounds__(BLOCK) void k_emit(EmitArgs a) {
-    constexpr uint32_t GPW = WAVE / G;  // groups (packets in flight) per wave
-    // the header block with 16 zero bytes before and after it, as 16-B blocks
-    __shared__ u32x4 tmpl[INGOT_MAX_EMIT_HDR / 16 + 2];
-    for (uint32_t k = threadIdx.x; k < INGOT_MAX_EMIT_HDR / 16 + 2; k += BLOCK) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    // the header block between zero bytes, as 16-B blocks
+    u32x4* tmpl = reinterpret_cast<u32x4*>(smem);
+    constexpr uint32_t TB = INGOT_MAX_EMIT_HDR / 16 + 4;  // 16 B before, 48 B after
+    for (uint32_t k = threadIdx.x; k < TB; k += BLOCK) {
         const bool in = k >= 1 && k <= INGOT_MAX_EMIT_HDR / 16;
         tmpl[k] = in ? u32x4{a.hdr[4 * k - 4], a.hdr[4 * k - 3], a.hdr[4 * k - 2],
                              a.hdr[4 * k - 1]}
                      : u32x4{0u, 0u, 0u, 0u};
     }
-    __syncthreads();
-    const uint32_t lane = threadIdx.x % WAVE;
-    const uint32_t gl = lane % G;  // lane within the group
-    const uint32_t gw = lane / G;  // group within the wave
-    const uint64_t wave = (uint64_t)blockIdx.x * (BLOCK / WAVE) + threadIdx.x / WAVE;
-    const uint64_t base = wave * WAVE;
-    if (base >= a.n) return;
     const uint32_t H = a.hdr_len;
+    const uint32_t RS = region_bytes(H);
+    const uint32_t lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
+    WaveDesc& wd = reinterpret_cast<WaveDesc*>(smem + TB * 16)[w];
+    uint8_t* regions = smem + TB * 16 + (BLOCK / WAVE) * sizeof(WaveDesc) + w * WAVE * RS;
+    __syncthreads();
+    const uint64_t base = ((uint64_t)blockIdx.x * (BLOCK / WAVE) + w) * WAVE;
+    if (base >= a.n) return;
 
-    // lane j: packet base + j's descriptors and per-packet set values
-    const uint64_t mine = base + lane;
-    const bool have = mine < a.n;
-    const uint32_t my_len = have ? (uint32_t)gbl(a.len)[mine] : 0u;
-    const uint64_t my_dst = have ? (a.dst_off ? gbl(a.dst_off)[mine] : mine * (uint64_t)a.stride)
-                                 : 0u;
-    const uint64_t my_src = (COPY && have) ? gbl(a.off)[mine] : 0u;
-    uint32_t my_val[INGOT_MAX_EMIT_SETS];
+    // 1. lane j: packet base + j (coalesced descriptor and set-value loads)
+    const uint64_t i = base + lane;
+    const bool live = i < a.n;
+    const uint32_t L = live ? (uint32_t)gbl(a.len)[i] : 0u;
+    const uint64_t doff = live ? (a.dst_off ? gbl(a.dst_off)[i] : i * (uint64_t)a.stride) : 0u;
+    const uint64_t soff = (COPY && live) ? gbl(a.off)[i] : 0u;
+    uint32_t v[INGOT_MAX_EMIT_SETS];
 #pragma unroll
     for (uint32_t s = 0; s < INGOT_MAX_EMIT_SETS; ++s)
-        my_val[s] = (s < a.n_sets && have) ? set_value(a.sets[s], mine, H + my_len) : 0u;
+        v[s] = (s < a.n_sets && live) ? set_value(a.sets[s], i, H + L) : 0u;
+    uint8_t* D = a.dst + doff;
+    const uint8_t* S = COPY ? a.src + soff : nullptr;
+    const uint32_t T = H + (COPY ? L : 0u);
+    const uint32_t dmis = (uint32_t)((uintptr_t)D & 15u);
+    const uint32_t s_mis = COPY ? (uint32_t)((uintptr_t)(S - H - dmis) & 15u) : 0u;
+    const uint32_t nch = live ? (dmis + T + 15u) / 16u : 0u;
 
-    const uint32_t count = (uint32_t)min<uint64_t>(WAVE, a.n - base);
-    for (uint32_t p = 0; p < count; p += GPW) {
-        const uint32_t j = p + gw;  // this group's packet within the wave's 64
-        const bool live = j < count;
-        const uint32_t jj = live ? j : p;
-        const uint32_t L = (uint32_t)__shfl((int)my_len, (int)jj);
-        const uint64_t doff = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(my_dst >> 32), (int)jj)
-                               << 32) |
-                              (uint32_t)__shfl((int)(uint32_t)my_dst, (int)jj);
-        const uint64_t soff =
-            COPY ? ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(my_src >> 32), (int)jj) << 32) |
-                       (uint32_t)__shfl((int)(uint32_t)my_src, (int)jj)
-                 : 0u;
-        uint32_t v[INGOT_MAX_EMIT_SETS];
+    // 2. the packet's header block in its region: template bytes shifted to
+    //    the destination's alignment (region byte b = header byte b - dmis),
+    //    then the setters byte by byte (neighbouring bits kept)
+    uint8_t* R = regions + lane * RS;
+    if (H && live) {
+        const uint32_t* t32 = reinterpret_cast<const uint32_t*>(tmpl);
+        const uint32_t sh = 8u * ((16u - dmis) & 3u);
+        for (uint32_t m = 0; m < RS / 4u; ++m) {
+            const uint32_t tb = 16u + 4u * m - dmis;  // template byte of region byte 4m (+16)
+            const uint32_t lo = t32[tb >> 2], hi = t32[(tb >> 2) + 1];
+            reinterpret_cast<uint32_t*>(R)[m] =
+                sh ? (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) : lo;
+        }
 #pragma unroll
-        for (uint32_t s = 0; s < INGOT_MAX_EMIT_SETS; ++s)
-            v[s] = s < a.n_sets ? (uint32_t)__shfl((int)my_val[s], (int)jj) : 0u;
-        uint8_t* D = a.dst + doff;
-        const uint32_t T = H + (COPY ? L : 0u);
-        const uint32_t dmis = (uint32_t)((uintptr_t)D & 15u);
-        const uint32_t nch = (dmis + T + 15u) / 16u;
-        const uint8_t* S = COPY ? a.src + soff : nullptr;
-        // chunk c holds destination bytes r0 = 16c - dmis ...; header byte r
-        // is template block (r + 16) / 16, payload byte r is S + r - H: both
-        // shifts are uniform over the packet's chunks
-        const uint32_t t_mis = (16u - dmis) & 15u;
-        const uint32_t s_mis = COPY ? (uint32_t)((uintptr_t)(S - H - dmis) & 15u) : 0u;
-        uint32_t np = (nch + G - 1) / G;
-        // every group of the wave runs the same number of passes (shuffles)
+        for (uint32_t s = 0; s < INGOT_MAX_EMIT_SETS; ++s) {
+            if (s >= a.n_sets) break;
+            const EmitSet& e = a.sets[s];
+            const uint32_t fm = e.bits >= 32 ? 0xffffffffu : ((1u << e.bits) - 1u);
+            const uint32_t m = fm << e.rshift, vb = (v[s] & fm) << e.rshift;
+            for (uint32_t k = 0; k < e.nbytes; ++k) {
+                const uint32_t shb = 8u * (e.nbytes - 1u - k);
+                uint8_t& b = R[dmis + e.pos + k];
+                b = (uint8_t)((b & ~(m >> shb)) | ((vb >> shb) & (m >> shb)));
+            }
+        }
+    }
+
+    // 3. chunk counts -> inclusive prefix over the wave
+    uint32_t P = nch;
 #pragma unroll
-        for (uint32_t o = G; o < WAVE; o <<= 1) np = max(np, (uint32_t)__shfl_xor((int)np, (int)o));
-        for (uint32_t pass = 0; pass < np; ++pass) {
-            const uint32_t c = pass * G + gl;
-            const bool valid = live && c < nch;
-            const int32_t r0 = (int32_t)(16u * c) - (int32_t)dmis;
+    for (uint32_t o = 1; o < WAVE; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)P, o);
+        if (lane >= o) P += y;
+    }
+    wd.dst[lane] = (uint64_t)(uintptr_t)D;
+    wd.src[lane] = (uint64_t)(uintptr_t)S;
+    wd.pfx[lane] = P;
+    wd.len[lane] = L;
+    wd.mis[lane] = dmis | (s_mis << 8);
+    const uint32_t total = (uint32_t)__shfl((int)P, (int)WAVE - 1);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // 4. the wave's chunks, 64 per step and UNROLL steps at a time (all their
+    //    loads are issued before the first store: bytes in flight): chunk k
+    //    belongs to the first packet whose inclusive prefix exceeds k
+    for (uint32_t k0 = 0; k0 < total; k0 += WAVE * UNROLL) {
+        uint32_t q[UNROLL], c[UNROLL];
+        u32x4 own[UNROLL], nb[UNROLL];
+        bool extra[UNROLL];
+#pragma unroll
+        for (uint32_t u = 0; u < UNROLL; ++u) {
+            const uint32_t k = k0 + u * WAVE + lane;
+            const bool valid = k < total;
+            uint32_t qq = 0;
+#pragma unroll
+            for (uint32_t step = WAVE / 2; step; step >>= 1)
+                if (wd.pfx[qq + step - 1] <= k) qq += step;
+            qq = valid ? qq : 0u;
+            const uint32_t end = wd.pfx[qq];
+            c[u] = valid ? k - (qq ? wd.pfx[qq - 1] : 0u) : 0xffffu;
+            q[u] = qq;
+            own[u] = u32x4{0u, 0u, 0u, 0u};
+            nb[u] = u32x4{0u, 0u, 0u, 0u};
+            extra[u] = false;
+            if (COPY && valid) {
+                const uint32_t mis = wd.mis[qq];
+                const uint32_t qd = mis & 0xffu, qs = mis >> 8;
+                const uint8_t* QS = (const uint8_t*)(uintptr_t)wd.src[qq];
+                const int32_t r0 = (int32_t)(16u * c[u]) - (int32_t)qd;
+                const uintptr_t X = (uintptr_t)QS + (intptr_t)(r0 - (int32_t)H);
+                const uintptr_t B = X & ~(uintptr_t)15;
+                const uintptr_t S0 = (uintptr_t)QS, S1 = (uintptr_t)QS + wd.len[qq];
+                if (B + 16 > S0 && B < S1) own[u] = *(const __attribute__((address_space(1))) u32x4*)B;
+                // the next lane holds block B + 16 only if it has this packet's next chunk
+                if (qs != 0 && (lane == WAVE - 1 || k + 1 >= end) && B + 16 < S1 && B + 32 > S0) {
+                    nb[u] = *(const __attribute__((address_space(1))) u32x4*)(B + 16);
+                    extra[u] = true;
+                }
+            }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < UNROLL; ++u) {
+            const bool valid = c[u] != 0xffffu;
+            const uint32_t qq = q[u];
+            const uint32_t mis = wd.mis[qq];
+            const uint32_t qd = mis & 0xffu, qs = mis >> 8;
+            uint8_t* QD = (uint8_t*)(uintptr_t)wd.dst[qq];
+            const uint32_t QT = H + (COPY ? wd.len[qq] : 0u);
+            const int32_t r0 = (int32_t)(16u * c[u]) - (int32_t)qd;
             u32x4 out = u32x4{0u, 0u, 0u, 0u};
             if (COPY) {
-                // own aligned block: the one holding source byte S + r0 - H
-                const uintptr_t X = (uintptr_t)S + (intptr_t)(r0 - (int32_t)H);
-                const uintptr_t B = X & ~(uintptr_t)15;
-                const uintptr_t S0 = (uintptr_t)S, S1 = (uintptr_t)S + L;
-                u32x4 own = u32x4{0u, 0u, 0u, 0u};
-                if (valid && B + 16 > S0 && B < S1)
-                    own = *(const __attribute__((address_space(1))) u32x4*)B;
-                u32x4 nb;
-                nb.x = (uint32_t)__shfl_down((int)own.x, 1u, (int)G);
-                nb.y = (uint32_t)__shfl_down((int)own.y, 1u, (int)G);
-                nb.z = (uint32_t)__shfl_down((int)own.z, 1u, (int)G);
-                nb.w = (uint32_t)__shfl_down((int)own.w, 1u, (int)G);
-                if (valid && s_mis != 0 && (gl == G - 1 || c + 1 >= nch) && B + 16 < S1 &&
-                    B + 32 > S0)
-                    nb = *(const __attribute__((address_space(1))) u32x4*)(B + 16);
-                out = funnel(own, nb, s_mis);
+                u32x4 n2;
+                n2.x = (uint32_t)__shfl_down((int)own[u].x, 1u);
+                n2.y = (uint32_t)__shfl_down((int)own[u].y, 1u);
+                n2.z = (uint32_t)__shfl_down((int)own[u].z, 1u);
+                n2.w = (uint32_t)__shfl_down((int)own[u].w, 1u);
+                out = funnel(own[u], extra[u] ? nb[u] : n2, qs);
             }
             if (H && valid && r0 < (int32_t)H) {
-                const uint32_t tb = (uint32_t)(r0 + 16) >> 4;
-                u32x4 hb = funnel(tmpl[tb], tmpl[tb + 1], t_mis);
-                // the setters, byte by byte: each covering byte's new value
-                // depends only on its own mask and value bits
-#pragma unroll
-                for (uint32_t s = 0; s < INGOT_MAX_EMIT_SETS; ++s) {
-                    if (s >= a.n_sets) break;
-                    const EmitSet& e = a.sets[s];
-                    const uint32_t fm = e.bits >= 32 ? 0xffffffffu : ((1u << e.bits) - 1u);
-                    const uint32_t m = fm << e.rshift, vb = (v[s] & fm) << e.rshift;
-#pragma unroll
-                    for (uint32_t k = 0; k < 4; ++k) {
-                        if (k >= e.nbytes) break;
-                        const int32_t t = (int32_t)(e.pos + k) - r0;
-                        if (t < 0 || t >= 16) continue;
-                        const uint32_t sh = 8u * (e.nbytes - 1u - k);
-                        const uint32_t bm = ((m >> sh) & 0xffu) << (8u * ((uint32_t)t & 3u));
-                        const uint32_t bv = ((vb >> sh) & 0xffu) << (8u * ((uint32_t)t & 3u));
-                        const uint32_t d = (uint32_t)t >> 2;
-                        if (d == 0) hb.x = (hb.x & ~bm) | bv;
-                        if (d == 1) hb.y = (hb.y & ~bm) | bv;
-                        if (d == 2) hb.z = (hb.z & ~bm) | bv;
-                        if (d == 3) hb.w = (hb.w & ~bm) | bv;
-                    }
-                }
+                const u32x4 hb = *reinterpret_cast<const u32x4*>(regions + qq * RS + 16u * c[u]);
                 const int32_t hc = (int32_t)H - r0;
                 const uint32_t m0 = head_mask(hc, 0), m1 = head_mask(hc, 1),
                                m2 = head_mask(hc, 2), m3 = head_mask(hc, 3);
@@ -214,14 +260,20 @@ __global__ __launch_bounds__(BLOCK) void k_emit(EmitArgs a) {
             }
             if (valid) {
                 const int32_t t0 = r0 < 0 ? -r0 : 0;
-                const int32_t t1 = (int32_t)T - r0 < 16 ? (int32_t)T - r0 : 16;
+                const int32_t t1 = (int32_t)QT - r0 < 16 ? (int32_t)QT - r0 : 16;
                 if (t0 == 0 && t1 == 16) {
-                    *(__attribute__((address_space(1))) u32x4*)(D + r0) = out;
+                    *(__attribute__((address_space(1))) u32x4*)(QD + r0) = out;
                 } else {
-                    for (int32_t t = t0; t < t1; ++t) {
+                    for (int32_t t = t0; t < t1;) {
                         const uint32_t d = (uint32_t)t >> 2;
-                        const uint32_t w = d == 0 ? out.x : d == 1 ? out.y : d == 2 ? out.z : out.w;
-                        gbl_mut(D)[r0 + t] = (uint8_t)(w >> (8 * (t & 3)));
+                        const uint32_t wv = d == 0 ? out.x : d == 1 ? out.y : d == 2 ? out.z : out.w;
+                        if ((t & 3) == 0 && t + 4 <= t1) {
+                            *(__attribute__((address_space(1))) uint32_t*)(QD + r0 + t) = wv;
+                            t += 4;
+                        } else {
+                            gbl_mut(QD)[r0 + t] = (uint8_t)(wv >> (8 * (t & 3)));
+                            ++t;
+                        }
                     }
                 }
             }
@@ -229,12 +281,14 @@ __global__ __launch_bounds__(BLOCK) void k_emit(EmitArgs a) {
     }
 }
 
-template <uint32_t G, bool COPY>
+template <bool COPY>
 hipError_t go(const EmitArgs& a, hipStream_t s) {
     const uint64_t waves = (a.n + WAVE - 1) / WAVE;
     const uint64_t blocks = (waves + BLOCK / WAVE - 1) / (BLOCK / WAVE);
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((k_emit<G, COPY>), dim3((uint32_t)blocks), dim3(BLOCK), 0, s, a);
+    const size_t smem = (INGOT_MAX_EMIT_HDR / 16 + 4) * 16 +
+                        (BLOCK / WAVE) * (sizeof(WaveDesc) + WAVE * region_bytes(a.hdr_len));
+    hipLaunchKernelGGL((k_emit<COPY>), dim3((uint32_t)blocks), dim3(BLOCK), smem, s, a);
     return hipGetLastError();
 }
 
@@ -242,7 +296,7 @@ hipError_t go(const EmitArgs& a, hipStream_t s) {
 
 hipError_t launch_emit(const EmitArgs& a, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
-    return a.src ? go<64, true>(a, s) : go<16, false>(a, s);
+    return a.src ? go<true>(a, s) : go<false>(a, s);
 }
 
 }  // namespace ingot_gpu

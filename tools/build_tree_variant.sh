@@ -2,6 +2,7 @@
 # Build the native library of another git revision for tools/abvariant.py:
 #   bash tools/build_tree_variant.sh NAME REV
 # -> tools/variants/NAME/libingot_gpu.so (ingot_amd/csrc + include at REV).
+# DEFS (optional) adds compiler defines, e.g. DEFS=-DINGOT_EMIT_UNROLL=8.
 set -e
 cd "$(dirname "$0")/.."
 name=$1; rev=$2
@@ -13,7 +14,7 @@ for f in "$src"/ingot_amd/csrc/*.hip "$src"/ingot_amd/csrc/*.cpp; do
     o="$src/$(basename "$f").o"
     x=(); [[ $f == *.cpp ]] && x=(-x hip)
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function \
-        "${x[@]}" -I"$src/include" -c "$f" -o "$o" &
+        "${x[@]}" ${DEFS:-} -I"$src/include" -c "$f" -o "$o" &
     objs+=("$o")
 done
 wait
