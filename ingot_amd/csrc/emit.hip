@@ -51,34 +51,22 @@ __device__ __forceinline__ __attribute__((address_space(1))) T* gbl_mut(T* p) {
     return (__attribute__((address_space(1))) T*)p;
 }
 
-// dword d of the 16 bytes at byte s (uniform 0..15) of the 32-B pair a ++ b
-__device__ __forceinline__ uint32_t pick(const u32x4& a, const u32x4& b, uint32_t k) {
-    switch (k) {
-    case 0: return a.x;
-    case 1: return a.y;
-    case 2: return a.z;
-    case 3: return a.w;
-    case 4: return b.x;
-    case 5: return b.y;
-    case 6: return b.z;
-    case 7: return b.w;
-    default: return 0u;
-    }
-}
+// The 16 bytes at byte s (0..15, per lane) of the 32-B pair a ++ b: rotate
+// by whole dwords in two select stages (2, then 1), then v_alignbyte.
 __device__ __forceinline__ u32x4 funnel(const u32x4& a, const u32x4& b, uint32_t s) {
-    const uint32_t q = s >> 2, sh = (s & 3u) * 8u;
-    u32x4 r;
-    const uint32_t w0 = pick(a, b, q), w1 = pick(a, b, q + 1), w2 = pick(a, b, q + 2),
-                   w3 = pick(a, b, q + 3), w4 = pick(a, b, q + 4);
-    if (sh == 0) {
-        r = u32x4{w0, w1, w2, w3};
-    } else {
-        r.x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> sh);
-        r.y = (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh);
-        r.z = (uint32_t)((((uint64_t)w3 << 32) | w2) >> sh);
-        r.w = (uint32_t)((((uint64_t)w4 << 32) | w3) >> sh);
-    }
-    return r;
+    const bool r2 = s & 8u, r1 = s & 4u;
+    const uint32_t c0 = r2 ? a.z : a.x, c1 = r2 ? a.w : a.y, c2 = r2 ? b.x : a.z,
+                   c3 = r2 ? b.y : a.w, c4 = r2 ? b.z : b.x, c5 = r2 ? b.w : b.y;
+    const uint32_t d0 = r1 ? c1 : c0, d1 = r1 ? c2 : c1, d2 = r1 ? c3 : c2, d3 = r1 ? c4 : c3,
+                   d4 = r1 ? c5 : c4;
+    const uint32_t sh = s & 3u;
+    return u32x4{__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
+                 __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh)};
+}
+
+// The value of the next lane (lane 63: 0): DPP wave_shl:1, no LDS traffic.
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, true);
 }
 
 __device__ __forceinline__ uint32_t head_mask(int32_t hc, uint32_t d) {
@@ -242,10 +230,10 @@ __global__ __launch_bounds__(BLOCK) void k_emit(EmitArgs a) {
             u32x4 out = u32x4{0u, 0u, 0u, 0u};
             if (COPY) {
                 u32x4 n2;
-                n2.x = (uint32_t)__shfl_down((int)own[u].x, 1u);
-                n2.y = (uint32_t)__shfl_down((int)own[u].y, 1u);
-                n2.z = (uint32_t)__shfl_down((int)own[u].z, 1u);
-                n2.w = (uint32_t)__shfl_down((int)own[u].w, 1u);
+                n2.x = from_next_lane(own[u].x);
+                n2.y = from_next_lane(own[u].y);
+                n2.z = from_next_lane(own[u].z);
+                n2.w = from_next_lane(own[u].w);
                 out = funnel(own[u], extra[u] ? nb[u] : n2, qs);
             }
             if (H && valid && r0 < (int32_t)H) {
@@ -264,15 +252,18 @@ __global__ __launch_bounds__(BLOCK) void k_emit(EmitArgs a) {
                 if (t0 == 0 && t1 == 16) {
                     *(__attribute__((address_space(1))) u32x4*)(QD + r0) = out;
                 } else {
-                    for (int32_t t = t0; t < t1;) {
-                        const uint32_t d = (uint32_t)t >> 2;
-                        const uint32_t wv = d == 0 ? out.x : d == 1 ? out.y : d == 2 ? out.z : out.w;
-                        if ((t & 3) == 0 && t + 4 <= t1) {
-                            *(__attribute__((address_space(1))) uint32_t*)(QD + r0 + t) = wv;
-                            t += 4;
+                    // an edge chunk (packets share it): whole dwords inside
+                    // [t0, t1) as dword stores, the rest byte by byte
+                    const uint32_t wv[4] = {out.x, out.y, out.z, out.w};
+#pragma unroll
+                    for (int32_t d = 0; d < 4; ++d) {
+                        if (4 * d >= t0 && 4 * d + 4 <= t1) {
+                            *(__attribute__((address_space(1))) uint32_t*)(QD + r0 + 4 * d) = wv[d];
                         } else {
-                            gbl_mut(QD)[r0 + t] = (uint8_t)(wv >> (8 * (t & 3)));
-                            ++t;
+#pragma unroll
+                            for (int32_t b = 0; b < 4; ++b)
+                                if (4 * d + b >= t0 && 4 * d + b < t1)
+                                    gbl_mut(QD)[r0 + 4 * d + b] = (uint8_t)(wv[d] >> (8 * b));
                         }
                     }
                 }
