@@ -31,6 +31,7 @@ launch streams.  `cpu_baseline` = the C restatement of ingot's parse
 from __future__ import annotations
 
 import argparse
+import ctypes
 import collections
 import json
 import os
@@ -78,9 +79,19 @@ CONFIGS = {
             "C2 frames as the reference's parse-read-v4 chunk chain (ingot-examples/benches/"
             "packet.rs:130-134, 152-156): one chunk per header, 14 / 20 / 8 B + payload, "
             "parse_read over chunk lists, 1,048,576 per GPU, UdpParser"),
+    "c6e": ("MIXED", 1 << 23, None, "GenericUlp",
+            "C6e (SURVEY 8f-4, ingot's Emit): OPTE outbound encapsulation, 8,388,608 inner "
+            "64-1500 B frames per GPU each emitted behind an owned outer Eth / IPv6 / UDP / "
+            "Geneve + 1 option stack (74 B) with per-packet setters (IPv6 payload_len, UDP "
+            "length, flow-entropy UDP source port, VNI) into a packed destination arena"),
 }
 # configs that time something other than the batched parse_slice records
-MODES = {"c5": "flows", "c2m": "modify", "c3r": "read", "c3p": "packed", "c2r": "read"}
+MODES = {"c5": "flows", "c2m": "modify", "c3r": "read", "c3p": "packed", "c2r": "read",
+         "c6e": "emit"}
+EMIT_METRIC = "Mpkt/s device-resident batched Emit (Geneve encapsulation), 64-1500 B inner frames"
+# per packet the emit kernel reads: u64 source offset, u16 length, u64
+# destination offset, the u16 source port and the u32 VNI of its setters
+EMIT_DESC_BYTES = 8 + 2 + 8 + 2 + 4
 # parse_read chunking: "split2" = header span | payload; "per_header" = one
 # chunk per parsed header, then the payload (the reference bench's shape)
 READ_CHUNKS = {"c3r": "split2", "c2r": "per_header"}
@@ -106,7 +117,7 @@ ROTATE_CAP_BYTES = 64 << 30
 # 15.2 us, C2m 20.5 vs 25.0) or 3 (C3s 112.5 vs 115.1); long gather-bound
 # launches gain nothing (C3 606 / 618, C4 324 / 324, C6 392 / 393 us on 1 / 2).
 STREAMS = {"c2": 2, "c2m": 2, "c3": 1, "c3p": 1, "c3r": 1, "c3s": 3, "c4": 1, "c5": 2,
-           "c6": 1, "c2r": 2}
+           "c6": 1, "c2r": 2, "c6e": 1}
 # Staggered streams (gated regions with >= 2 streams): stream i starts
 # i * STAGGER_US behind stream 0 (ingot_gpu_stream_delay), so the streams'
 # launches do not ramp up and drain in lockstep.  0 = start together.
@@ -316,6 +327,10 @@ def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode
             oracle.parse_modify_batch(arena_np, off_np, lens_np, chain,
                                       [(2, Field.UDP_DESTINATION, EditOp.SUB, 1)], stride=stride,
                                       n=n, lib=lib, nthreads=t)
+        elif mode == "emit":
+            hdr, sets, dst_np, dst_off = emit_args
+            oracle.emit_batch(hdr, sets, arena_np, off_np, lens_np[:n], dst_np, dst_off,
+                              nthreads=t, lib=lib)
         else:
             oracle.parse_batch(arena_np, off_np, lens_np, chain, stride=stride, n=n,
                                nthreads=t, lib=lib)
@@ -339,6 +354,14 @@ def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode
     lens_np = None if lens_np is None else np.array(lens_np, copy=True)
     if segs is not None:
         segs = tuple(np.array(x, copy=True) for x in segs)
+    emit_args = None
+    if mode == "emit":  # C6e's stack and setters; the packed destination (first-touched here)
+        hdr, sets = emit_stack()
+        ports, vnis = emit_values(n)
+        sets = [sets[0], sets[1], (*sets[2], ports), (*sets[3], vnis)]
+        ln = lens_np[:n].astype(np.int64) + len(hdr)
+        dst_off = np.cumsum(ln) - ln
+        emit_args = (hdr, sets, np.zeros(int(ln.sum()) + 64, np.uint8), dst_off)
 
     def place(pin):
         """pin: CPUs to pin worker t to (t mod len), or None = free within
@@ -443,7 +466,8 @@ def cpu_baseline(arena_np, off_np, lens_np, stride, n, chain, budget_s=1.5, mode
                  f"cgroup used {others} CPUs, workers got {lows[0]['share_median']} of theirs")
     else:
         cause = "unmeasured (no cgroup cpu.stat)"
-    what = {"parse": "parse_slice", "read": "parse_read", "modify": "parse + set_destination"}
+    what = {"parse": "parse_slice", "read": "parse_read", "modify": "parse + set_destination",
+            "emit": "Emit of the outer stack + payload copy"}
     return {
         "value": round(value, 3), "unit": "Mpkt/s", "cores": pick["workers"], "kind": "port",
         "sample": (f"{label}; {n} frames of the workload, C port of ingot "
@@ -677,6 +701,66 @@ class ModifyRunner:
         self.launch = lambda k: lib.ingot_gpu_parse_modify(h, aptrs[k % reps], optr, lptr,
                                                            stride or 0, n, c, eptr, 1, None,
                                                            sps[k % ns])
+
+    def run(self, steps, gate=None):
+        return _timed(self.torch, self.streams, self.launch, steps, gate=gate)
+
+
+def emit_stack():
+    """C6e's owned outer stack (host serialiser, ingot_amd.emit) and setters:
+    OPTE's outbound Geneve encapsulation (ingot-examples/src/packets.rs:27-40)."""
+    from ingot_amd import EmitSource, Field
+    from ingot_amd import emit as E
+
+    hdr = (E.ethernet(bytes.fromhex("a84025777776"), bytes.fromhex("a84025777777"), 0x86DD)
+           + E.ipv6(bytes.fromhex("fd00000000f7010100000000000000" + "02"),
+                    bytes.fromhex("fd00000000f7010100000000000000" + "01"), 17, hop_limit=64)
+           + E.udp(0, 6081) + E.geneve(0, options=E.geneve_opt(0x0129, 0)))
+    sets = [(14, Field.V6_PAYLOAD_LEN, EmitSource.LENGTH, -40),
+            (54, Field.UDP_LENGTH, EmitSource.LENGTH, 0),
+            (54, Field.UDP_SOURCE, EmitSource.U16, 0),
+            (62, Field.GENEVE_VNI, EmitSource.U32, 0)]
+    return hdr, sets
+
+
+def emit_values(n: int, first: int = 0):
+    """Per-packet flow-entropy source ports and VNIs (pure in the index)."""
+    i = np.arange(first, first + n, dtype=np.uint64)
+    h = (i * np.uint64(0x9E3779B97F4A7C15)) >> np.uint64(32)
+    return ((h & np.uint64(0x3FFF)) | np.uint64(0xC000)).astype(np.uint16), \
+        (h >> np.uint64(8) & np.uint64(0xFFFFFF)).astype(np.uint32)
+
+
+class EmitRunner:
+    """C6e: ingot_gpu_emit_packets per step — arena k % R's frames emitted
+    behind the owned outer stack into a packed destination arena."""
+
+    def __init__(self, torch, lib, ctx, n, arenas, off, lens, first, streams):
+        import ingot_amd
+
+        self.torch, self.streams = torch, streams
+        hdr, sets = emit_stack()
+        ports, vnis = emit_values(n, first)
+        dev = arenas[0].device
+        self._vals = [torch.from_numpy(ports.view(np.int16)).to(dev),
+                      torch.from_numpy(vnis.view(np.int32)).to(dev)]
+        rows = [sets[0], sets[1], (*sets[2], self._vals[0].data_ptr()),
+                (*sets[3], self._vals[1].data_ptr())]
+        self._sets = ingot_amd.emit_sets_array(rows)
+        self._hdr = (ctypes.c_uint8 * len(hdr)).from_buffer_copy(hdr)
+        ln = lens.to(torch.int64)
+        self.dst_off = torch.cumsum(ln + len(hdr), 0) - (ln + len(hdr))
+        self.dst = torch.empty(int((ln + len(hdr)).sum().item()) + 64, dtype=torch.uint8,
+                               device=dev)
+        h, reps = ctx._h, len(arenas)
+        aptrs = [a.data_ptr() for a in arenas]
+        sp, hp, H = self._sets.ctypes.data, ctypes.addressof(self._hdr), len(hdr)
+        optr, lptr = off.data_ptr(), lens.data_ptr()
+        dptr, doptr = self.dst.data_ptr(), self.dst_off.data_ptr()
+        sps = [s.cuda_stream for s in streams]
+        self.launch = lambda k: lib.ingot_gpu_emit_packets(
+            h, hp, H, sp, len(rows), aptrs[k % reps], optr, lptr, n, dptr, doptr,
+            sps[k % len(sps)])
 
     def run(self, steps, gate=None):
         return _timed(self.torch, self.streams, self.launch, steps, gate=gate)
@@ -963,7 +1047,7 @@ def kernel_sources_sha() -> str:
 
 KERNEL_FILE = {"k_parse_read": "read.hip", "k_flows_bits": "tuple.hip",
                "k_parse_pipe": "ring.hip", "k_modify_pipe": "ring.hip",
-               "k_parse_ring": "ring.hip"}
+               "k_parse_ring": "ring.hip", "k_emit": "emit.hip"}
 
 
 def kernel_family(mode: str, ring: bool) -> str:
@@ -972,6 +1056,8 @@ def kernel_family(mode: str, ring: bool) -> str:
         return "k_parse_read"
     if mode == "flows":  # offset-addressed frames, 16-bit table (tuple.hip)
         return "k_flows_bits"
+    if mode == "emit":
+        return "k_emit"
     if mode == "modify":
         return "k_modify_pipe" if ring else "k_parse"
     return "k_parse_pipe" if ring else "k_parse"
@@ -1438,7 +1524,8 @@ def run_config(args, config, env):
     profile, chain = GenProfile[prof_name], Chain[chain_name]
     mode = MODES.get(config, "parse")
     flows = mode == "flows"
-    no_variants = args.no_variants or flows
+    emit = mode == "emit"
+    no_variants = args.no_variants or flows or emit
     # the persistent ring consumer serves fixed slots without a length array
     # (the ring kernel's layout), 16- or 8-B records, not the tunnel chain
     ring_ok = (mode == "parse" and stride is not None and stride >= 64 and prof_name == "V4UDP64"
@@ -1512,6 +1599,8 @@ def run_config(args, config, env):
         if mode == "modify":
             return ModifyRunner(torch, lib, ctx, chain, n, stride, arenas, off, lens,
                                 streams[:nstreams])
+        if emit:
+            return EmitRunner(torch, lib, ctx, n, arenas, off, lens, first, streams[:nstreams])
         if mode == "packed":
             return PackedRunner(torch, lib, ctx, chain, n, arenas, lens, outs,
                                 streams[:nstreams])
@@ -1521,7 +1610,7 @@ def run_config(args, config, env):
         return Runner(torch, lib, ctx, chain, n, stride, arenas, off, lens, outs,
                       streams[:nstreams], record)
 
-    if mode in ("modify", "read", "packed") and args.record == 8:
+    if mode in ("modify", "read", "packed", "emit") and args.record == 8:
         raise SystemExit("8-B records are not offered for this config")
     if chain == Chain.GeneveOverV6Tunnel and args.record == 8:
         raise SystemExit("8-B records are not offered for the tunnel chain (include/ingot_gpu.h)")
@@ -1605,6 +1694,12 @@ def run_config(args, config, env):
         # tile-sum pass; tile sums and bases: 12 B per 64 packets
         rd, wr = algorithmic_bytes(recs_np, lens_np, 0, 2, args.record)
         rd += 2 * n + 12 * ((n + 63) // 64)
+    elif emit:
+        # the payload bytes copied + descriptors and setter values read; the
+        # outer stack + payload written per packet
+        H = len(emit_stack()[0])
+        rd = int(lens_np.astype(np.int64).sum()) + EMIT_DESC_BYTES * n
+        wr = int(lens_np.astype(np.int64).sum()) + H * n
     else:
         rd, wr = algorithmic_bytes(recs_np, lens_np, stride or 0, 0 if stride else 10,
                                    args.record)
@@ -1634,7 +1729,9 @@ def run_config(args, config, env):
         launch_ms = ms_iso / iso_launches
         per_launch = G
     else:
-        iso = runner(1, args.record, flows_only=True)
+        # (C6e: its single-stream runner is the main one; a second would
+        # hold another destination arena)
+        iso = main_run if emit else runner(1, args.record, flows_only=True)
         iso.run(max(10, min(args.warmup, 50)))
         iso_steps = max(20, min(args.steps, 1000))
         ms_iso, _ = iso.run(iso_steps, gate)
@@ -1790,6 +1887,8 @@ def run_config(args, config, env):
                            mode="parse" if flows else mode, segs=segs)
         cpu["measured"] = "after the GPU run (device-generated sample copied back)"
     kname = {"modify": ", parse + setters",
+             "emit": " (ingot_gpu_emit_packets: the wave's packets as one flat run of 16-B "
+                     "destination chunks, header blocks patched once per packet in LDS)",
              "read": ", LAYOUT_SEGMENTED (parse_read" +
                      (", chunk 0 per packet: ingot_gpu_parse_read_first" if read_first else "") +
                      (", chunk bounds on demand: INGOT_TUNE_READ_PLAN 17)" if read_lazy else ")"),
@@ -1799,7 +1898,7 @@ def run_config(args, config, env):
                       "SGPRs; the step adds k_flow_count16 / k_flow_reduce16)"}.get(mode, "")
     read_frac_step = step_rd / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS
     return {
-        "metric": METRIC,
+        "metric": EMIT_METRIC if emit else METRIC,
         "value": round(value, 2),
         "unit": "Mpkt/s",
         "n_gpus": world,

@@ -98,6 +98,38 @@ struct WaveDesc {
 
 __host__ __device__ constexpr uint32_t region_bytes(uint32_t H) { return (H + 15u + 15u) / 16u * 16u; }
 
+__device__ __forceinline__ uint32_t byte_at(const u32x4& v, int32_t t) {
+    const uint32_t d = (uint32_t)t >> 2;
+    const uint32_t w = d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
+    return w >> (8u * ((uint32_t)t & 3u));
+}
+
+// Bytes [t0, t1) of the 16-B chunk v at p (16-B aligned; neighbouring packets
+// own the rest): the whole dwords inside as dword stores, then the head and
+// tail pieces as at most byte + short + byte and short + byte — 9 store
+// instructions for the wave whatever the lanes' ranges.
+__device__ __forceinline__ void store_edge(uint8_t* p, const u32x4& v, int32_t t0, int32_t t1) {
+    auto* g8 = gbl_mut(p);
+    auto* g16 = (__attribute__((address_space(1))) uint16_t*)p;
+    auto* g32 = (__attribute__((address_space(1))) uint32_t*)p;
+    if (0 >= t0 && 4 <= t1) g32[0] = v.x;
+    if (4 >= t0 && 8 <= t1) g32[1] = v.y;
+    if (8 >= t0 && 12 <= t1) g32[2] = v.z;
+    if (12 >= t0 && 16 <= t1) g32[3] = v.w;
+    if (t0 >= t1) return;
+    // head: [t0, end of its dword) cut by t1, when t0 is not dword-aligned
+    int32_t a = t0, hb = (t0 | 3) + 1 < t1 ? (t0 | 3) + 1 : t1;
+    const bool head = (t0 & 3) != 0 || hb - t0 < 4;
+    if (head && (a & 1) && a < hb) { g8[a] = (uint8_t)byte_at(v, a); ++a; }
+    if (head && hb - a >= 2) { g16[a >> 1] = (uint16_t)byte_at(v, a) | (uint16_t)(byte_at(v, a + 1) << 8); a += 2; }
+    if (head && hb - a == 1) g8[a] = (uint8_t)byte_at(v, a);
+    // tail: [start of t1's dword, t1) when t1 cuts a dword after the head's
+    int32_t c = t1 & ~3;
+    const bool tail = (t1 & 3) != 0 && c >= (head ? hb : t0);
+    if (tail && t1 - c >= 2) { g16[c >> 1] = (uint16_t)byte_at(v, c) | (uint16_t)(byte_at(v, c + 1) << 8); c += 2; }
+    if (tail && t1 - c == 1) g8[c] = (uint8_t)byte_at(v, c);
+}
+
 template <bool COPY>
 __global__ __launch_bounds__(BLOCK) void k_emit(EmitArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -141,13 +173,9 @@ __global__ __launch_bounds__(BLOCK) void k_emit(EmitArgs a) {
     //    then the setters byte by byte (neighbouring bits kept)
     uint8_t* R = regions + lane * RS;
     if (H && live) {
-        const uint32_t* t32 = reinterpret_cast<const uint32_t*>(tmpl);
-        const uint32_t sh = 8u * ((16u - dmis) & 3u);
-        for (uint32_t m = 0; m < RS / 4u; ++m) {
-            const uint32_t tb = 16u + 4u * m - dmis;  // template byte of region byte 4m (+16)
-            const uint32_t lo = t32[tb >> 2], hi = t32[(tb >> 2) + 1];
-            reinterpret_cast<uint32_t*>(R)[m] =
-                sh ? (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) : lo;
+        for (uint32_t m = 0; m < RS / 16u; ++m) {
+            const uint32_t tb = 16u + 16u * m - dmis;  // template byte of region byte 16m (+16)
+            reinterpret_cast<u32x4*>(R)[m] = funnel(tmpl[tb >> 4], tmpl[(tb >> 4) + 1], tb & 15u);
         }
 #pragma unroll
         for (uint32_t s = 0; s < INGOT_MAX_EMIT_SETS; ++s) {
@@ -175,7 +203,9 @@ __global__ __launch_bounds__(BLOCK) void k_emit(EmitArgs a) {
     wd.pfx[lane] = P;
     wd.len[lane] = L;
     wd.mis[lane] = dmis | (s_mis << 8);
-    const uint32_t total = (uint32_t)__shfl((int)P, (int)WAVE - 1);
+    const uint32_t CP = (15u + H + 15u) / 16u;
+    const uint32_t total =
+        COPY ? (uint32_t)__shfl((int)P, (int)WAVE - 1) : (uint32_t)min<uint64_t>(WAVE, a.n - base) * CP;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -191,13 +221,20 @@ __global__ __launch_bounds__(BLOCK) void k_emit(EmitArgs a) {
         for (uint32_t u = 0; u < UNROLL; ++u) {
             const uint32_t k = k0 + u * WAVE + lane;
             const bool valid = k < total;
-            uint32_t qq = 0;
+            uint32_t qq = 0, end = 0;
+            if (COPY) {
 #pragma unroll
-            for (uint32_t step = WAVE / 2; step; step >>= 1)
-                if (wd.pfx[qq + step - 1] <= k) qq += step;
-            qq = valid ? qq : 0u;
-            const uint32_t end = wd.pfx[qq];
-            c[u] = valid ? k - (qq ? wd.pfx[qq - 1] : 0u) : 0xffffu;
+                for (uint32_t step = WAVE / 2; step; step >>= 1)
+                    if (wd.pfx[qq + step - 1] <= k) qq += step;
+                qq = valid ? qq : 0u;
+                end = wd.pfx[qq];
+                c[u] = valid ? k - (qq ? wd.pfx[qq - 1] : 0u) : 0xffffu;
+            } else {
+                // header blocks: CP chunks per packet (the most any alignment
+                // needs); the ones past a packet's own count write nothing
+                qq = valid ? k / CP : 0u;
+                c[u] = valid ? k - qq * CP : 0xffffu;
+            }
             q[u] = qq;
             own[u] = u32x4{0u, 0u, 0u, 0u};
             nb[u] = u32x4{0u, 0u, 0u, 0u};
@@ -252,20 +289,7 @@ __global__ __launch_bounds__(BLOCK) void k_emit(EmitArgs a) {
                 if (t0 == 0 && t1 == 16) {
                     *(__attribute__((address_space(1))) u32x4*)(QD + r0) = out;
                 } else {
-                    // an edge chunk (packets share it): whole dwords inside
-                    // [t0, t1) as dword stores, the rest byte by byte
-                    const uint32_t wv[4] = {out.x, out.y, out.z, out.w};
-#pragma unroll
-                    for (int32_t d = 0; d < 4; ++d) {
-                        if (4 * d >= t0 && 4 * d + 4 <= t1) {
-                            *(__attribute__((address_space(1))) uint32_t*)(QD + r0 + 4 * d) = wv[d];
-                        } else {
-#pragma unroll
-                            for (int32_t b = 0; b < 4; ++b)
-                                if (4 * d + b >= t0 && 4 * d + b < t1)
-                                    gbl_mut(QD)[r0 + 4 * d + b] = (uint8_t)(wv[d] >> (8 * b));
-                        }
-                    }
+                    store_edge(QD + r0, out, t0, t1);
                 }
             }
         }

@@ -225,14 +225,15 @@ def parse_modify(frame: bytes, chain: Chain, edits):
 
 
 def emit_batch(hdr: bytes, sets, src, off, lens, dst, dst_off=None, stride: int = 0,
-               copy: bool = True):
+               copy: bool = True, nthreads: int = 1, lib: ctypes.CDLL | None = None):
     """ingot_gpu_emit_packets (copy) / ingot_gpu_emit_headers semantics into
     the numpy u8 array `dst`, in place.  sets = [(at, Field, EmitSource, add[,
     per-packet numpy u16/u32 array]), ...]."""
-    lib = load()
+    lib = lib or load()
     vp = ctypes.c_void_p
     lib.oracle_emit_batch.argtypes = [vp, ctypes.c_uint32, vp, ctypes.c_uint32, vp, vp, vp,
-                                      ctypes.c_uint64, vp, vp, ctypes.c_uint32, ctypes.c_int]
+                                      ctypes.c_uint64, vp, vp, ctypes.c_uint32, ctypes.c_int,
+                                      ctypes.c_int]
     lens = np.ascontiguousarray(lens, dtype=np.uint16)
     keep = []
     rows = []
@@ -249,7 +250,8 @@ def emit_batch(hdr: bytes, sets, src, off, lens, dst, dst_off=None, stride: int 
     if dst_off is not None:
         dst_off = np.ascontiguousarray(dst_off, dtype=np.uint64)
     if lib.oracle_emit_batch(_p(hb), len(bytes(hdr)), _p(a), len(a), _p(src), _p(off), _p(lens),
-                             len(lens), _p(dst), _p(dst_off), stride, int(copy)) != 0:
+                             len(lens), _p(dst), _p(dst_off), stride, int(copy),
+                             nthreads) != 0:
         raise ValueError("oracle_emit_batch: bad arguments")
     return dst
 

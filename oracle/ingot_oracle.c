@@ -934,23 +934,28 @@ int oracle_parse_modify_batch(uint8_t* arena, const uint64_t* off, const uint16_
  * sources read host arrays here.  copy = 0: header blocks only, at
  * dst_off[i] or i * stride.
  * ---------------------------------------------------------------------- */
-int oracle_emit_batch(const uint8_t* hdr, uint32_t hdr_len, const ingot_emit_set* sets,
-                      uint32_t n_sets, const uint8_t* src, const uint64_t* off,
-                      const uint16_t* len, uint64_t n, uint8_t* dst, const uint64_t* dst_off,
-                      uint32_t stride, int copy) {
+typedef struct {
+    const uint8_t* hdr;
+    uint32_t hdr_len;
+    const ingot_emit_set* sets;
+    uint32_t n_sets;
+    const uint8_t* src;
+    const uint64_t* off;
+    const uint16_t* len;
+    uint8_t* dst;
+    const uint64_t* dst_off;
+    uint32_t stride;
+    int copy;
+} emit_job_t;
+
+static void emit_range(void* ctx, uint64_t lo, uint64_t hi) {
+    const emit_job_t* j = (const emit_job_t*)ctx;
     uint8_t buf[INGOT_MAX_EMIT_HDR];
-    if (hdr_len > INGOT_MAX_EMIT_HDR || n_sets > INGOT_MAX_EMIT_SETS) return -1;
-    for (uint32_t k = 0; k < n_sets; ++k) {
-        const ingot_emit_set* e = &sets[k];
-        if (e->field >= INGOT_F_COUNT || e->source > INGOT_EMIT_VALUE) return -1;
-        const uint32_t bit = FIELD_GEO[e->field].bit, bits = FIELD_GEO[e->field].bits;
-        if (e->at + (bit + bits + 7u) / 8u > hdr_len) return -1;
-    }
-    for (uint64_t i = 0; i < n; ++i) {
-        const uint32_t total = hdr_len + len[i];
-        memcpy(buf, hdr, hdr_len);
-        for (uint32_t k = 0; k < n_sets; ++k) {
-            const ingot_emit_set* e = &sets[k];
+    for (uint64_t i = lo; i < hi; ++i) {
+        const uint32_t total = j->hdr_len + j->len[i];
+        memcpy(buf, j->hdr, j->hdr_len);
+        for (uint32_t k = 0; k < j->n_sets; ++k) {
+            const ingot_emit_set* e = &j->sets[k];
             uint32_t v;
             switch (e->source) {
             case INGOT_EMIT_LENGTH: v = total - e->at + (uint32_t)e->add; break;
@@ -962,11 +967,25 @@ int oracle_emit_batch(const uint8_t* hdr, uint32_t hdr_len, const ingot_emit_set
             const uint64_t m = bits >= 32 ? 0xffffffffull : ((1ull << bits) - 1u);
             oracle_be_set_bits(buf + e->at, FIELD_GEO[e->field].bit, bits, v & m);
         }
-        uint8_t* d = dst + (dst_off ? dst_off[i] : i * (uint64_t)stride);
-        memcpy(d, buf, hdr_len);
-        if (copy) memcpy(d + hdr_len, src + off[i], len[i]);
+        uint8_t* d = j->dst + (j->dst_off ? j->dst_off[i] : i * (uint64_t)j->stride);
+        memcpy(d, buf, j->hdr_len);
+        if (j->copy) memcpy(d + j->hdr_len, j->src + j->off[i], j->len[i]);
     }
-    return 0;
+}
+
+int oracle_emit_batch(const uint8_t* hdr, uint32_t hdr_len, const ingot_emit_set* sets,
+                      uint32_t n_sets, const uint8_t* src, const uint64_t* off,
+                      const uint16_t* len, uint64_t n, uint8_t* dst, const uint64_t* dst_off,
+                      uint32_t stride, int copy, int nthreads) {
+    if (hdr_len > INGOT_MAX_EMIT_HDR || n_sets > INGOT_MAX_EMIT_SETS) return -1;
+    for (uint32_t k = 0; k < n_sets; ++k) {
+        const ingot_emit_set* e = &sets[k];
+        if (e->field >= INGOT_F_COUNT || e->source > INGOT_EMIT_VALUE) return -1;
+        const uint32_t bit = FIELD_GEO[e->field].bit, bits = FIELD_GEO[e->field].bits;
+        if (e->at + (bit + bits + 7u) / 8u > hdr_len) return -1;
+    }
+    emit_job_t j = {hdr, hdr_len, sets, n_sets, src, off, len, dst, dst_off, stride, copy};
+    return parallel_ranges(n, nthreads, emit_range, &j) != 0 ? -1 : 0;
 }
 
 /* ------------------------------------------------------------------------

@@ -76,11 +76,12 @@ int oracle_parse_modify_batch(uint8_t* arena, const uint64_t* off, const uint16_
                               uint32_t n_edits, ingot_rec* rec, int nthreads);
 
 /* ingot_gpu_emit_packets (copy = 1) / ingot_gpu_emit_headers (copy = 0)
- * semantics on the host; U16 / U32 set sources are host arrays. */
+ * semantics on the host; U16 / U32 set sources are host arrays.  Packets
+ * written by different threads must not share destination bytes. */
 int oracle_emit_batch(const uint8_t* hdr, uint32_t hdr_len, const ingot_emit_set* sets,
                       uint32_t n_sets, const uint8_t* src, const uint64_t* off,
                       const uint16_t* len, uint64_t n, uint8_t* dst, const uint64_t* dst_off,
-                      uint32_t stride, int copy);
+                      uint32_t stride, int copy, int nthreads);
 
 /* IpProtocol::class (ingot/src/ip.rs:40-54): 0 = None, 1 = FragmentHeader,
  * 2 = Rfc6564. */

@@ -49,7 +49,7 @@ def test_config_table():
         Chain[chain]
     # the metric's configuration (BASELINE.json configs[1]) is the default
     assert bench.CONFIGS["c2"][:4] == ("V4UDP64", 1 << 20, 64, "UdpParser")
-    assert set(bench.MODES.values()) <= {"flows", "modify", "read", "packed"}
+    assert set(bench.MODES.values()) <= {"flows", "modify", "read", "packed", "emit"}
     assert set(bench.STREAMS) == set(bench.CONFIGS)
     assert all(1 <= v <= 4 for v in bench.STREAMS.values())
 
@@ -531,3 +531,15 @@ def test_cpu_baseline_labels_what_it_measured():
     assert {p["placement"].split()[1] for p in c["placements"]} >= {"pinned", "free"}
     assert isinstance(c["contention"], str) and c["contention"]
     assert len(c["sample"]) < 200
+
+
+def test_emit_config_stack_and_values():
+    """C6e's owned stack is OPTE's outer Eth / IPv6 / UDP / Geneve + 1 option
+    (74 B) and its per-packet setter values are pure in the packet index."""
+    hdr, sets = bench.emit_stack()
+    assert len(hdr) == 74 and hdr[12:14] == b"\x86\xdd" and hdr[56:58] == (6081).to_bytes(2, "big")
+    assert [s[0] for s in sets] == [14, 54, 54, 62]
+    p0, v0 = bench.emit_values(1000, first=0)
+    p1, v1 = bench.emit_values(500, first=500)
+    assert (p0[500:] == p1).all() and (v0[500:] == v1).all()
+    assert (p0 >= 0xC000).all() and (v0 < (1 << 24)).all()

@@ -53,7 +53,7 @@ def run_pass(counter: str, config: str, outdir: Path, steps: int, extra=()) -> l
     with open(files[0]) as f:
         for row in csv.DictReader(f):
             name = row.get("Kernel_Name", "")
-            if "k_parse" not in name and "k_modify" not in name and "k_flows" not in name:
+            if not any(k in name for k in ("k_parse", "k_modify", "k_flows", "k_emit")):
                 continue
             c = row.get("Counter_Name")
             if c not in vals:
