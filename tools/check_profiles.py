@@ -61,8 +61,8 @@ def main():
             bad.append(f"{cfg}: no line from the profiled run ({pl})")
             prof_line = line
         rows = list(csv.DictReader(open(sp)))
-        parse = [r for r in rows if "k_parse" in r["Name"] or "k_modify" in r["Name"]
-                 or "k_flows" in r["Name"]]
+        parse = [r for r in rows if any(k in r["Name"] for k in ("k_parse", "k_modify", "k_flows",
+                                                                   "k_emit"))]
         # the line names its kernel (and a C2 run's summary also holds the
         # C3 sub-line's k_parse): match it; else the most-called parse kernel
         named = [r for r in parse if r["Name"] == prof_line["roofline"].get("kernel")]

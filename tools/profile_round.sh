@@ -10,7 +10,7 @@
 #   /usr/local/graft/bin/gpurun --timeout 1200 -- bash tools/profile_round.sh r04 [cfgs...]
 set -u
 tag=${1:-r02}; shift || true
-cfgs=${*:-"c2 c2m c2r c3 c3p c3r c3s c4 c5 c6"}
+cfgs=${*:-"c2 c2m c2r c3 c3p c3r c3s c4 c5 c6 c6e"}
 cd "$GRAFT_REPO_ROOT"
 R=$GRAFT_REPO_ROOT
 export TMPDIR=/tmp
