@@ -29,7 +29,7 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
-CONFIGS = "c2 c2m c2r c3 c3p c3r c3s c4 c5 c6".split()
+CONFIGS = "c2 c2m c2r c3 c3p c3r c3s c4 c5 c6 c6e".split()
 # kernels launched by one timed call besides the dominant one
 EXTRA = {"c3p": ("k_tile_sums", "k_group_scan")}
 
@@ -43,9 +43,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", default="r02")
     ap.add_argument("--logs", default=str(ROOT / "gpurun_out"))
+    ap.add_argument("--configs", default=None,
+                    help="comma list: check only these and merge them into the tag's existing "
+                         "<tag>_bench_all_configs.json")
     args = ap.parse_args()
     out, bad = {}, []
-    for cfg in CONFIGS:
+    dst = ROOT / "profiles" / f"{args.tag}_bench_all_configs.json"
+    only = args.configs.split(",") if args.configs else None
+    if only and dst.exists():
+        prev = json.loads(dst.read_text())
+        out = {k: v for k, v in prev["configs"].items() if k not in only}
+        bad = [b for b in prev["checks_failed"] if b.split(":")[0] not in only]
+    for cfg in (only or CONFIGS):
         lp = Path(args.logs) / f"bench_{cfg}.log"
         sp = ROOT / "profiles" / f"{args.tag}_{cfg}_streams1_kernel_stats.csv"
         pp = ROOT / "profiles" / f"{args.tag}_pmc_{cfg}.json"
@@ -100,7 +109,6 @@ def main():
         print(f"{cfg:4s} value {line['value']:10.1f}  frac line {rl['frac']:.4f} profiled-run "
               f"{pr['frac']:.4f} profile {frac_p:.4f}  mean {mean_us:9.2f} us (profiled-run "
               f"line {pr['launch_mean_us']})  traffic x{rec['traffic_ratio']}")
-    dst = ROOT / "profiles" / f"{args.tag}_bench_all_configs.json"
     dst.write_text(json.dumps({"checks_failed": bad, "configs": out}, indent=1) + "\n")
     for b in bad:
         print("FAIL", b)

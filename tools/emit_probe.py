@@ -12,7 +12,7 @@ interleaved rounds):
   copy      torch's device-to-device copy of the same source bytes (the
             plain-copy ceiling for the packets' payload bytes);
 
-and reports algorithmic GB/s: packets = read sum(len) + 22 B/packet of
+and reports algorithmic GB/s: packets = read sum(len) + 24 B/packet of
 descriptors and set values, write sum(74 + len); headers = read 8 B/packet
 (len + values), write 74 B/packet.
 
@@ -78,7 +78,7 @@ def main():
         "headers": lambda: ctx.emit_header_blocks(hdr, sets, lens, slots, stride=stride),
         "copy": lambda: copy_dst.copy_(arena[:payload]),
     }
-    algo = {"packets": payload + 22 * n + total, "headers": 8 * n + H * n, "copy": 2 * payload}
+    algo = {"packets": payload + 24 * n + total, "headers": 8 * n + H * n, "copy": 2 * payload}
     for f in runs.values():
         f()
     torch.cuda.synchronize()
