@@ -550,6 +550,82 @@ inline std::vector<Modified> modify_batch(Context& ctx,
     return out;
 }
 
+// Batched Emit (ingot_gpu_emit_packets): `hdr` = an owned header stack
+// emitted once (ingot's emit_vec on the host), the setters applied per packet
+// (values per packet for INGOT_EMIT_U16 / U32 sources), then each payload.
+// Returns the emitted packets.
+struct EmitSet {
+    uint16_t at;
+    int field;
+    int source;
+    int32_t add;
+    std::vector<uint32_t> values;  // U16 / U32 sources: one per payload
+};
+
+inline std::vector<std::vector<uint8_t>> emit_batch(Context& ctx, const std::vector<uint8_t>& hdr,
+                                                    const std::vector<EmitSet>& sets,
+                                                    const std::vector<std::vector<uint8_t>>& payloads) {
+    const size_t n = payloads.size();
+    std::vector<uint64_t> off(n), doff(n);
+    std::vector<uint16_t> len(n);
+    size_t total = 0, dtotal = 0;
+    for (size_t i = 0; i < n; ++i) {
+        if (payloads[i].size() + hdr.size() > 65535) throw std::length_error("packet too long");
+        off[i] = total;
+        doff[i] = dtotal;
+        len[i] = (uint16_t)payloads[i].size();
+        total += (payloads[i].size() + 15) / 16 * 16 + 16;
+        dtotal += hdr.size() + payloads[i].size();
+    }
+    std::vector<uint8_t> arena(total + 64, 0), out(dtotal + 64, 0);
+    for (size_t i = 0; i < n; ++i)
+        if (!payloads[i].empty()) std::memcpy(arena.data() + off[i], payloads[i].data(), payloads[i].size());
+    uint8_t *d_arena = nullptr, *d_dst = nullptr;
+    uint64_t *d_off = nullptr, *d_doff = nullptr;
+    uint16_t* d_len = nullptr;
+    std::vector<void*> d_vals;
+    std::vector<ingot_emit_set> es(sets.size());
+    hip_check(hipMalloc(&d_arena, arena.size()), "hipMalloc");
+    hip_check(hipMalloc(&d_dst, out.size()), "hipMalloc");
+    hip_check(hipMalloc(&d_off, n * 8 + 8), "hipMalloc");
+    hip_check(hipMalloc(&d_doff, n * 8 + 8), "hipMalloc");
+    hip_check(hipMalloc(&d_len, n * 2 + 8), "hipMalloc");
+    for (size_t k = 0; k < sets.size(); ++k) {
+        const EmitSet& s = sets[k];
+        es[k] = ingot_emit_set{s.at, (uint8_t)s.field, (uint8_t)s.source, s.add, nullptr};
+        if (s.source == INGOT_EMIT_U16 || s.source == INGOT_EMIT_U32) {
+            if (s.values.size() != n) throw std::invalid_argument("one set value per payload");
+            void* d = nullptr;
+            hip_check(hipMalloc(&d, n * 4 + 8), "hipMalloc");
+            if (s.source == INGOT_EMIT_U16) {
+                std::vector<uint16_t> v(s.values.begin(), s.values.end());
+                hip_check(hipMemcpy(d, v.data(), n * 2, hipMemcpyHostToDevice), "H2D");
+            } else {
+                hip_check(hipMemcpy(d, s.values.data(), n * 4, hipMemcpyHostToDevice), "H2D");
+            }
+            es[k].d_values = d;
+            d_vals.push_back(d);
+        }
+    }
+    hip_check(hipMemcpy(d_arena, arena.data(), arena.size(), hipMemcpyHostToDevice), "H2D");
+    hip_check(hipMemcpy(d_off, off.data(), n * 8, hipMemcpyHostToDevice), "H2D");
+    hip_check(hipMemcpy(d_doff, doff.data(), n * 8, hipMemcpyHostToDevice), "H2D");
+    hip_check(hipMemcpy(d_len, len.data(), n * 2, hipMemcpyHostToDevice), "H2D");
+    check(ingot_gpu_emit_packets(ctx.get(), hdr.data(), (uint32_t)hdr.size(), es.data(),
+                                 (uint32_t)es.size(), d_arena, d_off, d_len, n, d_dst, d_doff,
+                                 nullptr),
+          "ingot_gpu_emit_packets");
+    hip_check(hipMemcpy(out.data(), d_dst, out.size(), hipMemcpyDeviceToHost), "D2H");
+    std::vector<std::vector<uint8_t>> pkts(n);
+    for (size_t i = 0; i < n; ++i)
+        pkts[i].assign(out.begin() + (long)doff[i],
+                       out.begin() + (long)(doff[i] + hdr.size() + len[i]));
+    for (void* p : {(void*)d_arena, (void*)d_dst, (void*)d_off, (void*)d_doff, (void*)d_len})
+        (void)hipFree(p);
+    for (void* p : d_vals) (void)hipFree(p);
+    return pkts;
+}
+
 inline Context& default_context() {
     static Context ctx(0);
     return ctx;

@@ -429,6 +429,52 @@ TEST(bitset_fields_do_not_disturb_neighbours) {
     }
 }
 
+// ingot-examples/src/tests.rs:189-268: the reference tunnel frame's outer
+// stack emitted in front of its inner frame (batched, with OPTE's per-packet
+// setters) parses back as GeneveOverV6Tunnel with those values.
+TEST(encapsulate_and_parse_back) {
+    static const uint8_t frame[] = {
+        0xA8, 0x40, 0x25, 0x77, 0x77, 0x76, 0xA8, 0x40, 0x25, 0x77, 0x77, 0x77, 0x86, 0xDD,
+        0x60, 0x00, 0x00, 0x00, 0x00, 0x10, 0x11, 0xF0,
+        0xFD, 0x00, 0x00, 0x00, 0x00, 0xF7, 0x01, 0x01, 0, 0, 0, 0, 0, 0, 0, 0x02,
+        0xFD, 0x00, 0x00, 0x00, 0x00, 0xF7, 0x01, 0x01, 0, 0, 0, 0, 0, 0, 0, 0x01,
+        0x1E, 0x61, 0x17, 0xC1, 0x00, 0x14, 0x00, 0x00,
+        0x01, 0x00, 0x65, 0x58, 0x00, 0x04, 0xD2, 0x00, 0x01, 0x29, 0x00, 0x00,
+        0xAA, 0x00, 0x04, 0x00, 0xFF, 0x10, 0xAA, 0x00, 0x04, 0x00, 0xFF, 0x01, 0x08, 0x00,
+        0x45, 0x00, 0x00, 36, 0x00, 0x00, 0x00, 0x00, 0xF0, 0x11, 0x00, 0x00,
+        8, 8, 8, 8, 192, 168, 0, 5,
+        0x00, 0x80, 0x00, 53, 0x00, 0x08, 0x00, 0x00, 0, 1, 2, 3, 4, 5, 6, 7};
+    const std::vector<uint8_t> hdr(frame, frame + 74), inner(frame + 74, frame + sizeof(frame));
+    std::vector<std::vector<uint8_t>> payloads;
+    std::vector<uint32_t> ports, vnis;
+    for (uint32_t i = 0; i < 300; ++i) {
+        payloads.push_back(inner);
+        payloads.back().resize(inner.size() + i % 37, (uint8_t)i);  // varied lengths
+        ports.push_back(0xC000 | i);
+        vnis.push_back(0x100000 + i);
+    }
+    auto pkts = gpu::emit_batch(
+        gpu::default_context(), hdr,
+        {{14, INGOT_F_V6_PAYLOAD_LEN, INGOT_EMIT_LENGTH, -40, {}},
+         {54, INGOT_F_UDP_LENGTH, INGOT_EMIT_LENGTH, 0, {}},
+         {54, INGOT_F_UDP_SOURCE, INGOT_EMIT_U16, 0, ports},
+         {62, INGOT_F_GENEVE_VNI, INGOT_EMIT_U32, 0, vnis}},
+        payloads);
+    for (uint32_t i = 0; i < 300; ++i) {
+        const auto& p = pkts[i];
+        ASSERT_EQ(p.size(), 74 + payloads[i].size());
+        ASSERT_TRUE(std::equal(payloads[i].begin(), payloads[i].end(), p.begin() + 74));
+        auto [h, hint, rest] = GeneveOverV6Tunnel::parse(p).unwrap();
+        (void)hint;
+        (void)rest;
+        ASSERT_EQ(h.outer_v6.payload_len(), (uint16_t)(p.size() - 54));
+        ASSERT_EQ(h.outer_udp.length(), (uint16_t)(p.size() - 54));
+        ASSERT_EQ(h.outer_udp.source(), (uint16_t)(0xC000 | i));
+        ASSERT_EQ(h.outer_encap.vni(), 0x100000u + i);
+        ASSERT_EQ(h.outer_udp.destination(), 6081);
+    }
+}
+
 int main() {
     for (auto& [name, fn] : registry()) {
         ++g_run;
