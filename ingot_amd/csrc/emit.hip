@@ -203,7 +203,11 @@ __global__ __launch_bounds__(BLOCK) void k_emit(EmitArgs a) {
     wd.pfx[lane] = P;
     wd.len[lane] = L;
     wd.mis[lane] = dmis | (s_mis << 8);
-    const uint32_t CP = (15u + H + 15u) / 16u;
+    // header blocks: every packet takes CP chunk slots, the most any packet
+    // of this wave needs (5 for 74 B at 16-B aligned slots, 6 unaligned)
+    uint32_t CP = nch;
+#pragma unroll
+    for (uint32_t o = 1; o < WAVE; o <<= 1) CP = max(CP, (uint32_t)__shfl_xor((int)CP, (int)o));
     const uint32_t total =
         COPY ? (uint32_t)__shfl((int)P, (int)WAVE - 1) : (uint32_t)min<uint64_t>(WAVE, a.n - base) * CP;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -213,12 +217,13 @@ __global__ __launch_bounds__(BLOCK) void k_emit(EmitArgs a) {
     // 4. the wave's chunks, 64 per step and UNROLL steps at a time (all their
     //    loads are issued before the first store: bytes in flight): chunk k
     //    belongs to the first packet whose inclusive prefix exceeds k
-    for (uint32_t k0 = 0; k0 < total; k0 += WAVE * UNROLL) {
-        uint32_t q[UNROLL], c[UNROLL];
-        u32x4 own[UNROLL], nb[UNROLL];
-        bool extra[UNROLL];
+    constexpr uint32_t U = COPY ? UNROLL : 2u;  // header blocks: no loads to overlap
+    for (uint32_t k0 = 0; k0 < total; k0 += WAVE * U) {
+        uint32_t q[U], c[U];
+        u32x4 own[U], nb[U];
+        bool extra[U];
 #pragma unroll
-        for (uint32_t u = 0; u < UNROLL; ++u) {
+        for (uint32_t u = 0; u < U; ++u) {
             const uint32_t k = k0 + u * WAVE + lane;
             const bool valid = k < total;
             uint32_t qq = 0, end = 0;
@@ -256,7 +261,7 @@ __global__ __launch_bounds__(BLOCK) void k_emit(EmitArgs a) {
             }
         }
 #pragma unroll
-        for (uint32_t u = 0; u < UNROLL; ++u) {
+        for (uint32_t u = 0; u < U; ++u) {
             const bool valid = c[u] != 0xffffu;
             const uint32_t qq = q[u];
             const uint32_t mis = wd.mis[qq];
