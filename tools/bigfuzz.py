@@ -187,6 +187,67 @@ def main():
         print(chain.name, "ring64", r, flush=True)
         del arena, g16, g8
         torch.cuda.empty_cache()
+    # batched Emit (ingot_gpu_emit_packets / _headers): random header blocks
+    # (1-256 B) with random setters over generator frames, destinations packed
+    # with random gaps (the bytes between packets must stay untouched)
+    from ingot_amd import EmitSource, Field
+
+    for case in range(3):
+        rng = np.random.default_rng(args.seed + 50 + case)
+        prof = (GenProfile.MIXED, GenProfile.ADVERSARIAL, GenProfile.GENEVE)[case]
+        arena, off, lens = ingot_amd.gen_frames(prof, n, seed=args.seed + 60 + case)
+        H = int(rng.integers(1, 257))
+        hdr = rng.integers(0, 256, H, dtype=np.uint8).tobytes()
+        u16 = rng.integers(0, 1 << 16, n, dtype=np.uint64).astype(np.uint16)
+        u32 = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+        host_sets, dev_sets = [], []
+        fields = [f for f in Field]
+        for _ in range(int(rng.integers(0, 9))):
+            f = fields[int(rng.integers(0, len(fields)))]
+            at = int(rng.integers(0, max(1, H - 3)))
+            src = EmitSource(int(rng.integers(0, 4)))
+            add = int(rng.integers(-(1 << 31), 1 << 31))
+            vals = u16 if src == EmitSource.U16 else u32 if src == EmitSource.U32 else None
+            host_sets.append((at, f, src, add) + ((vals,) if vals is not None else ()))
+            dev_sets.append((at, f, src, add) + (
+                (torch.from_numpy(vals.view(np.int16 if vals.dtype == np.uint16 else np.int32))
+                 .cuda(),) if vals is not None else ()))
+        # drop setters whose field would not lie inside the header block
+        keep = []
+        for hs, ds in zip(host_sets, dev_sets):
+            try:
+                oracle.emit_batch(hdr, [hs[:4] + hs[4:5]], np.zeros(16, np.uint8), [0], [0],
+                                  np.zeros(H + 16, np.uint8), [0])
+                keep.append((hs, ds))
+            except ValueError:
+                pass
+        host_sets = [k[0] for k in keep]
+        dev_sets = [k[1] for k in keep]
+        ln = lens.cpu().numpy()
+        tot = H + ln.astype(np.int64)
+        gaps = rng.integers(0, 33, n)
+        dst_off = np.cumsum(np.r_[0, (tot + gaps)[:-1]]) + int(rng.integers(0, 16))
+        fill = rng.integers(0, 256, int(dst_off[-1] + tot[-1] + 64), dtype=np.uint8)
+        dst = torch.from_numpy(fill).cuda()
+        ctx.emit_packets(hdr, dev_sets, arena, off, lens, dst,
+                         torch.from_numpy(dst_off.astype(np.int64)).cuda())
+        # header blocks into each frame's headroom of a second copy
+        hfill = rng.integers(0, 256, int(dst_off[-1] + tot[-1] + 64), dtype=np.uint8)
+        hdst = torch.from_numpy(hfill).cuda()
+        ctx.emit_header_blocks(hdr, dev_sets, lens, hdst,
+                               out_off=torch.from_numpy(dst_off.astype(np.int64)).cuda())
+        torch.cuda.synchronize()
+        want = fill.copy()
+        a = arena.cpu().numpy()
+        oracle.emit_batch(hdr, host_sets, a, off.cpu().numpy(), ln, want, dst_off, nthreads=16)
+        hwant = hfill.copy()
+        oracle.emit_batch(hdr, host_sets, None, None, ln, hwant, dst_off, copy=False, nthreads=16)
+        key = f"emit/{prof.name}/H{H}/sets{len(host_sets)}"
+        res[key] = {"packet_byte_mismatches": int((dst.cpu().numpy() != want).sum()),
+                    "header_block_byte_mismatches": int((hdst.cpu().numpy() != hwant).sum())}
+        print(key, res[key], flush=True)
+        del arena, off, lens, dst, hdst
+        torch.cuda.empty_cache()
     out = {"frames_per_case": n, "seed": args.seed, "wall_s": round(time.time() - t0, 1),
            "cases": res,
            "all_zero": all(v == 0 for c in res.values() for k, v in c.items() if "mismatch" in k)}
