@@ -208,6 +208,8 @@ __global__ __launch_bounds__(BLOCK) void k_emit(EmitArgs a) {
     uint32_t CP = nch;
 #pragma unroll
     for (uint32_t o = 1; o < WAVE; o <<= 1) CP = max(CP, (uint32_t)__shfl_xor((int)CP, (int)o));
+    CP = max(CP, 1u);
+    const uint32_t cp_inv = CP > 1u ? 0xffffffffu / CP + 1u : 0u;  // CP == 1: q = k
     const uint32_t total =
         COPY ? (uint32_t)__shfl((int)P, (int)WAVE - 1) : (uint32_t)min<uint64_t>(WAVE, a.n - base) * CP;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -235,9 +237,11 @@ __global__ __launch_bounds__(BLOCK) void k_emit(EmitArgs a) {
                 end = wd.pfx[qq];
                 c[u] = valid ? k - (qq ? wd.pfx[qq - 1] : 0u) : 0xffffu;
             } else {
-                // header blocks: CP chunks per packet (the most any alignment
-                // needs); the ones past a packet's own count write nothing
-                qq = valid ? k / CP : 0u;
+                // header blocks: CP chunks per packet (the most any packet of
+                // the wave needs); the ones past a packet's own count write
+                // nothing.  k / CP as a multiply-high by the wave's reciprocal
+                // (exact: k < 64 * CP)
+                qq = valid ? (CP == 1u ? k : __umulhi(k, cp_inv)) : 0u;
                 c[u] = valid ? k - qq * CP : 0xffffu;
             }
             q[u] = qq;
