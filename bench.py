@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """bench.py — device-resident L2/L3/L4 parse throughput on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2m|c3|c3r|c3s|c4|c5|c6]
-                    [--streams S] [--record 16|8]
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+                    [--config c2|c2m|c2r|c3|c3p|c3r|c3s|c4|c5|c6|c6e] [--streams S] [--record 16|8]
 
 A *step* is one launch of the parse path over one batch of synthetic frames
 already resident in HBM.  At N=1 the default workload is BASELINE.json
@@ -26,7 +26,10 @@ so concurrent launches on up to 4 streams never share data).
 min(len,128) + max(0, H_i-128) + D, W_i = record bytes) / (timed region / K),
 i.e. the HBM rate the device sustains on this path, from HIP events on the
 launch streams.  `cpu_baseline` = the C restatement of ingot's parse
-(oracle/, "port") on the host cores, rank 0, N=1.
+(oracle/, "port") on the host cores, rank 0, N=1.  C6e (not a parse config:
+ingot's Emit batched, OPTE's outbound encapsulation) reports its own metric:
+algorithmic bytes = the payload read + 24 B/packet of descriptors and setter
+values, the 74-B outer stack + payload written.
 """
 from __future__ import annotations
 
