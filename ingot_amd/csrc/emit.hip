@@ -98,36 +98,45 @@ struct WaveDesc {
 
 __host__ __device__ constexpr uint32_t region_bytes(uint32_t H) { return (H + 15u + 15u) / 16u * 16u; }
 
-__device__ __forceinline__ uint32_t byte_at(const u32x4& v, int32_t t) {
-    const uint32_t d = (uint32_t)t >> 2;
-    const uint32_t w = d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
-    return w >> (8u * ((uint32_t)t & 3u));
+__device__ __forceinline__ uint32_t dword_at(const u32x4& v, uint32_t d) {
+    return d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
 }
 
 // Bytes [t0, t1) of the 16-B chunk v at p (16-B aligned; neighbouring packets
-// own the rest): the whole dwords inside as dword stores, then the head and
-// tail pieces as at most byte + short + byte and short + byte — 9 store
-// instructions for the wave whatever the lanes' ranges.
+// own the rest).  An edge chunk is cut on one side: a packet's first chunk
+// keeps [t0, 16), its last [0, t1).  The whole dwords go as predicated dword
+// stores at constant offsets, the one cut dword as a byte / short piece at
+// p + 4 * (its index); a chunk cut on both sides (a packet shorter than a
+// chunk) takes the byte loop.
 __device__ __forceinline__ void store_edge(uint8_t* p, const u32x4& v, int32_t t0, int32_t t1) {
-    auto* g8 = gbl_mut(p);
-    auto* g16 = (__attribute__((address_space(1))) uint16_t*)p;
     auto* g32 = (__attribute__((address_space(1))) uint32_t*)p;
+    if (t0 >= t1) return;
+    if (t0 > 0 && t1 < 16) {
+        for (int32_t t = t0; t < t1; ++t)
+            gbl_mut(p)[t] = (uint8_t)(dword_at(v, (uint32_t)t >> 2) >> (8 * (t & 3)));
+        return;
+    }
+    // whole dwords inside [t0, t1)
     if (0 >= t0 && 4 <= t1) g32[0] = v.x;
     if (4 >= t0 && 8 <= t1) g32[1] = v.y;
     if (8 >= t0 && 12 <= t1) g32[2] = v.z;
     if (12 >= t0 && 16 <= t1) g32[3] = v.w;
-    if (t0 >= t1) return;
-    // head: [t0, end of its dword) cut by t1, when t0 is not dword-aligned
-    int32_t a = t0, hb = (t0 | 3) + 1 < t1 ? (t0 | 3) + 1 : t1;
-    const bool head = (t0 & 3) != 0 || hb - t0 < 4;
-    if (head && (a & 1) && a < hb) { g8[a] = (uint8_t)byte_at(v, a); ++a; }
-    if (head && hb - a >= 2) { g16[a >> 1] = (uint16_t)byte_at(v, a) | (uint16_t)(byte_at(v, a + 1) << 8); a += 2; }
-    if (head && hb - a == 1) g8[a] = (uint8_t)byte_at(v, a);
-    // tail: [start of t1's dword, t1) when t1 cuts a dword after the head's
-    int32_t c = t1 & ~3;
-    const bool tail = (t1 & 3) != 0 && c >= (head ? hb : t0);
-    if (tail && t1 - c >= 2) { g16[c >> 1] = (uint16_t)byte_at(v, c) | (uint16_t)(byte_at(v, c + 1) << 8); c += 2; }
-    if (tail && t1 - c == 1) g8[c] = (uint8_t)byte_at(v, c);
+    // the cut dword: bytes [t0 & 3, 4) of dword t0 >> 2, or [0, t1 & 3) of t1 >> 2
+    const bool head = t0 > 0;
+    const uint32_t cut = head ? (uint32_t)t0 & 3u : (uint32_t)t1 & 3u;
+    if (cut == 0) return;
+    const uint32_t d = head ? (uint32_t)t0 >> 2 : (uint32_t)t1 >> 2;
+    const uint32_t w = dword_at(v, d);
+    auto* q8 = gbl_mut(p + 4 * d);
+    auto* q16 = (__attribute__((address_space(1))) uint16_t*)(p + 4 * d);
+    if (head) {  // bytes cut..3
+        if (cut == 1) q8[1] = (uint8_t)(w >> 8);
+        if (cut <= 2) q16[1] = (uint16_t)(w >> 16);
+        if (cut == 3) q8[3] = (uint8_t)(w >> 24);
+    } else {     // bytes 0..cut-1
+        if (cut >= 2) q16[0] = (uint16_t)w;
+        if (cut != 2) q8[cut == 1 ? 0 : 2] = (uint8_t)(cut == 1 ? w : w >> 16);
+    }
 }
 
 template <bool COPY>
