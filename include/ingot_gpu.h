@@ -795,6 +795,10 @@ int ingot_gpu_parse_modify(ingot_gpu_ctx* ctx, uint8_t* d_arena,
  * hdr_len into the frames' own arena this is `emit_suffix` into headroom (the
  * packet becomes contiguous in place); into separate slots it is the header
  * chunk of a two-chunk packet that ingot_gpu_parse_read parses as is.
+ * hdr_len must be >= 1 here (EINVAL); slots narrower than the block
+ * (d_out_off NULL, out_stride < hdr_len) are ERANGE.  Header blocks are
+ * written exactly (neighbouring bytes untouched); destinations at any
+ * alignment.
  * ------------------------------------------------------------------------- */
 enum ingot_emit_source {
     INGOT_EMIT_LENGTH = 0,
