@@ -1036,15 +1036,19 @@ def _timed(torch, streams, launch, steps, finish=None, gate=None, group=1):
 def kernel_sources_sha() -> str:
     """Digest of every source the library's kernels are built from: a PMC
     profile in profiles/ is attached to a bench line only when it was taken
-    on these exact sources (tools/pmc_traffic.py records the same digest)."""
+    on these exact sources (tools/pmc_traffic.py records the same digest).
+    Comments and whitespace are left out, so a documentation edit does not
+    detach the profiles; any code change does."""
     import hashlib
+    import re
 
     h = hashlib.sha256()
     files = sorted((ROOT / "ingot_amd" / "csrc").glob("*")) + sorted((ROOT / "include").glob("*.h"))
     for f in files:
         if f.suffix in (".hip", ".h", ".cpp"):
+            code = re.sub(r"/\*.*?\*/|//[^\n]*", "", f.read_text(), flags=re.S)
             h.update(f.name.encode())
-            h.update(f.read_bytes())
+            h.update(re.sub(r"\s+", " ", code).strip().encode())
     return h.hexdigest()[:16]
 
 
