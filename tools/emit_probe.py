@@ -36,6 +36,9 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--hdr-strides", default="",
+                    help="also time header blocks into slots of these strides (comma list)")
+    ap.add_argument("--only", default="", help="time only these runs (comma list)")
     ap.add_argument("--lib", default=None, help="tools/variants/<name>/libingot_gpu.so instead")
     args = ap.parse_args()
     if args.lib:
@@ -79,6 +82,13 @@ def main():
         "copy": lambda: copy_dst.copy_(arena[:payload]),
     }
     algo = {"packets": payload + 24 * n + total, "headers": 8 * n + H * n, "copy": 2 * payload}
+    for st in [int(x) for x in args.hdr_strides.split(",") if x]:
+        sl = torch.empty(n * st + 64, dtype=torch.uint8, device="cuda")
+        runs[f"headers_stride{st}"] = (lambda sl=sl, st=st:
+                                       ctx.emit_header_blocks(hdr, sets, lens, sl, stride=st))
+        algo[f"headers_stride{st}"] = 8 * n + H * n
+    if args.only:
+        runs = {k: f for k, f in runs.items() if k in args.only.split(",")}
     for f in runs.values():
         f()
     torch.cuda.synchronize()
