@@ -10,7 +10,11 @@
 //            slots per instruction;
 //   lane16f  lane16 with the whole slot stored (H rounded up to 16) — the
 //            bound if the tail bytes were the kernel's to write;
-//   memset   the slots' whole span written contiguously, 16 B per lane.
+//   memset   the slots' whole span written contiguously, 16 B per lane;
+//   edit8    dwords 5 and 6 of every 64-B slot (bytes 20..27: an IPv4 TTL /
+//            checksum edit behind a 14-B Ethernet header), the rest of the
+//            line left alone — against memset of the same span, the choice
+//            an in-place rewrite (k_modify_pipe) makes.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -30,6 +34,14 @@ __device__ __forceinline__ void store_piece(uint8_t* p, u32x4 v, int t0, int t1)
         return;
     }
     for (int t = t0; t < t1; ++t) p[t] = (uint8_t)(v[t >> 2] >> (8 * (t & 3)));
+}
+
+__global__ void k_edit8(uint8_t* d, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    auto* p = (__attribute__((address_space(1))) uint32_t*)(d + 64 * i);
+    p[5] = (uint32_t)i;
+    p[6] = 7u;
 }
 
 template <bool FULL>
@@ -97,6 +109,8 @@ int main(int argc, char** argv) {
             timeit("flat16", st, [&] { k_flat16<<<(k + 255) / 256, 256>>>(d, n, st, H); });
         }
     }
+    timeit("edit8", 64, [&] { k_edit8<<<(n + 255) / 256, 256>>>(d, n); });
+    timeit("memset", 64, [&] { k_memset<<<(n * 4 + 255) / 256, 256>>>(d, n * 4); });
     hipFree(d);
     return 0;
 }
