@@ -2,6 +2,7 @@
 // header-block emit can take (ingot_gpu_emit_headers into slots).
 //   hipcc --offload-arch=gfx950 -O3 -o tools/variants/store_probe tools/store_probe.hip
 //   tools/variants/store_probe [n_slots]
+//   tools/variants/store_probe copy [bytes]   (device copy ceiling instead)
 // Each variant writes H bytes of every slot i at i * stride (H <= stride):
 //   flat16   lanes cover the slots' bytes as one flat run of 16-B chunks
 //            (full chunks whole, edge chunks cut), consecutive lanes ->
@@ -70,7 +71,195 @@ __global__ void k_flat16(uint8_t* d, uint64_t n, uint32_t stride, uint32_t H) {
     store_piece(d + i * stride + 16 * c, u32x4{(uint32_t)i, c, 2u, 3u}, 0, t1);
 }
 
+// one 16-B block per lane per step, U steps' loads in flight before the stores
+template <int U>
+__global__ void k_copy(const uint8_t* s, uint8_t* d, uint64_t nblk) {
+    const uint64_t i0 = ((uint64_t)blockIdx.x * U) * blockDim.x + threadIdx.x;
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t i = i0 + (uint64_t)u * blockDim.x;
+        if (i < nblk) v[u] = *(const __attribute__((address_space(1))) u32x4*)(s + 16 * i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t i = i0 + (uint64_t)u * blockDim.x;
+        if (i < nblk) *G(d + 16 * i) = v[u];
+    }
+}
+
+// each wave copies a contiguous run of `per_wave` 16-B blocks, 64 per step, U
+// steps' loads before their stores (the emit walk's shape without its math);
+// dynamic LDS only limits how many waves share a CU
+template <int U>
+__global__ void k_copy_walk(const uint8_t* s, uint8_t* d, uint64_t nblk, uint32_t per_wave) {
+    extern __shared__ uint8_t lds_pad[];
+    const uint32_t lane = threadIdx.x % 64;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;
+    const uint64_t b0 = wave * per_wave;
+    if (threadIdx.x == 1u << 20) lds_pad[0] = 0;
+    for (uint32_t k0 = 0; k0 < per_wave; k0 += 64 * U) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = b0 + k0 + u * 64 + lane;
+            if (k0 + u * 64 + lane < per_wave && i < nblk)
+                v[u] = *(const __attribute__((address_space(1))) u32x4*)(s + 16 * i);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = b0 + k0 + u * 64 + lane;
+            if (k0 + u * 64 + lane < per_wave && i < nblk) *G(d + 16 * i) = v[u];
+        }
+    }
+}
+
+// windows of 64 * U consecutive blocks; window w is taken by wave w % nwaves
+// in its (w / nwaves)-th iteration, so the waves in flight at any time work
+// on neighbouring windows (persistent waves, grid-interleaved windows)
+template <int U>
+__global__ void k_copy_interleaved(const uint8_t* s, uint8_t* d, uint64_t nblk) {
+    extern __shared__ uint8_t lds_pad[];
+    const uint32_t lane = threadIdx.x % 64;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;
+    const uint64_t nwaves = (uint64_t)gridDim.x * blockDim.x / 64;
+    if (threadIdx.x == 1u << 20) lds_pad[0] = 0;
+    for (uint64_t w = wave; w * 64 * U < nblk; w += nwaves) {
+        u32x4 v[U];
+        const uint64_t b0 = w * 64 * U + lane;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (b0 + u * 64 < nblk) v[u] = *(const __attribute__((address_space(1))) u32x4*)(s + 16 * (b0 + u * 64));
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (b0 + u * 64 < nblk) *G(d + 16 * (b0 + u * 64)) = v[u];
+    }
+}
+
+// the persistent interleaved loop as a two-stage pipeline: window t + 1's
+// loads go out before window t's stores, every load and store unconditional
+// (indices clamped), so the compiler's vmcnt waits never cover the stores
+template <int U>
+__global__ void k_copy_pipe(const uint8_t* s, uint8_t* d, uint64_t nblk) {
+    extern __shared__ uint8_t lds_pad[];
+    const uint32_t lane = threadIdx.x % 64;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;
+    const uint64_t nwaves = (uint64_t)gridDim.x * blockDim.x / 64;
+    if (threadIdx.x == 1u << 20) lds_pad[0] = 0;
+    const uint64_t nwin = nblk / (64 * U);  // whole windows only (the probe's sizes)
+    auto ld = [&](uint64_t w, u32x4* v) {
+        const uint64_t b0 = (w < nwin ? w : 0) * 64 * U + lane;
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = *(const __attribute__((address_space(1))) u32x4*)(s + 16 * (b0 + u * 64));
+    };
+    auto st = [&](uint64_t w, const u32x4* v) {
+        const uint64_t b0 = w * 64 * U + lane;
+#pragma unroll
+        for (int u = 0; u < U; ++u) *G(d + 16 * (b0 + u * 64)) = v[u];
+    };
+    u32x4 a[U], b[U];
+    uint64_t w = wave;
+    if (w >= nwin) return;
+    ld(w, a);
+    while (true) {
+        ld(w + nwaves, b);
+        st(w, a);
+        w += nwaves;
+        if (w >= nwin) break;
+        ld(w + nwaves, a);
+        st(w, b);
+        w += nwaves;
+        if (w >= nwin) break;
+    }
+}
+
+// a workgroup of W waves shares one contiguous run of `per_group` 16-B blocks
+// (the emit walk's 64 packets), wave w taking steps w, w + W, ... of 64 * U
+template <int U>
+__global__ void k_copy_group(const uint8_t* s, uint8_t* d, uint64_t nblk, uint32_t per_group) {
+    extern __shared__ uint8_t lds_pad[];
+    const uint32_t lane = threadIdx.x % 64, w = threadIdx.x / 64, W = blockDim.x / 64;
+    const uint64_t b0 = (uint64_t)blockIdx.x * per_group;
+    if (threadIdx.x == 1u << 20) lds_pad[0] = 0;
+    for (uint32_t k0 = w * 64 * U; k0 < per_group; k0 += W * 64 * U) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = b0 + k0 + u * 64 + lane;
+            if (k0 + u * 64 + lane < per_group && i < nblk)
+                v[u] = *(const __attribute__((address_space(1))) u32x4*)(s + 16 * i);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = b0 + k0 + u * 64 + lane;
+            if (k0 + u * 64 + lane < per_group && i < nblk) *G(d + 16 * i) = v[u];
+        }
+    }
+}
+
+static int copy_ceiling(uint64_t bytes) {
+    uint8_t *s, *d;
+    if (hipMalloc(&s, bytes) != hipSuccess || hipMalloc(&d, bytes) != hipSuccess) return 1;
+    hipMemset(s, 1, bytes);
+    const uint64_t nblk = bytes / 16;
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    auto timeit = [&](const char* name, auto launch) {
+        launch();
+        hipDeviceSynchronize();
+        float best = 1e30f;
+        for (int r = 0; r < 3; ++r) {
+            hipEventRecord(e0, 0);
+            for (int k = 0; k < 5; ++k) launch();
+            hipEventRecord(e1, 0);
+            hipEventSynchronize(e1);
+            float ms;
+            hipEventElapsedTime(&ms, e0, e1);
+            best = ms / 5 < best ? ms / 5 : best;
+        }
+        printf("{\"variant\": \"%s\", \"bytes\": %llu, \"us\": %.1f, \"rw_GB_s\": %.1f, \"err\": %d}\n",
+               name, (unsigned long long)bytes, best * 1e3, 2.0 * bytes / best / 1e6,
+               (int)hipGetLastError());
+        fflush(stdout);
+    };
+    timeit("copy_u1_b256", [&] { k_copy<1><<<(nblk + 255) / 256, 256>>>(s, d, nblk); });
+    timeit("copy_u4_b256", [&] { k_copy<4><<<(nblk + 1023) / 1024, 256>>>(s, d, nblk); });
+    timeit("copy_u8_b256", [&] { k_copy<8><<<(nblk + 2047) / 2048, 256>>>(s, d, nblk); });
+    timeit("copy_u4_b128", [&] { k_copy<4><<<(nblk + 511) / 512, 128>>>(s, d, nblk); });
+    const uint32_t pw = 3424;  // the emit wave's chunks (C6e: 64 packets, ~856 B each)
+    const uint64_t waves = (nblk + pw - 1) / pw, blocks = (waves + 1) / 2;
+    timeit("walk_u4_lds20k", [&] { k_copy_walk<4><<<blocks, 128, 20 * 1024>>>(s, d, nblk, pw); });
+    timeit("walk_u4_lds0", [&] { k_copy_walk<4><<<blocks, 128, 0>>>(s, d, nblk, pw); });
+    timeit("walk_u1_lds0", [&] { k_copy_walk<1><<<blocks, 128, 0>>>(s, d, nblk, pw); });
+    timeit("walk_u8_lds0", [&] { k_copy_walk<8><<<blocks, 128, 0>>>(s, d, nblk, pw); });
+    timeit("walk_u4_lds10k", [&] { k_copy_walk<4><<<blocks, 128, 10 * 1024>>>(s, d, nblk, pw); });
+    timeit("win_u4_oneshot", [&] { k_copy_interleaved<4><<<(nblk + 511) / 512, 128, 0>>>(s, d, nblk); });
+    timeit("win_u1_oneshot", [&] { k_copy_interleaved<1><<<(nblk + 127) / 128, 128, 0>>>(s, d, nblk); });
+    timeit("persist_u4_4096w_lds20k", [&] { k_copy_interleaved<4><<<2048, 128, 20 * 1024>>>(s, d, nblk); });
+    timeit("persist_u4_8192w", [&] { k_copy_interleaved<4><<<4096, 128, 0>>>(s, d, nblk); });
+    timeit("persist_u2_4096w_lds20k", [&] { k_copy_interleaved<2><<<2048, 128, 20 * 1024>>>(s, d, nblk); });
+    timeit("persist_u1_4096w_lds20k", [&] { k_copy_interleaved<1><<<2048, 128, 20 * 1024>>>(s, d, nblk); });
+    timeit("pipe_u4_4096w_lds20k", [&] { k_copy_pipe<4><<<2048, 128, 20 * 1024>>>(s, d, nblk); });
+    timeit("pipe_u2_4096w_lds20k", [&] { k_copy_pipe<2><<<2048, 128, 20 * 1024>>>(s, d, nblk); });
+    timeit("pipe_u4_8192w", [&] { k_copy_pipe<4><<<4096, 128, 0>>>(s, d, nblk); });
+    {
+        const uint64_t groups = (nblk + pw - 1) / pw;
+        timeit("group_w4_u4_lds12k", [&] { k_copy_group<4><<<groups, 256, 12 * 1024>>>(s, d, nblk, pw); });
+        timeit("group_w8_u4_lds12k", [&] { k_copy_group<4><<<groups, 512, 12 * 1024>>>(s, d, nblk, pw); });
+        timeit("group_w8_u2_lds12k", [&] { k_copy_group<2><<<groups, 512, 12 * 1024>>>(s, d, nblk, pw); });
+        timeit("group_w16_u2_lds12k", [&] { k_copy_group<2><<<groups, 1024, 12 * 1024>>>(s, d, nblk, pw); });
+        timeit("group_w16_u1_lds12k", [&] { k_copy_group<1><<<groups, 1024, 12 * 1024>>>(s, d, nblk, pw); });
+    }
+    timeit("hipMemcpyDtoD", [&] { hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToDevice, 0); });
+    hipFree(s);
+    hipFree(d);
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && argv[1][0] == 'c')
+        return copy_ceiling(argc > 2 ? strtoull(argv[2], 0, 10) : 6561093376ull);
     const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : (1ull << 23);
     const uint32_t H = 74;
     const uint32_t strides[] = {74, 80, 96, 128, 256};
