@@ -8,23 +8,21 @@
 // (bitfield.rs:188-315: the field's covering bytes read-modify-written
 // big-endian) — OPTE's outbound Geneve encapsulation.
 //
-// The header block sits in LDS once per workgroup.  A wave owns 64 packets:
-// lane j loads packet j's descriptors and per-packet set values (coalesced),
-// then the wave's groups of G lanes walk the packets (G = 64 for whole
-// packets, 16 for header blocks: 4 packets at a time).  A group covers the
-// packet's destination span [D, D + T) in aligned 16-B chunks, G per pass;
-// each lane builds its chunk from
-//   * the header bytes: two template blocks from LDS funnel-shifted by the
-//     destination's misalignment, then the setters' bytes that fall in the
-//     chunk (every covering byte's new value depends only on its own mask
-//     and value bits, so a field split over two chunks needs no exchange);
-//   * the payload bytes: one aligned 16-B source block per lane plus the
-//     neighbouring lane's block, funnel-shifted by the packet's uniform
-//     source-vs-destination misalignment;
-// and stores it: a whole chunk as one aligned 16-B store, the two edge chunks
-// byte by byte (packed packets share them).
-// HBM-bound copy: algorithmic bytes per packet = len + 18 B of descriptors
-// read, hdr_len + len written.
+// The header block sits in LDS once per workgroup.  A group of 64 packets:
+// lane j of the group's first wave loads packet j's descriptors and set
+// values (coalesced) and patches the header block for it into an LDS region
+// at its destination's 16-B alignment (template funnel-shifted, then the
+// setters byte by byte: every covering byte's new value depends only on its
+// own mask and value bits); a scan of the packets' chunk counts turns the
+// group into one flat run of aligned 16-B destination chunks, which the
+// group's W waves take in turns, 64 chunks per step.  A lane's chunk: its
+// packet by binary search of the scan; the payload bytes as one aligned
+// 16-B source block plus the next lane's (DPP), funnel-shifted by the
+// packet's source-vs-destination misalignment; the header bytes from the
+// region; a whole chunk leaves as one 16-B store, the two edge chunks a
+// packet shares with its neighbours as predicated pieces (store_edge).
+// HBM-bound copy: algorithmic bytes per packet = len + 24 B of descriptors
+// and set values read, hdr_len + len written.
 #include <hip/hip_runtime.h>
 
 #include "../../include/ingot_gpu.h"
@@ -33,8 +31,21 @@
 namespace ingot_gpu {
 namespace {
 
-constexpr uint32_t BLOCK = 128;  // two waves: <= 40 KiB of LDS at the largest header block
 constexpr uint32_t WAVE = 64;
+#ifndef INGOT_EMIT_GROUP_WAVES
+#define INGOT_EMIT_GROUP_WAVES 4
+#endif
+// Whole packets: the W waves of a workgroup share one group of 64 packets and
+// take turns over its chunks, so a group's span is written by W waves at once
+// and the spans in flight sit closer together (a plain copy of this shape:
+// 4.87 TB/s one wave per span, 5.40 four; the emit kernel 2.91 -> 2.78 ms at
+// W = 4, W = 2 / 6 / 8 / 16 slower; profiles/r05_emit_probe_history.json).
+// Header blocks: two one-wave groups.
+template <bool COPY> struct Shape {
+    static constexpr uint32_t W = COPY ? INGOT_EMIT_GROUP_WAVES : 1u;  // waves per group
+    static constexpr uint32_t BLOCK = COPY ? W * WAVE : 2u * WAVE;
+    static constexpr uint32_t G = BLOCK / (W * WAVE);                 // groups per block
+};
 #ifndef INGOT_EMIT_UNROLL
 #define INGOT_EMIT_UNROLL 4
 #endif
@@ -93,7 +104,9 @@ struct WaveDesc {
     uint32_t pfx[WAVE];   // inclusive prefix of chunk counts
     uint32_t len[WAVE];   // payload bytes
     uint32_t mis[WAVE];   // dmis | s_mis << 8
-    uint32_t _pad[WAVE];
+    uint32_t total;       // chunks of the group's walk
+    uint32_t cp, cp_inv;  // header blocks: chunk slots per packet, its reciprocal
+    uint32_t _pad[WAVE - 3];
 };
 
 __host__ __device__ constexpr uint32_t region_bytes(uint32_t H) { return (H + 15u + 15u) / 16u * 16u; }
@@ -140,7 +153,8 @@ __device__ __forceinline__ void store_edge(uint8_t* p, const u32x4& v, int32_t t
 }
 
 template <bool COPY>
-__global__ __launch_bounds__(BLOCK) void k_emit(EmitArgs a) {
+__global__ __launch_bounds__(Shape<COPY>::BLOCK) void k_emit(EmitArgs a) {
+    constexpr uint32_t BLOCK = Shape<COPY>::BLOCK, W = Shape<COPY>::W, G = Shape<COPY>::G;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     // the header block between zero bytes, as 16-B blocks
     u32x4* tmpl = reinterpret_cast<u32x4*>(smem);
@@ -153,83 +167,88 @@ __global__ __launch_bounds__(BLOCK) void k_emit(EmitArgs a) {
     }
     const uint32_t H = a.hdr_len;
     const uint32_t RS = region_bytes(H);
-    const uint32_t lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
-    WaveDesc& wd = reinterpret_cast<WaveDesc*>(smem + TB * 16)[w];
-    uint8_t* regions = smem + TB * 16 + (BLOCK / WAVE) * sizeof(WaveDesc) + w * WAVE * RS;
+    const uint32_t lane = threadIdx.x % WAVE, g = threadIdx.x / (W * WAVE);
+    const uint32_t wg = (threadIdx.x / WAVE) % W;  // this wave's turn in its group
+    WaveDesc& wd = reinterpret_cast<WaveDesc*>(smem + TB * 16)[g];
+    uint8_t* regions = smem + TB * 16 + G * sizeof(WaveDesc) + g * WAVE * RS;
     __syncthreads();
-    const uint64_t base = ((uint64_t)blockIdx.x * (BLOCK / WAVE) + w) * WAVE;
-    if (base >= a.n) return;
-
-    // 1. lane j: packet base + j (coalesced descriptor and set-value loads)
-    const uint64_t i = base + lane;
-    const bool live = i < a.n;
-    const uint32_t L = live ? (uint32_t)gbl(a.len)[i] : 0u;
-    const uint64_t doff = live ? (a.dst_off ? gbl(a.dst_off)[i] : i * (uint64_t)a.stride) : 0u;
-    const uint64_t soff = (COPY && live) ? gbl(a.off)[i] : 0u;
-    uint32_t v[INGOT_MAX_EMIT_SETS];
+    const uint64_t base = ((uint64_t)blockIdx.x * G + g) * WAVE;
+    if (wg == 0) {
+        // 1. lane j: packet base + j (coalesced descriptor and set-value loads)
+        const uint64_t i = base + lane;
+        const bool live = i < a.n;
+        const uint32_t L = live ? (uint32_t)gbl(a.len)[i] : 0u;
+        const uint64_t doff = live ? (a.dst_off ? gbl(a.dst_off)[i] : i * (uint64_t)a.stride) : 0u;
+        const uint64_t soff = (COPY && live) ? gbl(a.off)[i] : 0u;
+        uint32_t v[INGOT_MAX_EMIT_SETS];
 #pragma unroll
-    for (uint32_t s = 0; s < INGOT_MAX_EMIT_SETS; ++s)
-        v[s] = (s < a.n_sets && live) ? set_value(a.sets[s], i, H + L) : 0u;
-    uint8_t* D = a.dst + doff;
-    const uint8_t* S = COPY ? a.src + soff : nullptr;
-    const uint32_t T = H + (COPY ? L : 0u);
-    const uint32_t dmis = (uint32_t)((uintptr_t)D & 15u);
-    const uint32_t s_mis = COPY ? (uint32_t)((uintptr_t)(S - H - dmis) & 15u) : 0u;
-    const uint32_t nch = live ? (dmis + T + 15u) / 16u : 0u;
+        for (uint32_t s = 0; s < INGOT_MAX_EMIT_SETS; ++s)
+            v[s] = (s < a.n_sets && live) ? set_value(a.sets[s], i, H + L) : 0u;
+        uint8_t* D = a.dst + doff;
+        const uint8_t* S = COPY ? a.src + soff : nullptr;
+        const uint32_t T = H + (COPY ? L : 0u);
+        const uint32_t dmis = (uint32_t)((uintptr_t)D & 15u);
+        const uint32_t s_mis = COPY ? (uint32_t)((uintptr_t)(S - H - dmis) & 15u) : 0u;
+        const uint32_t nch = live ? (dmis + T + 15u) / 16u : 0u;
 
-    // 2. the packet's header block in its region: template bytes shifted to
-    //    the destination's alignment (region byte b = header byte b - dmis),
-    //    then the setters byte by byte (neighbouring bits kept)
-    uint8_t* R = regions + lane * RS;
-    if (H && live) {
-        for (uint32_t m = 0; m < RS / 16u; ++m) {
-            const uint32_t tb = 16u + 16u * m - dmis;  // template byte of region byte 16m (+16)
-            reinterpret_cast<u32x4*>(R)[m] = funnel(tmpl[tb >> 4], tmpl[(tb >> 4) + 1], tb & 15u);
-        }
+        // 2. the packet's header block in its region: template bytes shifted to
+        //    the destination's alignment (region byte b = header byte b - dmis),
+        //    then the setters byte by byte (neighbouring bits kept)
+        uint8_t* R = regions + lane * RS;
+        if (H && live) {
+            for (uint32_t m = 0; m < RS / 16u; ++m) {
+                const uint32_t tb = 16u + 16u * m - dmis;  // template byte of region byte 16m (+16)
+                reinterpret_cast<u32x4*>(R)[m] = funnel(tmpl[tb >> 4], tmpl[(tb >> 4) + 1], tb & 15u);
+            }
 #pragma unroll
-        for (uint32_t s = 0; s < INGOT_MAX_EMIT_SETS; ++s) {
-            if (s >= a.n_sets) break;
-            const EmitSet& e = a.sets[s];
-            const uint32_t fm = e.bits >= 32 ? 0xffffffffu : ((1u << e.bits) - 1u);
-            const uint32_t m = fm << e.rshift, vb = (v[s] & fm) << e.rshift;
-            for (uint32_t k = 0; k < e.nbytes; ++k) {
-                const uint32_t shb = 8u * (e.nbytes - 1u - k);
-                uint8_t& b = R[dmis + e.pos + k];
-                b = (uint8_t)((b & ~(m >> shb)) | ((vb >> shb) & (m >> shb)));
+            for (uint32_t s = 0; s < INGOT_MAX_EMIT_SETS; ++s) {
+                if (s >= a.n_sets) break;
+                const EmitSet& e = a.sets[s];
+                const uint32_t fm = e.bits >= 32 ? 0xffffffffu : ((1u << e.bits) - 1u);
+                const uint32_t m = fm << e.rshift, vb = (v[s] & fm) << e.rshift;
+                for (uint32_t k = 0; k < e.nbytes; ++k) {
+                    const uint32_t shb = 8u * (e.nbytes - 1u - k);
+                    uint8_t& b = R[dmis + e.pos + k];
+                    b = (uint8_t)((b & ~(m >> shb)) | ((vb >> shb) & (m >> shb)));
+                }
             }
         }
-    }
 
-    // 3. chunk counts -> inclusive prefix over the wave
-    uint32_t P = nch;
+        // 3. chunk counts -> inclusive prefix over the wave
+        uint32_t P = nch;
 #pragma unroll
-    for (uint32_t o = 1; o < WAVE; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)P, o);
-        if (lane >= o) P += y;
-    }
-    wd.dst[lane] = (uint64_t)(uintptr_t)D;
-    wd.src[lane] = (uint64_t)(uintptr_t)S;
-    wd.pfx[lane] = P;
-    wd.len[lane] = L;
-    wd.mis[lane] = dmis | (s_mis << 8);
-    // header blocks: every packet takes CP chunk slots, the most any packet
-    // of this wave needs (5 for 74 B at 16-B aligned slots, 6 unaligned)
-    uint32_t CP = nch;
+        for (uint32_t o = 1; o < WAVE; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)P, o);
+            if (lane >= o) P += y;
+        }
+        wd.dst[lane] = (uint64_t)(uintptr_t)D;
+        wd.src[lane] = (uint64_t)(uintptr_t)S;
+        wd.pfx[lane] = P;
+        wd.len[lane] = L;
+        wd.mis[lane] = dmis | (s_mis << 8);
+        // header blocks: every packet takes CP chunk slots, the most any packet
+        // of this wave needs (5 for 74 B at 16-B aligned slots, 6 unaligned)
+        uint32_t CP = nch;
 #pragma unroll
-    for (uint32_t o = 1; o < WAVE; o <<= 1) CP = max(CP, (uint32_t)__shfl_xor((int)CP, (int)o));
-    CP = max(CP, 1u);
-    const uint32_t cp_inv = CP > 1u ? 0xffffffffu / CP + 1u : 0u;  // CP == 1: q = k
-    const uint32_t total =
-        COPY ? (uint32_t)__shfl((int)P, (int)WAVE - 1) : (uint32_t)min<uint64_t>(WAVE, a.n - base) * CP;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t o = 1; o < WAVE; o <<= 1) CP = max(CP, (uint32_t)__shfl_xor((int)CP, (int)o));
+        CP = max(CP, 1u);
+        const uint32_t cp_inv = CP > 1u ? 0xffffffffu / CP + 1u : 0u;  // CP == 1: q = k
+        const uint32_t wtotal = COPY ? (uint32_t)__shfl((int)P, (int)WAVE - 1)
+                                     : (base < a.n ? (uint32_t)min<uint64_t>(WAVE, a.n - base) * CP : 0u);
+        if (lane == 0) {
+            wd.total = wtotal;
+            wd.cp = CP;
+            wd.cp_inv = cp_inv;
+        }
+    }  // wg == 0
+    __syncthreads();
+    const uint32_t total = wd.total, CP = wd.cp, cp_inv = wd.cp_inv;
 
     // 4. the wave's chunks, 64 per step and UNROLL steps at a time (all their
     //    loads are issued before the first store: bytes in flight): chunk k
     //    belongs to the first packet whose inclusive prefix exceeds k
     constexpr uint32_t U = COPY ? UNROLL : 2u;  // header blocks: no loads to overlap
-    for (uint32_t k0 = 0; k0 < total; k0 += WAVE * U) {
+    for (uint32_t k0 = wg * WAVE * U; k0 < total; k0 += W * WAVE * U) {
         uint32_t q[U], c[U];
         u32x4 own[U], nb[U];
         bool extra[U];
@@ -316,12 +335,13 @@ __global__ __launch_bounds__(BLOCK) void k_emit(EmitArgs a) {
 
 template <bool COPY>
 hipError_t go(const EmitArgs& a, hipStream_t s) {
-    const uint64_t waves = (a.n + WAVE - 1) / WAVE;
-    const uint64_t blocks = (waves + BLOCK / WAVE - 1) / (BLOCK / WAVE);
+    constexpr uint32_t G = Shape<COPY>::G;
+    const uint64_t groups = (a.n + WAVE - 1) / WAVE;
+    const uint64_t blocks = (groups + G - 1) / G;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
     const size_t smem = (INGOT_MAX_EMIT_HDR / 16 + 4) * 16 +
-                        (BLOCK / WAVE) * (sizeof(WaveDesc) + WAVE * region_bytes(a.hdr_len));
-    hipLaunchKernelGGL((k_emit<COPY>), dim3((uint32_t)blocks), dim3(BLOCK), smem, s, a);
+                        G * (sizeof(WaveDesc) + WAVE * region_bytes(a.hdr_len));
+    hipLaunchKernelGGL((k_emit<COPY>), dim3((uint32_t)blocks), dim3(Shape<COPY>::BLOCK), smem, s, a);
     return hipGetLastError();
 }
 
