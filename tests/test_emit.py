@@ -209,6 +209,32 @@ def test_emit_jumbo_and_empty_payloads(ctx, torch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 63, 65, 257])
+def test_emit_partial_groups_and_max_payload(ctx, torch, n):
+    """Batches that leave the last 64-packet group partial (a workgroup's four
+    waves then share fewer packets than lanes) and payloads up to the u16
+    maximum (65,535 B: one packet's span alone is 4,100 chunks)."""
+    rng = np.random.default_rng(100 + n)
+    ln = rng.integers(0, 2000, n).astype(np.uint16)
+    ln[rng.integers(0, n, max(1, n // 8))] = 65535
+    src_off = np.cumsum(np.r_[0, ln[:-1].astype(np.int64) + rng.integers(0, 20, n - 1)]) + 1
+    src = rng.integers(0, 256, int(src_off[-1] + ln[-1] + 64), dtype=np.uint8)
+    hdr = _opte_stack()
+    sets = [(14, Field.V6_PAYLOAD_LEN, EmitSource.LENGTH, -40),
+            (54, Field.UDP_LENGTH, EmitSource.LENGTH, 0)]
+    tot = len(hdr) + ln.astype(np.int64)
+    dst_off = np.cumsum(np.r_[0, tot[:-1] + rng.integers(0, 9, n - 1)]) + 7
+    fill = rng.integers(0, 256, int(dst_off[-1] + tot[-1] + 32), dtype=np.uint8)
+    dst = _dev(torch, fill)
+    ctx.emit_packets(hdr, sets, _dev(torch, src), _u64(torch, src_off), _u16(torch, ln), dst,
+                     _u64(torch, dst_off))
+    want = fill.copy()
+    oracle.emit_batch(hdr, sets, src, src_off, ln, want, dst_off)
+    bad = np.nonzero(dst.cpu().numpy() != want)[0]
+    assert bad.size == 0, (n, bad[:10])
+
+
+@pytest.mark.gpu
 def test_emit_gather_copy_without_headers(ctx, torch):
     """hdr_len 0: a gather copy (decapsulation: each tunnel frame's inner
     frame copied out from the offset the parse found)."""
