@@ -38,6 +38,9 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--hdr-strides", default="",
                     help="also time header blocks into slots of these strides (comma list)")
+    ap.add_argument("--hdr-pad", type=int, default=0,
+                    help="header blocks: also time the block zero-padded by this many bytes "
+                         "(a slot whose padding is the caller's to overwrite)")
     ap.add_argument("--only", default="", help="time only these runs (comma list)")
     ap.add_argument("--lib", default=None, help="tools/variants/<name>/libingot_gpu.so instead")
     args = ap.parse_args()
@@ -82,6 +85,13 @@ def main():
         "copy": lambda: copy_dst.copy_(arena[:payload]),
     }
     algo = {"packets": payload + 24 * n + total, "headers": 8 * n + H * n, "copy": 2 * payload}
+    if args.hdr_pad:
+        hp = hdr + bytes(args.hdr_pad)
+        stp = (len(hp) + 15) // 16 * 16
+        slp = torch.empty(n * stp + 64, dtype=torch.uint8, device="cuda")
+        runs[f"headers_padded{len(hp)}_stride{stp}"] = (
+            lambda: ctx.emit_header_blocks(hp, sets, lens, slp, stride=stp))
+        algo[f"headers_padded{len(hp)}_stride{stp}"] = 8 * n + H * n
     for st in [int(x) for x in args.hdr_strides.split(",") if x]:
         sl = torch.empty(n * st + 64, dtype=torch.uint8, device="cuda")
         runs[f"headers_stride{st}"] = (lambda sl=sl, st=st:
