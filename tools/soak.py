@@ -3,7 +3,7 @@
 launches of the ring kernel (C2 slots, 2 streams), the flow kernels
 (persistent grid with full hashes; one tile per wave with the 16-bit table,
 2 streams), parse_read over the reference bench's one-chunk-per-header
-shape (2 streams) and the packed-layout parse, each output compared on the
+shape (2 streams), the packed-layout parse and the batched emit (2 streams), each output compared on the
 device with the first run's over the same arena (which the parity tests pin
 to the oracle) — an intermittent race in LDS-image reuse or the persistent
 grids would show up as a mismatch.  Writes gpurun_out/soak.json.
@@ -119,6 +119,31 @@ def main():
         bad += int(not torch.equal(got, want))
     torch.cuda.synchronize()
     res["packed_layout"] = {"launches": args.iters // 10, "mismatching_launches": bad}
+
+    # batched emit (four waves sharing each 64-packet group's walk through
+    # LDS), steps over 2 streams, every packet at a fresh misalignment
+    import numpy as np
+    hdr, sets = bench.emit_stack()
+    ports, vnis = bench.emit_values(m)
+    dsets = [sets[0], sets[1], (*sets[2], torch.from_numpy(ports.view(np.int16)).cuda()),
+             (*sets[3], torch.from_numpy(vnis.view(np.int32)).cuda())]
+    tot = lens.to(torch.int64) + len(hdr) + 3
+    d_off = torch.cumsum(tot, 0) - tot
+    size = int(tot.sum().item()) + 64
+    e0 = torch.zeros(size, dtype=torch.uint8, device="cuda")
+    ctx.emit_packets(hdr, dsets, arena, off, lens, e0, d_off)
+    torch.cuda.synchronize()
+    eouts = [torch.zeros(size, dtype=torch.uint8, device="cuda") for _ in range(4)]
+    acc = [torch.zeros((), dtype=torch.int64, device="cuda") for _ in s]
+    for it in range(args.iters // 5):
+        k, st = it % 4, s[it % 2]
+        ctx.emit_packets(hdr, dsets, arena, off, lens, eouts[k], d_off, stream=st)
+        with torch.cuda.stream(st):
+            acc[it % 2] += (eouts[k] != e0).any().to(torch.int64)
+    torch.cuda.synchronize()
+    res["emit_packets"] = {"launches": args.iters // 5,
+                           "mismatching_launches": int(sum(a.item() for a in acc))}
+    del eouts, e0
 
     out = {"wall_s": round(time.time() - t0, 1), "checks": res,
            "all_zero": all(v["mismatching_launches"] == 0 for v in res.values())}
