@@ -8,14 +8,15 @@
 // (bitfield.rs:188-315: the field's covering bytes read-modify-written
 // big-endian) — OPTE's outbound Geneve encapsulation.
 //
-// The header block sits in LDS once per workgroup.  A group of 64 packets:
-// lane j of the group's first wave loads packet j's descriptors and set
-// values (coalesced) and patches the header block for it into an LDS region
+// The header block sits in LDS once per workgroup.  A group of 4 x 64
+// packets: lane j of the group's wave w < 4 loads packet 64 w + j's
+// descriptors and set values (coalesced) and patches the header block for it
+// into an LDS region
 // at its destination's 16-B alignment (template funnel-shifted, then the
 // setters byte by byte: every covering byte's new value depends only on its
 // own mask and value bits); a scan of the packets' chunk counts turns the
 // group into one flat run of aligned 16-B destination chunks, which the
-// group's W waves take in turns, 64 chunks per step.  A lane's chunk: its
+// group's 16 waves take in turns, 64 chunks per step.  A lane's chunk: its
 // packet by binary search of the scan; the payload bytes as one aligned
 // 16-B source block plus the next lane's (DPP), funnel-shifted by the
 // packet's source-vs-destination misalignment; the header bytes from the
@@ -33,18 +34,28 @@ namespace {
 
 constexpr uint32_t WAVE = 64;
 #ifndef INGOT_EMIT_GROUP_WAVES
-#define INGOT_EMIT_GROUP_WAVES 4
+#define INGOT_EMIT_GROUP_WAVES 16
 #endif
-// Whole packets: the W waves of a workgroup share one group of 64 packets and
+// Whole packets: the W waves of a workgroup share one group of packets and
 // take turns over its chunks, so a group's span is written by W waves at once
 // and the spans in flight sit closer together (a plain copy of this shape:
-// 4.87 TB/s one wave per span, 5.40 four; the emit kernel 2.91 -> 2.78 ms at
-// W = 4, W = 2 / 6 / 8 / 16 slower; profiles/r05_emit_probe_history.json).
+// 4.87 TB/s one wave per span, 5.40 four).  A group is PW subgroups of 64
+// packets whose descriptors PW waves load and patch in parallel, so the
+// walkers wait on one subgroup's prologue, not PW of them.  Measured with
+// equal output checksums (profiles/r05_emit_probe_history.json, r05aj /
+// r05am): one wave per 64 packets 2.91 ms, W = 4 2.78-2.81, W = 16 over four
+// subgroups 2.65-2.77 (the best of W / PW in {4, 6, 8, 10, 12, 16} x {1..4}).
 // Header blocks: two one-wave groups.
+#ifndef INGOT_EMIT_GROUP_SUBS
+#define INGOT_EMIT_GROUP_SUBS 4
+#endif
 template <bool COPY> struct Shape {
     static constexpr uint32_t W = COPY ? INGOT_EMIT_GROUP_WAVES : 1u;  // waves per group
+    static constexpr uint32_t PW = COPY ? INGOT_EMIT_GROUP_SUBS : 1u;  // 64-packet subgroups
+    static constexpr uint32_t NP = PW * WAVE;                          // packets per group
     static constexpr uint32_t BLOCK = COPY ? W * WAVE : 2u * WAVE;
     static constexpr uint32_t G = BLOCK / (W * WAVE);                 // groups per block
+    static_assert(PW <= W && PW <= 4, "one prologue wave per subgroup");
 };
 #ifndef INGOT_EMIT_UNROLL
 #define INGOT_EMIT_UNROLL 4
@@ -98,15 +109,16 @@ __device__ __forceinline__ uint32_t set_value(const EmitSet& e, uint64_t i, uint
 // Per-wave LDS: the 64 packets' descriptors, the inclusive prefix of their
 // chunk counts, and each packet's patched header block at its destination's
 // 16-B alignment (RS bytes per packet).
+template <uint32_t NP>
 struct WaveDesc {
-    uint64_t dst[WAVE];   // destination address of packet j
-    uint64_t src[WAVE];   // source address of its payload
-    uint32_t pfx[WAVE];   // inclusive prefix of chunk counts
-    uint32_t len[WAVE];   // payload bytes
-    uint32_t mis[WAVE];   // dmis | s_mis << 8
-    uint32_t total;       // chunks of the group's walk
+    uint64_t dst[NP];     // destination address of packet j
+    uint64_t src[NP];     // source address of its payload
+    uint32_t pfx[NP];     // inclusive prefix of chunk counts
+    uint32_t len[NP];     // payload bytes
+    uint32_t mis[NP];     // dmis | s_mis << 8
+    uint32_t sub[4];      // chunks of each 64-packet subgroup
     uint32_t cp, cp_inv;  // header blocks: chunk slots per packet, its reciprocal
-    uint32_t _pad[WAVE - 3];
+    uint32_t _pad[WAVE - 6];
 };
 
 __host__ __device__ constexpr uint32_t region_bytes(uint32_t H) { return (H + 15u + 15u) / 16u * 16u; }
@@ -155,6 +167,9 @@ __device__ __forceinline__ void store_edge(uint8_t* p, const u32x4& v, int32_t t
 template <bool COPY>
 __global__ __launch_bounds__(Shape<COPY>::BLOCK) void k_emit(EmitArgs a) {
     constexpr uint32_t BLOCK = Shape<COPY>::BLOCK, W = Shape<COPY>::W, G = Shape<COPY>::G;
+    constexpr uint32_t PW = Shape<COPY>::PW, NP = Shape<COPY>::NP;
+    constexpr uint32_t NPOW = NP <= 64 ? 64 : NP <= 128 ? 128 : 256;  // search span
+    using Desc = WaveDesc<NP>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     // the header block between zero bytes, as 16-B blocks
     u32x4* tmpl = reinterpret_cast<u32x4*>(smem);
@@ -169,13 +184,15 @@ __global__ __launch_bounds__(Shape<COPY>::BLOCK) void k_emit(EmitArgs a) {
     const uint32_t RS = region_bytes(H);
     const uint32_t lane = threadIdx.x % WAVE, g = threadIdx.x / (W * WAVE);
     const uint32_t wg = (threadIdx.x / WAVE) % W;  // this wave's turn in its group
-    WaveDesc& wd = reinterpret_cast<WaveDesc*>(smem + TB * 16)[g];
-    uint8_t* regions = smem + TB * 16 + G * sizeof(WaveDesc) + g * WAVE * RS;
+    Desc& wd = reinterpret_cast<Desc*>(smem + TB * 16)[g];
+    uint8_t* regions = smem + TB * 16 + G * sizeof(Desc) + g * NP * RS;
     __syncthreads();
-    const uint64_t base = ((uint64_t)blockIdx.x * G + g) * WAVE;
-    if (wg == 0) {
-        // 1. lane j: packet base + j (coalesced descriptor and set-value loads)
-        const uint64_t i = base + lane;
+    const uint64_t base = ((uint64_t)blockIdx.x * G + g) * NP;
+    if (wg < PW) {
+        // 1. wave wg of the group, lane j: packet base + 64 wg + j (coalesced
+        //    descriptor and set-value loads)
+        const uint32_t j = wg * WAVE + lane;  // the packet's index in the group
+        const uint64_t i = base + j;
         const bool live = i < a.n;
         const uint32_t L = live ? (uint32_t)gbl(a.len)[i] : 0u;
         const uint64_t doff = live ? (a.dst_off ? gbl(a.dst_off)[i] : i * (uint64_t)a.stride) : 0u;
@@ -194,7 +211,7 @@ __global__ __launch_bounds__(Shape<COPY>::BLOCK) void k_emit(EmitArgs a) {
         // 2. the packet's header block in its region: template bytes shifted to
         //    the destination's alignment (region byte b = header byte b - dmis),
         //    then the setters byte by byte (neighbouring bits kept)
-        uint8_t* R = regions + lane * RS;
+        uint8_t* R = regions + j * RS;
         if (H && live) {
             for (uint32_t m = 0; m < RS / 16u; ++m) {
                 const uint32_t tb = 16u + 16u * m - dmis;  // template byte of region byte 16m (+16)
@@ -221,11 +238,11 @@ __global__ __launch_bounds__(Shape<COPY>::BLOCK) void k_emit(EmitArgs a) {
             const uint32_t y = (uint32_t)__shfl_up((int)P, o);
             if (lane >= o) P += y;
         }
-        wd.dst[lane] = (uint64_t)(uintptr_t)D;
-        wd.src[lane] = (uint64_t)(uintptr_t)S;
-        wd.pfx[lane] = P;
-        wd.len[lane] = L;
-        wd.mis[lane] = dmis | (s_mis << 8);
+        wd.dst[j] = (uint64_t)(uintptr_t)D;
+        wd.src[j] = (uint64_t)(uintptr_t)S;
+        wd.pfx[j] = P;
+        wd.len[j] = L;
+        wd.mis[j] = dmis | (s_mis << 8);
         // header blocks: every packet takes CP chunk slots, the most any packet
         // of this wave needs (5 for 74 B at 16-B aligned slots, 6 unaligned)
         uint32_t CP = nch;
@@ -236,13 +253,25 @@ __global__ __launch_bounds__(Shape<COPY>::BLOCK) void k_emit(EmitArgs a) {
         const uint32_t wtotal = COPY ? (uint32_t)__shfl((int)P, (int)WAVE - 1)
                                      : (base < a.n ? (uint32_t)min<uint64_t>(WAVE, a.n - base) * CP : 0u);
         if (lane == 0) {
-            wd.total = wtotal;
+            wd.sub[wg] = wtotal;
             wd.cp = CP;
             wd.cp_inv = cp_inv;
         }
-    }  // wg == 0
+    }  // wg < PW
     __syncthreads();
-    const uint32_t total = wd.total, CP = wd.cp, cp_inv = wd.cp_inv;
+    if (PW > 1) {
+        // subgroups 1.. continue the prefix of the ones before them
+        if (wg > 0 && wg < PW) {
+            uint32_t before = 0;
+            for (uint32_t t = 0; t < wg; ++t) before += wd.sub[t];
+            wd.pfx[wg * WAVE + lane] += before;
+        }
+        __syncthreads();
+    }
+    uint32_t total = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < PW; ++t) total += wd.sub[t];
+    const uint32_t CP = wd.cp, cp_inv = wd.cp_inv;
 
     // 4. the wave's chunks, 64 per step and UNROLL steps at a time (all their
     //    loads are issued before the first store: bytes in flight): chunk k
@@ -259,8 +288,8 @@ __global__ __launch_bounds__(Shape<COPY>::BLOCK) void k_emit(EmitArgs a) {
             uint32_t qq = 0, end = 0;
             if (COPY) {
 #pragma unroll
-                for (uint32_t step = WAVE / 2; step; step >>= 1)
-                    if (wd.pfx[qq + step - 1] <= k) qq += step;
+                for (uint32_t step = NPOW / 2; step; step >>= 1)
+                    if ((NP == NPOW || qq + step <= NP) && wd.pfx[qq + step - 1] <= k) qq += step;
                 qq = valid ? qq : 0u;
                 end = wd.pfx[qq];
                 c[u] = valid ? k - (qq ? wd.pfx[qq - 1] : 0u) : 0xffffu;
@@ -335,12 +364,12 @@ __global__ __launch_bounds__(Shape<COPY>::BLOCK) void k_emit(EmitArgs a) {
 
 template <bool COPY>
 hipError_t go(const EmitArgs& a, hipStream_t s) {
-    constexpr uint32_t G = Shape<COPY>::G;
-    const uint64_t groups = (a.n + WAVE - 1) / WAVE;
+    constexpr uint32_t G = Shape<COPY>::G, NP = Shape<COPY>::NP;
+    const uint64_t groups = (a.n + NP - 1) / NP;
     const uint64_t blocks = (groups + G - 1) / G;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
     const size_t smem = (INGOT_MAX_EMIT_HDR / 16 + 4) * 16 +
-                        G * (sizeof(WaveDesc) + WAVE * region_bytes(a.hdr_len));
+                        G * (sizeof(WaveDesc<NP>) + NP * region_bytes(a.hdr_len));
     hipLaunchKernelGGL((k_emit<COPY>), dim3((uint32_t)blocks), dim3(Shape<COPY>::BLOCK), smem, s, a);
     return hipGetLastError();
 }

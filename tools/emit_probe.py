@@ -112,7 +112,16 @@ def main():
             e1.record(s)
             torch.cuda.synchronize()
             res[k].append(e0.elapsed_time(e1) * 1e3 / args.reps)
+    # position-weighted checksum of the emitted packets (variants must agree)
+    csum = None
+    if "packets" in runs:
+        csum, step = 0, 1 << 27
+        for a0 in range(0, total, step):
+            b0 = min(total, a0 + step)
+            w = torch.arange(a0, b0, device="cuda", dtype=torch.int64) % 65521 + 1
+            csum += int((dst[a0:b0].to(torch.int64) * w).sum().item())
     out = {"what": __doc__.split("\n\n")[0], "lib": args.lib or "in-tree", "frames": n,
+           "packets_checksum": csum,
            "hdr_len": H,
            "payload_bytes": payload, "emitted_bytes": total, "runs": {}}
     for k, v in res.items():
