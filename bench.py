@@ -1894,8 +1894,8 @@ def run_config(args, config, env):
                            mode="parse" if flows else mode, segs=segs)
         cpu["measured"] = "after the GPU run (device-generated sample copied back)"
     kname = {"modify": ", parse + setters",
-             "emit": " (ingot_gpu_emit_packets: a group of 64 packets as one flat run of 16-B "
-                     "destination chunks taken in turns by the workgroup's four waves, header "
+             "emit": " (ingot_gpu_emit_packets: a group of 256 packets as one flat run of 16-B "
+                     "destination chunks taken in turns by the workgroup's sixteen waves, header "
                      "blocks patched once per packet in LDS)",
              "read": ", LAYOUT_SEGMENTED (parse_read" +
                      (", chunk 0 per packet: ingot_gpu_parse_read_first" if read_first else "") +

@@ -211,9 +211,10 @@ def test_emit_jumbo_and_empty_payloads(ctx, torch):
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [1, 63, 65, 257])
 def test_emit_partial_groups_and_max_payload(ctx, torch, n):
-    """Batches that leave the last 64-packet group partial (a workgroup's four
-    waves then share fewer packets than lanes) and payloads up to the u16
-    maximum (65,535 B: one packet's span alone is 4,100 chunks)."""
+    """Batches that leave the last packet group partial (a workgroup's waves
+    then share fewer packets than they have lanes, some subgroups none) and
+    payloads up to the u16 maximum (65,535 B: one packet's span alone is
+    4,100 chunks)."""
     rng = np.random.default_rng(100 + n)
     ln = rng.integers(0, 2000, n).astype(np.uint16)
     ln[rng.integers(0, n, max(1, n // 8))] = 65535

@@ -120,7 +120,7 @@ def main():
     torch.cuda.synchronize()
     res["packed_layout"] = {"launches": args.iters // 10, "mismatching_launches": bad}
 
-    # batched emit (four waves sharing each 64-packet group's walk through
+    # batched emit (sixteen waves sharing each 256-packet group's walk through
     # LDS), steps over 2 streams, every packet at a fresh misalignment
     import numpy as np
     hdr, sets = bench.emit_stack()
