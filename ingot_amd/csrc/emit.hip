@@ -43,8 +43,9 @@ constexpr uint32_t WAVE = 64;
 // packets whose descriptors PW waves load and patch in parallel, so the
 // walkers wait on one subgroup's prologue, not PW of them.  Measured with
 // equal output checksums (profiles/r05_emit_probe_history.json, r05aj /
-// r05am): one wave per 64 packets 2.91 ms, W = 4 2.78-2.81, W = 16 over four
-// subgroups 2.65-2.77 (the best of W / PW in {4, 6, 8, 10, 12, 16} x {1..4}).
+// r05am / r05an): one wave per 64 packets 2.91 ms, W = 4 2.78-2.81, W = 16
+// over four subgroups 2.65-2.77 (the best of W in {4, 6, 8, 10, 12, 16} with
+// 1, 2, 3, 4, 8 or 16 subgroups).
 // Header blocks: two one-wave groups.
 #ifndef INGOT_EMIT_GROUP_SUBS
 #define INGOT_EMIT_GROUP_SUBS 4
