@@ -350,9 +350,24 @@ int ingot_gpu_ctx_device(const ingot_gpu_ctx* ctx);
  * d_out ...): the kernels then read only the header bytes they touch across
  * PCIe (LDS-DMA staging from host memory) instead of a whole-frame
  * hipMemcpy, and can write records straight into host memory.  Results are
- * identical to a device-resident arena.  ingot_gpu_host_unmap undoes a
- * registration made by ingot_gpu_host_map (a no-op for hipHostMalloc memory).
- * The caller keeps the bytes stable while a call that reads them runs.
+ * identical to a device-resident arena.
+ *
+ * Mappings are counted.  Every successful ingot_gpu_host_map is paired with
+ * one ingot_gpu_host_unmap(ctx, host) by the same context and the same
+ * `host` (INGOT_GPU_EINVAL if this context holds no mapping starting there).
+ * The library unregisters only what it registered itself: pageable ranges it
+ * page-locked, once the last mapping inside them is unmapped (by any context)
+ * or its context is destroyed.  Memory pinned by someone else (hipHostMalloc,
+ * the caller's own hipHostRegister) is never unregistered: unmapping it only
+ * forgets the mapping.  A range inside one registered by an earlier map
+ * shares that registration (e.g. a record buffer carved out of a mapped
+ * ring); a range that partly overlaps one is refused (INGOT_GPU_EINVAL).
+ * Two buffers whose bytes are disjoint but share a page are registered
+ * separately and may be mapped at the same time.  The caller keeps the bytes
+ * stable while a call that reads them runs, unmaps only after the calls that
+ * use a mapping have completed, and frees (or munmaps) pageable memory only
+ * after unmapping it: a registration whose pages were freed leaves a stale
+ * device mapping behind.
  */
 int ingot_gpu_host_map(ingot_gpu_ctx* ctx, void* host, size_t bytes, void** d_ptr);
 int ingot_gpu_host_unmap(ingot_gpu_ctx* ctx, void* host);

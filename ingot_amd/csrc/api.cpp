@@ -16,13 +16,38 @@
 #include "../../include/ingot_gpu.h"
 #include "kernels.h"
 
+namespace {
+
+// One ingot_gpu_host_map of [host, host + bytes) by a context.  `owned`:
+// the bytes lie inside a registration this library made (g_regs below);
+// otherwise the memory was pinned and mapped by someone else (hipHostMalloc,
+// or the caller's own hipHostRegister) and unmapping it is a no-op.
+struct HostMapping {
+    uintptr_t host, bytes, dev;
+    bool owned;
+};
+
+// Pageable host ranges this library page-locked (hipHostRegister, mapped).
+// Registration state is per process, not per context, so the table is too.
+// Each entry is the exact byte range registered; every ingot_gpu_host_map of
+// bytes inside it (by any context) holds a reference, and the last
+// ingot_gpu_host_unmap unregisters it.  Nothing else is ever unregistered.
+struct Registration {
+    uintptr_t host, bytes, dev;
+    uint32_t refs;
+};
+std::mutex g_reg_mu;
+std::vector<Registration> g_regs;
+
+}  // namespace
+
 struct ingot_gpu_ctx {
     int device;
     ingot_gpu::Tuning tuning;
     uint32_t wall_khz = 0;  // the device's constant-rate wall clock (stream delays)
-    // device address ranges of host memory mapped by ingot_gpu_host_map
+    // live ingot_gpu_host_map mappings of this context (dropped on unmap)
     std::mutex mu;
-    std::vector<std::pair<uintptr_t, uintptr_t>> host;
+    std::vector<HostMapping> host;
 };
 
 namespace {
@@ -58,9 +83,24 @@ ingot_gpu::Tuning tuning_for(ingot_gpu_ctx* ctx, const void* arena) {
     ingot_gpu::Tuning t = ctx->tuning;
     const uintptr_t a = (uintptr_t)arena;
     std::lock_guard<std::mutex> g(ctx->mu);
-    for (const auto& r : ctx->host)
-        if (a >= r.first && a < r.second) t.host_arena = true;
+    for (const auto& m : ctx->host)
+        if (a >= m.dev && a < m.dev + m.bytes) t.host_arena = true;
     return t;
+}
+
+// Drop one reference to the library's registration holding [h, h + n); the
+// last one unregisters it.  Caller holds g_reg_mu.
+void release_registration(uintptr_t h, uintptr_t n) {
+    for (size_t i = 0; i < g_regs.size(); ++i) {
+        Registration& r = g_regs[i];
+        if (h < r.host || h + n > r.host + r.bytes) continue;
+        if (--r.refs == 0) {
+            if (hipHostUnregister(reinterpret_cast<void*>(r.host)) != hipSuccess)
+                (void)hipGetLastError();
+            g_regs.erase(g_regs.begin() + (long)i);
+        }
+        return;
+    }
 }
 
 int stride_ok(const uint8_t* d_arena, uint32_t stride) {
@@ -170,7 +210,17 @@ int ingot_gpu_ctx_create(int device, ingot_gpu_ctx** out) {
     return INGOT_GPU_SUCCESS;
 }
 
-void ingot_gpu_ctx_destroy(ingot_gpu_ctx* ctx) { delete ctx; }
+void ingot_gpu_ctx_destroy(ingot_gpu_ctx* ctx) {
+    if (!ctx) return;
+    {  // the context's mappings still open release their registrations
+        std::lock_guard<std::mutex> g(g_reg_mu);
+        std::lock_guard<std::mutex> c(ctx->mu);
+        for (const HostMapping& m : ctx->host)
+            if (m.owned) release_registration(m.host, m.bytes);
+        ctx->host.clear();
+    }
+    delete ctx;
+}
 
 int ingot_gpu_ctx_device(const ingot_gpu_ctx* ctx) { return ctx ? ctx->device : -1; }
 
@@ -217,39 +267,71 @@ int ingot_gpu_parse_header(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uin
 int ingot_gpu_host_map(ingot_gpu_ctx* ctx, void* host, size_t bytes, void** d_ptr) {
     if (!ctx || !host || !d_ptr || bytes == 0) return INGOT_GPU_EINVAL;
     *d_ptr = nullptr;
+    const uintptr_t h = (uintptr_t)host;
+    if (h + bytes < h) return INGOT_GPU_ERANGE;
     if (int e = enter(ctx)) return e;
-    // already pinned and mapped (hipHostMalloc): use it as it is
-    hipPointerAttribute_t attr;
-    if (!(hipPointerGetAttributes(&attr, host) == hipSuccess && attr.type == hipMemoryTypeHost &&
-          hipHostGetDevicePointer(d_ptr, host, 0) == hipSuccess)) {
-        (void)hipGetLastError();  // clear the probe's error
-        if (hipHostRegister(host, bytes, hipHostRegisterMapped) != hipSuccess)
-            return INGOT_GPU_EHIP;
-        if (hipHostGetDevicePointer(d_ptr, host, 0) != hipSuccess) {
-            (void)hipHostUnregister(host);
-            *d_ptr = nullptr;
-            return INGOT_GPU_EHIP;
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    HostMapping m{h, bytes, 0, false};
+    // 1. inside one of our registrations: one more reference to it
+    for (Registration& r : g_regs) {
+        if (h >= r.host && h + bytes <= r.host + r.bytes) {
+            ++r.refs;
+            m.dev = r.dev + (h - r.host);
+            m.owned = true;
+            break;
+        }
+        // partly overlapping bytes we registered: the rest is not ours to
+        // register, and a second registration of the same bytes is refused
+        if (h < r.host + r.bytes && r.host < h + bytes) return INGOT_GPU_EINVAL;
+    }
+    if (!m.owned) {
+        // 2. pinned and mapped by someone else (hipHostMalloc, the caller's
+        //    own hipHostRegister): used as it is, never unregistered here
+        hipPointerAttribute_t attr;
+        void* d = nullptr;
+        if (hipPointerGetAttributes(&attr, host) == hipSuccess &&
+            attr.type == hipMemoryTypeHost && hipHostGetDevicePointer(&d, host, 0) == hipSuccess) {
+            m.dev = (uintptr_t)d;
+        } else {
+            // 3. pageable: page-lock and map exactly these bytes (pages
+            //    shared with neighbours stay usable by them)
+            (void)hipGetLastError();  // clear the probe's error
+            if (hipHostRegister(host, bytes, hipHostRegisterMapped) != hipSuccess) {
+                (void)hipGetLastError();
+                return INGOT_GPU_EHIP;
+            }
+            if (hipHostGetDevicePointer(&d, host, 0) != hipSuccess) {
+                (void)hipHostUnregister(host);
+                (void)hipGetLastError();
+                return INGOT_GPU_EHIP;
+            }
+            m.dev = (uintptr_t)d;
+            m.owned = true;
+            g_regs.push_back(Registration{h, bytes, m.dev, 1u});
         }
     }
-    const uintptr_t d = (uintptr_t)*d_ptr;
-    std::lock_guard<std::mutex> g(ctx->mu);
-    ctx->host.emplace_back(d, d + bytes);
+    {
+        std::lock_guard<std::mutex> c(ctx->mu);
+        ctx->host.push_back(m);
+    }
+    *d_ptr = reinterpret_cast<void*>(m.dev);
     return INGOT_GPU_SUCCESS;
 }
 
 int ingot_gpu_host_unmap(ingot_gpu_ctx* ctx, void* host) {
     if (!ctx || !host) return INGOT_GPU_EINVAL;
-    if (int e = enter(ctx)) return e;
-    void* d = nullptr;
-    if (hipHostGetDevicePointer(&d, host, 0) == hipSuccess) {
-        std::lock_guard<std::mutex> g(ctx->mu);
-        for (size_t i = 0; i < ctx->host.size(); ++i)
-            if (ctx->host[i].first == (uintptr_t)d) {
-                ctx->host.erase(ctx->host.begin() + (long)i);
-                break;
-            }
+    const uintptr_t h = (uintptr_t)host;
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    HostMapping m{};
+    {
+        std::lock_guard<std::mutex> c(ctx->mu);
+        size_t i = ctx->host.size();
+        while (i > 0 && ctx->host[i - 1].host != h) --i;  // the latest mapping of `host`
+        if (i == 0) return INGOT_GPU_EINVAL;               // not mapped by this context
+        m = ctx->host[i - 1];
+        ctx->host.erase(ctx->host.begin() + (long)(i - 1));
     }
-    if (hipHostUnregister(host) != hipSuccess) (void)hipGetLastError();  // not registered by us
+    if (m.owned) release_registration(m.host, m.bytes);  // registrations are per process
     return INGOT_GPU_SUCCESS;
 }
 
