@@ -1263,7 +1263,8 @@ def gate_policy(flows: bool, world: int, backend: str, no_gate: bool) -> str:
       "off"   — from host submission: --no-gate, or the gloo rehearsal of
                 config 5 at N > 1, whose histogram reduce copies through the
                 host (a held stream would block it);
-      "until_collective" — config 5 over RCCL at N > 1: launches are held
+      "until_collective" — config 5 over RCCL (the library's one-rank
+                communicator at N = 1, the ranks' at N > 1): launches are held
                 behind the doorbell only up to the first collective of the
                 region; the runner rings it before issuing any all-reduce, so
                 no collective is ever enqueued while a stream of this process
@@ -1272,8 +1273,8 @@ def gate_policy(flows: bool, world: int, backend: str, no_gate: bool) -> str:
       "hold"  — everything else: the first Gate.HOLD launches are held."""
     if no_gate:
         return "off"
-    if flows and world > 1:
-        return "off" if backend == "gloo" else "until_collective"
+    if flows:
+        return "off" if backend == "gloo" and world > 1 else "until_collective"
     return "hold"
 
 
@@ -1572,10 +1573,22 @@ def run_config(args, config, env):
     if flows:
         hists = [torch.zeros(FLOW_BINS, dtype=torch.int32, device=dev) for _ in range(reps)]
         flow_ids = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(reps)]
-        if world > 1:  # communicators up before any gated region (eager, ungated)
+        # config 5's reduce is the product's (ingot_gpu_flow_hist_allreduce over
+        # the library's RCCL communicator, a one-rank one at N = 1); the gloo
+        # rehearsal of N > 1 reduces through torch.distributed instead.
+        # Communicators up before any gated region (eager, ungated).
+        comm = None
+        if args.dist_backend == "gloo" and world > 1:
+            reduce_fn = idist.reduce_histogram_async
             idist.reduce_histogram(hists[0])
-            hists[0].zero_()
-            torch.cuda.synchronize(dev)
+        else:
+            comm = getattr(ctx, "_flow_comm", None)
+            if comm is None:
+                comm = ctx._flow_comm = idist.product_comm(ctx)
+            reduce_fn = idist.product_reduce(comm)
+            comm.allreduce_hist(hists[0])
+        hists[0].zero_()
+        torch.cuda.synchronize(dev)
     recs0 = None
     if mode == "read":
         # mblk-style packets over the same frames (chunks inside each frame)
@@ -1601,7 +1614,7 @@ def run_config(args, config, env):
                               ring_outs if record == 16 else outs8, streams[0], record, group)
         if flows:
             return FlowRunner(torch, lib, ctx, chain, n, arenas, off, lens, hists, flow_ids,
-                              streams[:nstreams], idist.reduce_histogram_async, flows_only,
+                              streams[:nstreams], reduce_fn, flows_only,
                               open_before_collective=policy == "until_collective")
         if mode == "modify":
             return ModifyRunner(torch, lib, ctx, chain, n, stride, arenas, off, lens,
@@ -1975,9 +1988,13 @@ def run_config(args, config, env):
         "distributed": {
             **idist.world_info(),
             "region_ms_per_rank": [round(x, 5) for x in region_ms_per_rank],
-            "collective": (f"all_reduce SUM of the {FLOW_BINS} x u32 flow histogram every step "
-                           f"({'RCCL' if args.dist_backend == 'nccl' else 'gloo'})"
-                           if flows and world > 1 else None),
+            "collective": ((f"ingot_gpu_flow_hist_allreduce every step: RCCL all-reduce SUM "
+                            f"(ncclUint32) of the {FLOW_BINS} x u32 flow histogram over the "
+                            f"library's {world}-rank communicator, on the step's stream"
+                            if args.dist_backend == "nccl" or world == 1 else
+                            f"gloo rehearsal: torch all_reduce SUM of the {FLOW_BINS} x u32 "
+                            "histogram through host memory")
+                           if flows else None),
             "flow_hist_check": hist_check,
         },
         "ms_per_step_ungated": ungated,

@@ -886,6 +886,40 @@ int ingot_gpu_flow_hist_ws(ingot_gpu_ctx* ctx, const uint8_t* d_arena,
                            size_t work_bytes, void* stream);
 size_t ingot_gpu_flow_hist_workspace_size(uint64_t n, uint32_t bins);
 
+/*
+ * The multi-GPU reduce of config 5 (the only collective of the design).
+ * Packets shard across GPUs by contiguous index ranges with no exchange;
+ * each rank's ingot_gpu_flow_hist leaves a per-rank histogram, and the job's
+ * histogram is their element-wise sum: RCCL all-reduce (sum, uint32) over
+ * xGMI, 65,536 x u32 = 256 KiB at the default bins.
+ *
+ * One process (or thread) per GPU.  Rank 0 makes a communicator id with
+ * ingot_gpu_comm_unique_id and the host sends its INGOT_COMM_ID_BYTES bytes to
+ * every rank over its own control channel; every rank then calls
+ * ingot_gpu_comm_create with the same id, nranks and its own rank (this
+ * blocks until all ranks have joined).  The communicator is bound to ctx's
+ * device.  RCCL is loaded at the first call of these functions (librccl.so.1,
+ * the one already in the process if there is one); INGOT_GPU_ENODEV if it
+ * cannot be loaded, INGOT_GPU_ECOMM if an RCCL call fails.
+ *
+ * ingot_gpu_flow_hist_allreduce enqueues the in-place sum of d_hist (bins x
+ * u32, device memory of the communicator's device) across all ranks on
+ * `stream`, ordered after the work already enqueued there (e.g. the
+ * ingot_gpu_flow_hist that filled it) and before what follows; every rank
+ * must enqueue the same sequence of reduces.  The counts wrap modulo 2^32.
+ */
+#define INGOT_GPU_ECOMM (-6)    /* a collective (RCCL) call failed */
+#define INGOT_COMM_ID_BYTES 128
+typedef struct ingot_gpu_comm ingot_gpu_comm;
+int ingot_gpu_comm_unique_id(uint8_t id[INGOT_COMM_ID_BYTES]);
+int ingot_gpu_comm_create(ingot_gpu_ctx* ctx, int nranks, int rank,
+                          const uint8_t id[INGOT_COMM_ID_BYTES], ingot_gpu_comm** out);
+void ingot_gpu_comm_destroy(ingot_gpu_comm* comm);
+int ingot_gpu_comm_size(const ingot_gpu_comm* comm);
+int ingot_gpu_comm_rank(const ingot_gpu_comm* comm);
+int ingot_gpu_flow_hist_allreduce(ingot_gpu_comm* comm, uint32_t* d_hist, uint32_t bins,
+                                  void* stream);
+
 /* ---------------------------------------------------------------------------
  * Frames stored back to back with only a length array (a capture buffer, a
  * ring without a descriptor table): frame i starts at d_arena + the sum of

@@ -657,6 +657,55 @@ class Doorbell:
             self._h = None
 
 
+COMM_ID_BYTES = 128  # INGOT_COMM_ID_BYTES
+
+
+def comm_unique_id() -> bytes:
+    """ingot_gpu_comm_unique_id: a new communicator id (rank 0 makes it; the
+    host sends the bytes to every rank)."""
+    lib = _lib.load()
+    buf = (ctypes.c_uint8 * COMM_ID_BYTES)()
+    _lib.check(lib.ingot_gpu_comm_unique_id(buf), "ingot_gpu_comm_unique_id")
+    return bytes(buf)
+
+
+class Comm:
+    """ingot_gpu_comm: the RCCL communicator of config 5's histogram reduce,
+    bound to `ctx`'s device.  Creating it blocks until all `nranks` ranks
+    have joined with the same `uid`."""
+
+    def __init__(self, ctx: Context, nranks: int, rank: int, uid: bytes):
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError(f"a communicator id is {COMM_ID_BYTES} bytes")
+        self._lib = _lib.load()
+        h = ctypes.c_void_p()
+        buf = (ctypes.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
+        _lib.check(self._lib.ingot_gpu_comm_create(ctx._h, int(nranks), int(rank), buf,
+                                                   ctypes.byref(h)), "ingot_gpu_comm_create")
+        self._h = h
+        self.device = ctx.device
+        self.size = int(self._lib.ingot_gpu_comm_size(h))
+        self.rank = int(self._lib.ingot_gpu_comm_rank(h))
+
+    def allreduce_hist(self, hist, stream=None):
+        """ingot_gpu_flow_hist_allreduce: in-place sum of a (bins,) u32 / i32
+        histogram over the ranks, enqueued on `stream` (default: torch's
+        current stream).  Returns `hist`."""
+        if hist.element_size() != 4 or not hist.is_contiguous() or not hist.is_cuda:
+            raise ValueError("hist must be a contiguous 32-bit device tensor")
+        if hist.device.index != self.device:
+            raise ValueError(f"hist is on {hist.device}, the communicator on cuda:{self.device}")
+        _lib.check(self._lib.ingot_gpu_flow_hist_allreduce(
+            self._h, hist.data_ptr(), hist.numel(), _stream(stream, self.device)),
+            "ingot_gpu_flow_hist_allreduce")
+        return hist
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.ingot_gpu_comm_destroy(self._h)
+            self._h = None
+
+
 def records_to_numpy(t):
     """(n, 16) uint8 tensor/array -> numpy structured array of ingot_rec."""
     import numpy as np

@@ -127,6 +127,14 @@ SIGNATURES = {
          ctypes.c_uint32, c_u8p, c_u8p, c_u8p, c_u8p, ctypes.c_size_t, ctypes.c_void_p],
     ),
     "ingot_gpu_flow_hist_workspace_size": (ctypes.c_size_t, [c_u64, ctypes.c_uint32]),
+    "ingot_gpu_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
+    "ingot_gpu_comm_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "ingot_gpu_comm_destroy": (None, [ctypes.c_void_p]),
+    "ingot_gpu_comm_size": (ctypes.c_int, [ctypes.c_void_p]),
+    "ingot_gpu_comm_rank": (ctypes.c_int, [ctypes.c_void_p]),
+    "ingot_gpu_flow_hist_allreduce": (ctypes.c_int, [ctypes.c_void_p, c_u8p, ctypes.c_uint32,
+                                                     ctypes.c_void_p]),
     "ingot_gpu_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "ingot_parse_error_name": (ctypes.c_char_p, [ctypes.c_int]),
     "ingot_chain_layer_label": (ctypes.c_char_p, [ctypes.c_int, ctypes.c_int]),

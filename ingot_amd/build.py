@@ -21,7 +21,7 @@ CSRC = PKG / "csrc"
 BUILD = PKG / "build"
 LIB = PKG / "lib" / "libingot_gpu.so"
 SOURCES = ["parse.hip", "read.hip", "ring.hip", "flow.hip", "tuple.hip", "header.hip", "packed.hip",
-           "pktgen.hip", "pktgen_host.cpp", "stream.hip", "emit.hip", "api.cpp"]
+           "pktgen.hip", "pktgen_host.cpp", "stream.hip", "emit.hip", "api.cpp", "comm.cpp"]
 ARCH = "gfx950"
 
 
@@ -81,7 +81,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
             raise
     if force or jobs or _stale(LIB, objs):
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB)]
-        cmd += [str(o) for o in objs]
+        cmd += [str(o) for o in objs] + ["-ldl"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

@@ -784,6 +784,7 @@ const char* ingot_gpu_strerror(int code) {
     case INGOT_GPU_ENOMEM: return "out of host memory";
     case INGOT_GPU_ENODEV: return "no such gfx950 device";
     case INGOT_GPU_ERANGE: return "size outside the supported range";
+    case INGOT_GPU_ECOMM: return "collective (RCCL) call failed";
     default: return "unknown error";
     }
 }

@@ -155,3 +155,46 @@ def reduce_histogram_async(hist):
         reduce_histogram(hist)
         return _Done()
     return dist.all_reduce(view, op=dist.ReduceOp.SUM, async_op=True)
+
+
+def product_comm(ctx):
+    """The library's own communicator for config 5's reduce
+    (ingot_gpu_comm_create behind the C ABI), over the same ranks as the
+    torch.distributed group: rank 0 makes the id and the group carries its
+    128 bytes to every rank.  World 1 (no group): a one-rank communicator, so
+    the reduce is the same RCCL call at every N."""
+    import torch.distributed as dist
+
+    import ingot_amd
+
+    if _active():
+        obj = [ingot_amd.comm_unique_id() if dist.get_rank() == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        return ingot_amd.Comm(ctx, dist.get_world_size(), dist.get_rank(), obj[0])
+    return ingot_amd.Comm(ctx, 1, 0, ingot_amd.comm_unique_id())
+
+
+class _StreamDone:
+    """Completion of a reduce enqueued on the current stream: wait() orders
+    the caller's current stream after it (an event, no host wait)."""
+
+    def __init__(self, torch):
+        self._torch = torch
+        self.ev = torch.cuda.Event()
+        self.ev.record()
+
+    def wait(self):
+        self._torch.cuda.current_stream().wait_event(self.ev)
+
+
+def product_reduce(comm):
+    """reduce_fn for the config-5 runner: ingot_gpu_flow_hist_allreduce of the
+    step's histogram, enqueued on the step's stream after its flow kernels (the
+    next steps' kernels on the other streams overlap it)."""
+    import torch
+
+    def reduce(hist):
+        comm.allreduce_hist(hist)
+        return _StreamDone(torch)
+
+    return reduce

@@ -251,11 +251,13 @@ def test_timed_region_spans_earliest_start_to_latest_end(monkeypatch):
 
 
 def test_gate_policy():
-    """No collective behind an unrung doorbell: config 5 over RCCL at N > 1
-    holds launches only until its first collective; the gloo rehearsal
-    (host-side reduce) is not gated; everything else holds Gate.HOLD."""
+    """No collective behind an unrung doorbell: config 5 reduces through the
+    library's RCCL communicator at every N (one rank at N = 1) and holds
+    launches only until its first collective; the gloo rehearsal (host-side
+    reduce) is not gated; everything else holds Gate.HOLD."""
     assert bench.gate_policy(False, 1, "nccl", False) == "hold"
-    assert bench.gate_policy(True, 1, "nccl", False) == "hold"
+    assert bench.gate_policy(True, 1, "nccl", False) == "until_collective"
+    assert bench.gate_policy(True, 1, "gloo", False) == "until_collective"
     assert bench.gate_policy(False, 8, "nccl", False) == "hold"
     assert bench.gate_policy(True, 8, "nccl", False) == "until_collective"
     assert bench.gate_policy(True, 2, "gloo", False) == "off"
