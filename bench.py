@@ -753,17 +753,19 @@ class EmitRunner:
         self._hdr = (ctypes.c_uint8 * len(hdr)).from_buffer_copy(hdr)
         ln = lens.to(torch.int64)
         self.dst_off = torch.cumsum(ln + len(hdr), 0) - (ln + len(hdr))
-        self.dst = torch.empty(int((ln + len(hdr)).sum().item()) + 64, dtype=torch.uint8,
-                               device=dev)
+        # one destination per stream: launches running together never write
+        # the same bytes (as the parse runners' record buffers)
+        size = int((ln + len(hdr)).sum().item()) + 64
+        self.dst = [torch.empty(size, dtype=torch.uint8, device=dev) for _ in streams]
         h, reps = ctx._h, len(arenas)
         aptrs = [a.data_ptr() for a in arenas]
         sp, hp, H = self._sets.ctypes.data, ctypes.addressof(self._hdr), len(hdr)
         optr, lptr = off.data_ptr(), lens.data_ptr()
-        dptr, doptr = self.dst.data_ptr(), self.dst_off.data_ptr()
+        dptrs, doptr = [d.data_ptr() for d in self.dst], self.dst_off.data_ptr()
         sps = [s.cuda_stream for s in streams]
         self.launch = lambda k: lib.ingot_gpu_emit_packets(
-            h, hp, H, sp, len(rows), aptrs[k % reps], optr, lptr, n, dptr, doptr,
-            sps[k % len(sps)])
+            h, hp, H, sp, len(rows), aptrs[k % reps], optr, lptr, n, dptrs[k % len(sps)],
+            doptr, sps[k % len(sps)])
 
     def run(self, steps, gate=None):
         return _timed(self.torch, self.streams, self.launch, steps, gate=gate)

@@ -45,6 +45,7 @@ struct ingot_gpu_ctx {
     int device;
     ingot_gpu::Tuning tuning;
     uint32_t wall_khz = 0;  // the device's constant-rate wall clock (stream delays)
+    size_t lds_bytes = 160u * 1024u;  // LDS per workgroup (the device's, at create)
     // live ingot_gpu_host_map mappings of this context (dropped on unmap)
     std::mutex mu;
     std::vector<HostMapping> host;
@@ -202,6 +203,11 @@ int ingot_gpu_ctx_create(int device, ingot_gpu_ctx** out) {
     ingot_gpu_ctx* c = new (std::nothrow) ingot_gpu_ctx{device, {}};
     if (!c) return INGOT_GPU_ENOMEM;
     if (prop.multiProcessorCount > 0) c->tuning.cus = (uint32_t)prop.multiProcessorCount;
+    int lds = 0;
+    if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) ==
+            hipSuccess &&
+        lds > 0)
+        c->lds_bytes = (size_t)lds;
     int khz = 0;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess &&
         khz > 0)
@@ -655,9 +661,10 @@ int emit_args(const uint8_t* hdr, uint32_t hdr_len, const ingot_emit_set* sets,
             return INGOT_GPU_EINVAL;
         const FieldGeo g = kFieldGeo[e.field];
         ingot_gpu::EmitSet& d = a.sets[k];
-        d.pos = (uint16_t)(e.at + g.bit / 8u);
+        const uint32_t pos = (uint32_t)e.at + g.bit / 8u;  // 32 bits: no wrap before the check
         d.nbytes = (uint8_t)((g.bit % 8u + g.bits + 7u) / 8u);
-        if ((uint32_t)d.pos + d.nbytes > hdr_len) return INGOT_GPU_EINVAL;  // field inside hdr
+        if (pos + d.nbytes > hdr_len) return INGOT_GPU_EINVAL;  // field inside hdr
+        d.pos = (uint16_t)pos;
         d.rshift = (uint8_t)((8u - ((g.bit + g.bits) % 8u)) % 8u);
         d.bits = g.bits;
         d.source = e.source;
@@ -667,6 +674,11 @@ int emit_args(const uint8_t* hdr, uint32_t hdr_len, const ingot_emit_set* sets,
     }
     a.n_sets = n_sets;
     return INGOT_GPU_SUCCESS;
+}
+
+// The device's LDS per workgroup must hold one emit block's (ERANGE if not).
+int emit_fits(const ingot_gpu_ctx* ctx, const ingot_gpu::EmitArgs& a) {
+    return ingot_gpu::emit_lds_bytes(a) <= ctx->lds_bytes ? INGOT_GPU_SUCCESS : INGOT_GPU_ERANGE;
 }
 
 }  // namespace
@@ -689,6 +701,7 @@ int ingot_gpu_emit_packets(ingot_gpu_ctx* ctx, const uint8_t* hdr, uint32_t hdr_
     a.dst = d_dst;
     a.dst_off = d_dst_off;
     a.n = n;
+    if (int e = emit_fits(ctx, a)) return e;
     return from_hip(ingot_gpu::launch_emit(a, (hipStream_t)stream));
 }
 
@@ -708,6 +721,7 @@ int ingot_gpu_emit_headers(ingot_gpu_ctx* ctx, const uint8_t* hdr, uint32_t hdr_
     a.dst_off = d_out_off;
     a.stride = out_stride;
     a.n = n;
+    if (int e = emit_fits(ctx, a)) return e;
     return from_hip(ingot_gpu::launch_emit(a, (hipStream_t)stream));
 }
 

@@ -363,19 +363,33 @@ __global__ __launch_bounds__(Shape<COPY>::BLOCK) void k_emit(EmitArgs a) {
     }
 }
 
+// Dynamic LDS of one k_emit block for a header block of H bytes.
+template <bool COPY>
+constexpr size_t emit_smem(uint32_t H) {
+    return (INGOT_MAX_EMIT_HDR / 16 + 4) * 16 +
+           Shape<COPY>::G * (sizeof(WaveDesc<Shape<COPY>::NP>) + Shape<COPY>::NP * region_bytes(H));
+}
+// gfx950: 160 KiB of LDS per workgroup.  A build with other group shapes
+// (INGOT_EMIT_GROUP_SUBS / _WAVES) must still fit the largest header block.
+static_assert(emit_smem<true>(INGOT_MAX_EMIT_HDR) <= 160u * 1024u, "k_emit<copy> LDS > 160 KiB");
+static_assert(emit_smem<false>(INGOT_MAX_EMIT_HDR) <= 160u * 1024u, "k_emit LDS > 160 KiB");
+
 template <bool COPY>
 hipError_t go(const EmitArgs& a, hipStream_t s) {
     constexpr uint32_t G = Shape<COPY>::G, NP = Shape<COPY>::NP;
     const uint64_t groups = (a.n + NP - 1) / NP;
     const uint64_t blocks = (groups + G - 1) / G;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    const size_t smem = (INGOT_MAX_EMIT_HDR / 16 + 4) * 16 +
-                        G * (sizeof(WaveDesc<NP>) + NP * region_bytes(a.hdr_len));
+    const size_t smem = emit_smem<COPY>(a.hdr_len);
     hipLaunchKernelGGL((k_emit<COPY>), dim3((uint32_t)blocks), dim3(Shape<COPY>::BLOCK), smem, s, a);
     return hipGetLastError();
 }
 
 }  // namespace
+
+size_t emit_lds_bytes(const EmitArgs& a) {
+    return a.src ? emit_smem<true>(a.hdr_len) : emit_smem<false>(a.hdr_len);
+}
 
 hipError_t launch_emit(const EmitArgs& a, hipStream_t s) {
     if (a.n == 0) return hipSuccess;

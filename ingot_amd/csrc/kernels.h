@@ -152,6 +152,8 @@ struct EmitArgs {
     uint32_t hdr[INGOT_MAX_EMIT_HDR / 4];  // the header block, zero-padded
 };
 static_assert(sizeof(EmitArgs) <= 4096, "EmitArgs exceeds the 4 KiB kernel-argument limit");
+// bytes of dynamic LDS one emit block needs (checked against the device)
+size_t emit_lds_bytes(const EmitArgs& a);
 hipError_t launch_emit(const EmitArgs& a, hipStream_t s);
 
 // Lengths-only packed frames (packed.hip): tile base = u64 base of its group

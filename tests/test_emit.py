@@ -354,6 +354,11 @@ def test_emit_argument_errors(ctx, torch):
     assert lib.ingot_gpu_emit_headers(ctx._h, a, 257, None, 0, p, 1, p, None, 512, None) == -1
     assert lib.ingot_gpu_emit_headers(ctx._h, a, 64, sp, 9, p, 1, p, None, 64, None) == -1
     assert lib.ingot_gpu_emit_headers(ctx._h, a, 5, sp, 1, p, 1, p, None, 64, None) == -1
+    # a setter offset past the block (at + byte offset would wrap in 16 bits)
+    for at in (65535, 65534, 256):
+        far = ingot_amd.emit_sets_array([(at, Field.UDP_DESTINATION, EmitSource.VALUE, 7)])
+        assert lib.ingot_gpu_emit_headers(ctx._h, a, 64, far.ctypes.data_as(ctypes.c_void_p), 1,
+                                          p, 1, p, None, 64, None) == -1, at
     # a U16 source without values; an unknown source / field
     bad = ingot_amd.emit_sets_array([(0, Field.UDP_SOURCE, EmitSource.U16, 0)])
     assert lib.ingot_gpu_emit_headers(ctx._h, a, 8, bad.ctypes.data_as(ctypes.c_void_p), 1, p,

@@ -130,13 +130,19 @@ def main():
     tot = lens.to(torch.int64) + len(hdr) + 3
     d_off = torch.cumsum(tot, 0) - tot
     size = int(tot.sum().item()) + 64
-    e0 = torch.zeros(size, dtype=torch.uint8, device="cuda")
+    # every launch writes into a buffer refilled with a sentinel first (gap
+    # bytes included, which must stay untouched), so a launch that writes
+    # nothing or only part of its output is a mismatch
+    SENT = 0xEE
+    e0 = torch.full((size,), SENT, dtype=torch.uint8, device="cuda")
     ctx.emit_packets(hdr, dsets, arena, off, lens, e0, d_off)
     torch.cuda.synchronize()
-    eouts = [torch.zeros(size, dtype=torch.uint8, device="cuda") for _ in range(4)]
+    eouts = [torch.empty(size, dtype=torch.uint8, device="cuda") for _ in range(4)]
     acc = [torch.zeros((), dtype=torch.int64, device="cuda") for _ in s]
     for it in range(args.iters // 5):
         k, st = it % 4, s[it % 2]
+        with torch.cuda.stream(st):
+            eouts[k].fill_(SENT)
         ctx.emit_packets(hdr, dsets, arena, off, lens, eouts[k], d_off, stream=st)
         with torch.cuda.stream(st):
             acc[it % 2] += (eouts[k] != e0).any().to(torch.int64)
