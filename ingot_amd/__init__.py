@@ -15,6 +15,7 @@ Device memory, streams and torch.distributed come from PyTorch (plumbing).
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -108,12 +109,27 @@ class PacketParseError(Exception):
         return self.inner
 
 
+def _one_hip_runtime() -> None:
+    """Refuse to run with two HIP runtimes mapped in this process (the
+    library's from /opt/rocm beside PyTorch's own copy; _lib.load)."""
+    try:
+        with open("/proc/self/maps") as f:
+            paths = {ln.split()[-1] for ln in f if "libamdhip64.so" in ln and "/" in ln}
+    except OSError:
+        return
+    real = {os.path.realpath(p) for p in paths}
+    if len(real) > 1:
+        raise RuntimeError(f"two HIP runtimes are loaded in this process: {sorted(real)}; "
+                           "import torch before loading libingot_gpu.so")
+
+
 class Context:
     """One device.  Mirrors `ingot_gpu_ctx`; all calls are async on `stream`
     (default: torch's current stream on that device)."""
 
     def __init__(self, device: int = 0):
         self._lib = _lib.load()
+        _one_hip_runtime()
         h = ctypes.c_void_p()
         _lib.check(self._lib.ingot_gpu_ctx_create(int(device), ctypes.byref(h)),
                    "ingot_gpu_ctx_create")

@@ -175,6 +175,16 @@ def load() -> ctypes.CDLL:
             f"{LIB_PATH} is missing: build it with `python -m ingot_amd.build` "
             "(hipcc --offload-arch=gfx950); there is no fallback path"
         )
+    # One HIP runtime per process.  PyTorch-ROCm ships its own libamdhip64
+    # (soname libamdhip64.so.7) and its libraries name it "libamdhip64.so";
+    # this library names the soname.  Loaded after torch, the library binds
+    # to torch's copy; loaded first, it brings /opt/rocm's in and torch then
+    # loads a second runtime beside it (contexts fail: ENODEV).  So torch
+    # first, whenever it is installed.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(str(LIB_PATH))
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
