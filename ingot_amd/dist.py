@@ -167,11 +167,36 @@ def product_comm(ctx):
 
     import ingot_amd
 
-    if _active():
-        obj = [ingot_amd.comm_unique_id() if dist.get_rank() == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        return ingot_amd.Comm(ctx, dist.get_world_size(), dist.get_rank(), obj[0])
-    return ingot_amd.Comm(ctx, 1, 0, ingot_amd.comm_unique_id())
+    with _stdout_to_stderr():  # RCCL prints its version banner on stdout
+        if _active():
+            obj = [ingot_amd.comm_unique_id() if dist.get_rank() == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            return ingot_amd.Comm(ctx, dist.get_world_size(), dist.get_rank(), obj[0])
+        return ingot_amd.Comm(ctx, 1, 0, ingot_amd.comm_unique_id())
+
+
+class _stdout_to_stderr:
+    """File descriptor 1 pointed at fd 2 for the block: what native code
+    prints there (RCCL's init banner) stays out of bench.py's one-line
+    stdout."""
+
+    def __enter__(self):
+        import os
+        import sys
+
+        sys.stdout.flush()
+        self._saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        import os
+        import sys
+
+        sys.stdout.flush()
+        os.dup2(self._saved, 1)
+        os.close(self._saved)
+        return False
 
 
 class _StreamDone:

@@ -475,16 +475,19 @@ def _fake_line(value, cpu_label="clean", variants=None, ratio=1.3):
 
 
 def test_compact_line_ends_in_a_summary_of_every_config(tmp_path, monkeypatch):
-    """The driver keeps the line's last ~1,800 characters: the
-    line drops each cpu_baseline's detail and ends in a summary that names
-    C2 (and its 1 GiB record-ring read share), C3, C4 and C5 with their
-    value, step time, kernel roofline fraction, traffic ratio and CPU
-    baseline (clean / contended)."""
+    """The driver keeps the last ~8,000 characters of stdout:
+    the whole line fits in 7,000, every config keeps its value, step time,
+    roofline fraction and CPU baseline, C2 its host-inclusive rate and
+    1 GiB record-ring read share, and the line ends in a summary that names
+    C2, C3, C4 and C5 (traffic ratio, CPU baseline clean / contended)."""
     import json
 
     monkeypatch.setattr(bench, "ROOT", tmp_path)
     main = _fake_line(88_000, variants={"streams2_rec16_records64": {
         "us_per_step": 12.5, "read_frac": 0.667}})
+    main["roofline"]["read_frac_records_dram"] = 0.667
+    main["host_inclusive"] = {"frames_per_batch": 1 << 20, "memcpy_Mpkt_s": 700.7,
+                              "zero_copy_Mpkt_s": 827.6, "source": "x" * 400}
     subs = {"c3": _fake_line(29_000, "contended"), "c4": _fake_line(29_100),
             "c5": _fake_line(26_000, variants={"plain_parse_streams1_rec16": {
                 "flows_over_plain": 1.07}})}
@@ -500,6 +503,12 @@ def test_compact_line_ends_in_a_summary_of_every_config(tmp_path, monkeypatch):
     s = out["summary"]
     assert s["c3"]["cpu"].endswith("contended") and s["c4"]["cpu"].endswith("clean")
     assert s["c2_records_1GiB_ring"]["step_read_frac"] == 0.667
+    assert len(text) < 7000, len(text)
+    c3 = out["sublines"]["c3"]
+    assert c3["value"] == 29_000 and c3["ms_per_step"] and c3["roofline"]["frac"] == 0.72
+    assert c3["cpu_baseline"]["value"] == 800.0
+    assert out["host_inclusive"]["zero_copy_Mpkt_s"] == 827.6
+    assert out["roofline"]["read_frac_records_dram"] == 0.667
 
 
 def test_read_chunks_np_equals_read_chunks():
