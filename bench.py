@@ -1424,8 +1424,12 @@ def main():
         result["wall_s_command"] = round(time.perf_counter() - T_START, 2)
     if rank == 0:
         print(json.dumps(jsonable(compact_line(result, args.config))), flush=True)
+    comm = getattr(ctx, "_flow_comm", None)
     if world > 1:
         dist.barrier()
+    if comm is not None:  # every rank releases config 5's communicator together
+        comm.close()
+    if world > 1:
         dist.destroy_process_group()
 
 
