@@ -351,6 +351,34 @@ class Context {
     ingot_gpu_ctx* h_ = nullptr;
 };
 
+// Config 5's reduce: one rank's RCCL communicator (ingot_gpu_comm_*).  Rank 0
+// calls Comm::unique_id() and the host carries the bytes to every rank;
+// allreduce_hist sums a device histogram (bins x u32) over the ranks on
+// `stream`, after the work already enqueued there.
+class Comm {
+   public:
+    using Id = std::array<uint8_t, INGOT_COMM_ID_BYTES>;
+    static Id unique_id() {
+        Id id{};
+        check(ingot_gpu_comm_unique_id(id.data()), "comm_unique_id");
+        return id;
+    }
+    Comm(Context& ctx, int nranks, int rank, const Id& id) {
+        check(ingot_gpu_comm_create(ctx.get(), nranks, rank, id.data(), &h_), "comm_create");
+    }
+    ~Comm() { ingot_gpu_comm_destroy(h_); }
+    Comm(const Comm&) = delete;
+    Comm& operator=(const Comm&) = delete;
+    int size() const { return ingot_gpu_comm_size(h_); }
+    int rank() const { return ingot_gpu_comm_rank(h_); }
+    void allreduce_hist(uint32_t* d_hist, uint32_t bins, hipStream_t stream = nullptr) {
+        check(ingot_gpu_flow_hist_allreduce(h_, d_hist, bins, stream), "flow_hist_allreduce");
+    }
+
+   private:
+    ingot_gpu_comm* h_ = nullptr;
+};
+
 // Uploads host frames into a packed device arena, runs the records + field
 // kernels for `chain`, copies the per-packet field blocks back.
 inline std::vector<Packet> parse_batch(Context& ctx, const std::vector<std::vector<uint8_t>>& frames,

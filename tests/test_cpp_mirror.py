@@ -70,3 +70,24 @@ def test_cpp_doorbell_ring_on_device():
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "first held: ok" in r.stdout
+
+
+@pytest.mark.gpu
+def test_cpp_flow_reduce_example_on_device():
+    """tests/cpp/example_flow_reduce.cpp: config 5's step from a host that
+    binds only the C ABI — flow hash + histogram, then the RCCL reduce over a
+    communicator made from rank 0's id (one rank on this box; RCCL opened by
+    the library itself, no PyTorch in the process)."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    exe = ROOT / "tests" / "cpp" / "build" / "example_flow_reduce"
+    if not exe.exists():
+        from ingot_amd.build import build_cpp_tests
+
+        build_cpp_tests()
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 mismatches" in r.stdout and "rccl reduce over 1 rank(s)" in r.stdout
