@@ -1461,7 +1461,8 @@ def _short_roofline(r):
     k = r.get("kernel") or ""
     k = k.replace("void ingot_gpu::(anonymous namespace)::", "")
     out["kernel"] = (k.rsplit("(ingot_gpu::", 1)[0] if "(ingot_gpu::" in k else k)[:70]
-    for key in ("launch_mean_us", "read_frac", "pipelined_read_frac", "read_frac_records_dram"):
+    for key in ("launch_mean_us", "algorithmic_bytes_per_launch", "read_frac",
+                "pipelined_read_frac", "read_frac_records_dram"):
         if r.get(key) is not None:
             out[key] = r[key]
     return out

@@ -74,14 +74,21 @@ def main():
                                                                    "k_emit"))]
         # the line names its kernel (and a C2 run's summary also holds the
         # C3 sub-line's k_parse): match it; else the most-called parse kernel
-        named = [r for r in parse if r["Name"] == prof_line["roofline"].get("kernel")]
+        kname = prof_line["roofline"].get("kernel") or ""
+        # (the printed line names it without the "void ingot_gpu::(anon)::"
+        # prefix and the argument list)
+        named = [r for r in parse if r["Name"] == kname] or \
+            [r for r in parse if kname and "<" in kname and kname in r["Name"]]
         dom = named[0] if named else max(parse, key=lambda r: int(r["Calls"]))
         mean_us = float(dom["AverageNs"]) / 1e3
         for extra in EXTRA.get(cfg, ()):
             mean_us += sum(float(r["AverageNs"]) / 1e3 for r in rows if extra in r["Name"])
         rl = line["roofline"]
         pr = prof_line["roofline"]
-        alg = pr["algorithmic_bytes_per_launch"]
+        # (lines printed before the field joined the compact form: achieved
+        # GB/s x the launch mean gives the same bytes to ~1e-5)
+        alg = pr.get("algorithmic_bytes_per_launch") or \
+            pr["achieved"] * pr["launch_mean_us"] * 1e3
         frac_p = alg / (mean_us * 1e-6) / 1e9 / pr["peak"]
         rec = {"value": line["value"], "ms_per_step": line["ms_per_step"],
                "frac_line": rl["frac"], "frac_profiled_run_line": pr["frac"],
@@ -89,7 +96,8 @@ def main():
                "launch_mean_us_line": rl["launch_mean_us"],
                "launch_mean_us_profiled_run": pr["launch_mean_us"],
                "profile_mean_us": round(mean_us, 3), "profile_kernel": dom["Name"],
-               "traffic_ratio": (rl.get("traffic_detail") or {}).get("ratio_to_algorithmic"),
+               "traffic_ratio": (rl.get("traffic_detail") or {}).get("ratio_to_algorithmic",
+                                                                     rl.get("traffic_ratio")),
                "line": line, "profiled_run_line": prof_line}
         if abs(frac_p - pr["frac"]) > 0.02 * pr["frac"]:
             bad.append(f"{cfg}: profiled run's frac {pr['frac']} vs its profile {frac_p:.4f}")
