@@ -286,3 +286,59 @@ def test_c5_subline_plumbing_world4_gloo():
     assert all(o["info"] == {"world_size": 4, "backend": "gloo", "process_group": True}
                for o in out)
     assert all(o["slowest"] == pytest.approx(0.4) for o in out)
+
+
+def _comm_id_worker(rank, world, port, q):
+    """idist.product_comm at world > 1 without a GPU: the library's
+    communicator calls are replaced by recorders, so what is checked is the
+    plumbing around them — rank 0 alone makes the id, every rank creates its
+    communicator with that id, the group's size and its own rank, and fd 1
+    is restored after the stdout redirect around RCCL's init."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import ingot_amd
+
+        made = []
+
+        def fake_id():
+            made.append(rank)
+            return bytes([rank + 1]) * ingot_amd.COMM_ID_BYTES
+
+        class FakeComm:
+            def __init__(self, ctx, nranks, r, uid):
+                self.args = (ctx, nranks, r, uid)
+
+        ingot_amd.comm_unique_id = fake_id
+        ingot_amd.Comm = FakeComm
+        before = os.fstat(1)
+        c = idist.product_comm("ctx")
+        after = os.fstat(1)
+        fd1 = (before.st_dev, before.st_ino) == (after.st_dev, after.st_ino)
+        out = [None] * world
+        dist.all_gather_object(out, (made, c.args[1:], fd1))
+        if rank == 0:
+            q.put(out)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_product_comm_id_exchange_gloo():
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_id_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    uid0 = bytes([1]) * 128
+    for r, (made, (nranks, rank, uid), fd1) in enumerate(out):
+        assert made == ([0] if r == 0 else [])  # only rank 0 makes the id
+        assert (nranks, rank, uid) == (world, r, uid0)
+        assert fd1
