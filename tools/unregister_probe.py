@@ -7,12 +7,18 @@ such a call, whether it still knows the pointer as host memory
 (hipPointerGetAttributes).  No kernel or copy touches the buffer after the
 call, and the process ends with os._exit so torch never frees it.
 
-    python tools/unregister_probe.py
+    python tools/unregister_probe.py [--inner]
 -> one JSON line (also gpurun_out/unregister_probe.json)
+
+--inner: the call on a pointer 4 KiB inside the pinned allocation (a
+sub-range mapping of a pinned ring) instead of its start.  Measured on the
+box: ROCclr aborts the process (device.cpp:359 "Memobj map does not have
+ptr"), exit status 134 — run it last in a command.
 """
 import ctypes
 import json
 import os
+import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
@@ -38,23 +44,15 @@ def main():
         return {"rc": rc, "type": a.type if rc == 0 else None}
 
     torch.cuda.init()
+    inner = "--inner" in sys.argv
     t = torch.empty(1 << 20, dtype=torch.uint8, pin_memory=True)
     p = t.data_ptr()
     before = attr(p)
-    rc = hip.hipHostUnregister(ctypes.c_void_p(p))
+    rc = hip.hipHostUnregister(ctypes.c_void_p(p + (4096 if inner else 0)))
     hip.hipGetLastError()
     after = attr(p)
-    # the same call on a pointer 4 KiB inside the allocation (a sub-range
-    # mapping of a pinned ring)
-    t2 = torch.empty(1 << 20, dtype=torch.uint8, pin_memory=True)
-    p2 = t2.data_ptr()
-    before2 = attr(p2)
-    rc2 = hip.hipHostUnregister(ctypes.c_void_p(p2 + 4096))
-    hip.hipGetLastError()
-    after2 = attr(p2)
-    res = {"hipHostMalloc_start": {"before": before, "hipHostUnregister_rc": rc, "after": after},
-           "hipHostMalloc_inner": {"before": before2, "hipHostUnregister_rc": rc2,
-                                   "after": after2},
+    res = {("hipHostMalloc_inner" if inner else "hipHostMalloc_start"):
+           {"before": before, "hipHostUnregister_rc": rc, "after": after},
            "note": "type 1 = hipMemoryTypeHost; rc 0 = hipSuccess"}
     line = json.dumps(res)
     print(line, flush=True)
