@@ -96,7 +96,8 @@ int ingot_gpu_comm_create(ingot_gpu_ctx* ctx, int nranks, int rank,
 
 void ingot_gpu_comm_destroy(ingot_gpu_comm* comm) {
     if (!comm) return;
-    if (set_device(comm->device) == INGOT_GPU_SUCCESS) (void)rccl().destroy(comm->nccl);
+    (void)set_device(comm->device);
+    (void)rccl().destroy(comm->nccl);
     delete comm;
 }
 
