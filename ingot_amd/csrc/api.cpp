@@ -42,7 +42,7 @@ std::vector<Registration> g_regs;
 }  // namespace
 
 struct ingot_gpu_ctx {
-    int device;
+    int device = 0;
     ingot_gpu::Tuning tuning;
     uint32_t wall_khz = 0;  // the device's constant-rate wall clock (stream delays)
     size_t lds_bytes = 160u * 1024u;  // LDS per workgroup (the device's, at create)
@@ -200,8 +200,9 @@ int ingot_gpu_ctx_create(int device, ingot_gpu_ctx** out) {
     // Code objects are built for gfx950 only.
     if (prop.gcnArchName[0] && std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         return INGOT_GPU_ENODEV;
-    ingot_gpu_ctx* c = new (std::nothrow) ingot_gpu_ctx{device, {}};
+    ingot_gpu_ctx* c = new (std::nothrow) ingot_gpu_ctx();  // value-initialised
     if (!c) return INGOT_GPU_ENOMEM;
+    c->device = device;
     if (prop.multiProcessorCount > 0) c->tuning.cus = (uint32_t)prop.multiProcessorCount;
     int lds = 0;
     if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) ==
@@ -345,7 +346,7 @@ int ingot_gpu_host_unmap(ingot_gpu_ctx* ctx, void* host) {
 // (hipStreamWaitValue32).  Host stores to coherent memory are seen by the
 // device without a flush.
 struct ingot_gpu_doorbell {
-    int device;
+    int device = 0;
     uint32_t* word;
     uint32_t* dword = nullptr;  // the word's device address (ingot_gpu_parse_ring polls it)
 };
@@ -766,8 +767,8 @@ int ingot_gpu_flow_hist_ws(ingot_gpu_ctx* ctx, const uint8_t* d_arena, const uin
     for (uint32_t e = 0; e < 2 * ingot_gpu::FLOW_TAB16_DW; ++e) {
         const uint32_t p = e / 16u, v = e & 15u;
         uint32_t acc = 0;
-        for (uint32_t k = 0; k < 4; ++k)
-            if ((v >> (3u - k)) & 1u) acc ^= a.w[4u * p + k];
+        for (uint32_t j = 0; j < 4; ++j)
+            if ((v >> (3u - j)) & 1u) acc ^= a.w[4u * p + j];
         a.tab16[e / 2] |= (acc & 0xffffu) << (16u * (e & 1u));
     }
     const hipStream_t s = (hipStream_t)stream;
