@@ -1097,6 +1097,11 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+# --rehearse-one-gpu: RCCL over loopback sockets between ranks sharing a GPU
+REHEARSAL_ENV = {"NCCL_P2P_DISABLE": "1", "NCCL_SHM_DISABLE": "1", "NCCL_IB_DISABLE": "1",
+                 "NCCL_SOCKET_IFNAME": "lo"}
+
+
 def launch_ranks(n: int, argv: list) -> int:
     """`--gpus N` without a launcher: start N child processes of this script,
     one per GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* as torchrun sets
@@ -1344,6 +1349,11 @@ def main():
                     help="minimum bytes of distinct arenas rotated across steps")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl = RCCL over xGMI (default); gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="N > 1 ranks on ONE GPU with RCCL: each rank gets its own "
+                         "NCCL_HOSTID and the ranks talk over loopback sockets (P2P, SHM, "
+                         "InfiniBand off), so RCCL accepts them on one device; the N > 1 path "
+                         "runs with real RCCL kernels, the rates mean nothing")
     args = ap.parse_args()
     if args.streams <= 0:
         args.streams = STREAMS.get(args.config, 2)
@@ -1370,6 +1380,11 @@ def main():
     if args.plan:
         plan(args, world, rank)
         return
+    if args.rehearse_one_gpu and world > 1:
+        # before anything initialises RCCL (tests/test_comm_world2.py: the same
+        # settings for the product reduce alone)
+        os.environ.update(REHEARSAL_ENV)
+        os.environ["NCCL_HOSTID"] = f"ingot-rehearsal-rank{rank}"
     # The CPU baselines first, while no GPU runtime or torch thread shares
     # this process's CPU quota: N=1, rank 0.
     args.cpu_pre = {}
@@ -1484,6 +1499,8 @@ def _short_line(line, top):
     d = line.get("distributed") or {}
     chk = d.get("flow_hist_check")
     out["distributed"] = {"world_size": d.get("world_size"), "backend": d.get("backend")}
+    if d.get("rehearsal"):
+        out["distributed"]["rehearsal"] = d["rehearsal"]
     if d.get("collective"):
         out["distributed"]["collective"] = d["collective"][:90]
     if chk:
@@ -2049,6 +2066,9 @@ def run_config(args, config, env):
         },
         "distributed": {
             **idist.world_info(),
+            **({"rehearsal": f"{world} ranks on one GPU, RCCL over loopback sockets "
+                             "(--rehearse-one-gpu): the path runs, the rates mean nothing"}
+               if getattr(args, "rehearse_one_gpu", False) and world > 1 else {}),
             "region_ms_per_rank": [round(x, 5) for x in region_ms_per_rank],
             "collective": ((f"ingot_gpu_flow_hist_allreduce every step: RCCL all-reduce SUM "
                             f"(ncclUint32) of the {FLOW_BINS} x u32 flow histogram over the "

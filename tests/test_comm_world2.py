@@ -20,8 +20,12 @@ import pytest
 
 N = 65_536
 BINS = 1 << 16
-RANK_ENV = {"NCCL_P2P_DISABLE": "1", "NCCL_SHM_DISABLE": "1", "NCCL_IB_DISABLE": "1",
-            "NCCL_SOCKET_IFNAME": "lo"}
+
+
+def _rank_env():
+    import bench
+
+    return bench.REHEARSAL_ENV
 
 
 def _free_port():
@@ -33,7 +37,7 @@ def _free_port():
 
 
 def _worker(rank, world, port, q):
-    os.environ.update(RANK_ENV)
+    os.environ.update(_rank_env())
     os.environ["NCCL_HOSTID"] = f"ingot-rehearsal-rank{rank}"
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
