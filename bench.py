@@ -1097,6 +1097,9 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+# seconds each teardown step of an N > 1 run may take (bench.teardown)
+TEARDOWN_BUDGET_S = 100.0
+
 # --rehearse-one-gpu: RCCL over loopback sockets between ranks sharing a GPU
 REHEARSAL_ENV = {"NCCL_P2P_DISABLE": "1", "NCCL_SHM_DISABLE": "1", "NCCL_IB_DISABLE": "1",
                  "NCCL_SOCKET_IFNAME": "lo"}
@@ -1439,13 +1442,49 @@ def main():
         result["wall_s_command"] = round(time.perf_counter() - T_START, 2)
     if rank == 0:
         print(json.dumps(jsonable(compact_line(result, args.config))), flush=True)
-    comm = getattr(ctx, "_flow_comm", None)
+    teardown(dist, world, getattr(ctx, "_flow_comm", None))
+
+
+def teardown(dist, world, comm, budget_s=None):
+    """End of the run, every step logged on stderr: config 5's communicator,
+    then the process group.  At N > 1 each step gets a time budget: the line
+    is printed and every rank has passed the final barrier, so a library
+    teardown that does not return (seen once in the one-GPU RCCL rehearsal:
+    ncclCommDestroy on both ranks) must not turn a finished run into a hung
+    one — the process then exits 0 without waiting for it."""
+    import threading
+
+    budget = budget_s if budget_s is not None else TEARDOWN_BUDGET_S
+
+    def bounded(what, fn):
+        t0 = time.perf_counter()
+        log(f"[bench] teardown: {what}")
+        if world <= 1:
+            fn()
+            return True
+        th = threading.Thread(target=fn, daemon=True)
+        th.start()
+        th.join(budget)
+        dt = time.perf_counter() - t0
+        if th.is_alive():
+            log(f"[bench] teardown: {what} did not return in {dt:.0f} s; exiting without it")
+            return False
+        log(f"[bench] teardown: {what} took {dt:.2f} s")
+        return True
+
+    ok = True
     if world > 1:
+        log("[bench] teardown: barrier")
         dist.barrier()
     if comm is not None:  # every rank releases config 5's communicator together
-        comm.close()
-    if world > 1:
-        dist.destroy_process_group()
+        ok = bounded("ingot_gpu_comm_destroy", comm.close)
+    if ok and world > 1:
+        ok = bounded("destroy_process_group", dist.destroy_process_group)
+    if not ok:
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
+    log("[bench] teardown: done")
 
 
 def _summary_entry(line):

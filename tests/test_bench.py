@@ -554,3 +554,45 @@ def test_emit_config_stack_and_values():
     p1, v1 = bench.emit_values(500, first=500)
     assert (p0[500:] == p1).all() and (v0[500:] == v1).all()
     assert (p0 >= 0xC000).all() and (v0 < (1 << 24)).all()
+
+
+def test_teardown_is_bounded_at_n_above_one():
+    """bench.teardown at N > 1: a communicator destroy that never returns
+    (seen once in the one-GPU RCCL rehearsal) ends the process with exit
+    status 0 after its budget, the line having been printed; one that
+    returns lets the process group go down normally."""
+    import subprocess
+    import sys
+
+    code = r"""
+import sys, threading, time
+sys.path.insert(0, {root!r})
+import bench
+
+class Dist:
+    def barrier(self): print("barrier", flush=True)
+    def destroy_process_group(self): print("pg destroyed", flush=True)
+
+class Comm:
+    def __init__(self, hang): self.hang = hang
+    def close(self):
+        if self.hang:
+            threading.Event().wait()
+        print("comm closed", flush=True)
+
+print("line", flush=True)
+bench.teardown(Dist(), 2, Comm({hang}), budget_s=0.5)
+print("after teardown", flush=True)
+"""
+    from pathlib import Path
+
+    root = str(Path(bench.__file__).resolve().parent)
+    for hang in (False, True):
+        r = subprocess.run([sys.executable, "-c", code.format(root=root, hang=hang)],
+                           capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0, r.stderr
+        out = r.stdout.split()
+        if hang:
+            assert out == ["line", "barrier"] and "did not return" in r.stderr
+        else:
+            assert "pg" in out and "after" in out and "comm" in out
