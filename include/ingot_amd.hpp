@@ -366,7 +366,9 @@ class Comm {
     Comm(Context& ctx, int nranks, int rank, const Id& id) {
         check(ingot_gpu_comm_create(ctx.get(), nranks, rank, id.data(), &h_), "comm_create");
     }
-    ~Comm() { ingot_gpu_comm_destroy(h_); }
+    ~Comm() {
+        if (h_) (void)ingot_gpu_comm_destroy(h_);
+    }
     Comm(const Comm&) = delete;
     Comm& operator=(const Comm&) = delete;
     int size() const { return ingot_gpu_comm_size(h_); }

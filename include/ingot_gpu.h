@@ -907,6 +907,12 @@ size_t ingot_gpu_flow_hist_workspace_size(uint64_t n, uint32_t bins);
  * `stream`, ordered after the work already enqueued there (e.g. the
  * ingot_gpu_flow_hist that filled it) and before what follows; every rank
  * must enqueue the same sequence of reduces.  The counts wrap modulo 2^32.
+ *
+ * Release: ingot_gpu_comm_destroy on every rank flushes the reduces issued,
+ * waits until the communicator is quiescent on all ranks (ncclCommFinalize)
+ * and frees it; ingot_gpu_comm_abort frees it at once, locally, aborting any
+ * reduce still in flight (error paths, or a process that is exiting after its
+ * streams have drained).  Either way the handle is gone afterwards.
  */
 #define INGOT_GPU_ECOMM (-6)    /* a collective (RCCL) call failed */
 #define INGOT_COMM_ID_BYTES 128
@@ -914,7 +920,8 @@ typedef struct ingot_gpu_comm ingot_gpu_comm;
 int ingot_gpu_comm_unique_id(uint8_t id[INGOT_COMM_ID_BYTES]);
 int ingot_gpu_comm_create(ingot_gpu_ctx* ctx, int nranks, int rank,
                           const uint8_t id[INGOT_COMM_ID_BYTES], ingot_gpu_comm** out);
-void ingot_gpu_comm_destroy(ingot_gpu_comm* comm);
+int ingot_gpu_comm_destroy(ingot_gpu_comm* comm);
+int ingot_gpu_comm_abort(ingot_gpu_comm* comm);
 int ingot_gpu_comm_size(const ingot_gpu_comm* comm);
 int ingot_gpu_comm_rank(const ingot_gpu_comm* comm);
 int ingot_gpu_flow_hist_allreduce(ingot_gpu_comm* comm, uint32_t* d_hist, uint32_t bins,

@@ -717,9 +717,16 @@ class Comm:
         return hist
 
     def close(self) -> None:
+        """ingot_gpu_comm_destroy: every rank together, after its reduces."""
         if getattr(self, "_h", None):
-            self._lib.ingot_gpu_comm_destroy(self._h)
-            self._h = None
+            h, self._h = self._h, None
+            _lib.check(self._lib.ingot_gpu_comm_destroy(h), "ingot_gpu_comm_destroy")
+
+    def abort(self) -> None:
+        """ingot_gpu_comm_abort: local and immediate."""
+        if getattr(self, "_h", None):
+            h, self._h = self._h, None
+            _lib.check(self._lib.ingot_gpu_comm_abort(h), "ingot_gpu_comm_abort")
 
 
 def records_to_numpy(t):

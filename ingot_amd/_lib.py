@@ -130,7 +130,8 @@ SIGNATURES = {
     "ingot_gpu_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
     "ingot_gpu_comm_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
-    "ingot_gpu_comm_destroy": (None, [ctypes.c_void_p]),
+    "ingot_gpu_comm_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "ingot_gpu_comm_abort": (ctypes.c_int, [ctypes.c_void_p]),
     "ingot_gpu_comm_size": (ctypes.c_int, [ctypes.c_void_p]),
     "ingot_gpu_comm_rank": (ctypes.c_int, [ctypes.c_void_p]),
     "ingot_gpu_flow_hist_allreduce": (ctypes.c_int, [ctypes.c_void_p, c_u8p, ctypes.c_uint32,

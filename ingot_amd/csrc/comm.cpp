@@ -31,7 +31,9 @@ namespace {
 struct Rccl {
     decltype(&ncclGetUniqueId) get_unique_id = nullptr;
     decltype(&ncclCommInitRank) init_rank = nullptr;
+    decltype(&ncclCommFinalize) finalize = nullptr;
     decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclCommAbort) abort = nullptr;
     decltype(&ncclAllReduce) all_reduce = nullptr;
     bool ok = false;
 };
@@ -45,9 +47,12 @@ const Rccl& rccl() {
         if (!h) return;
         r.get_unique_id = (decltype(r.get_unique_id))dlsym(h, "ncclGetUniqueId");
         r.init_rank = (decltype(r.init_rank))dlsym(h, "ncclCommInitRank");
+        r.finalize = (decltype(r.finalize))dlsym(h, "ncclCommFinalize");
         r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
+        r.abort = (decltype(r.abort))dlsym(h, "ncclCommAbort");
         r.all_reduce = (decltype(r.all_reduce))dlsym(h, "ncclAllReduce");
-        r.ok = r.get_unique_id && r.init_rank && r.destroy && r.all_reduce;
+        r.ok = r.get_unique_id && r.init_rank && r.finalize && r.destroy && r.abort &&
+               r.all_reduce;
     });
     return r;
 }
@@ -94,11 +99,25 @@ int ingot_gpu_comm_create(ingot_gpu_ctx* ctx, int nranks, int rank,
     return INGOT_GPU_SUCCESS;
 }
 
-void ingot_gpu_comm_destroy(ingot_gpu_comm* comm) {
-    if (!comm) return;
+// Graceful: flush every reduce issued and wait until the communicator is
+// quiescent on all ranks (ncclCommFinalize), then free it locally.
+int ingot_gpu_comm_destroy(ingot_gpu_comm* comm) {
+    if (!comm) return INGOT_GPU_EINVAL;
     (void)set_device(comm->device);
-    (void)rccl().destroy(comm->nccl);
+    const Rccl& r = rccl();
+    const bool ok = r.finalize(comm->nccl) == ncclSuccess;
+    const bool freed = r.destroy(comm->nccl) == ncclSuccess;
     delete comm;
+    return ok && freed ? INGOT_GPU_SUCCESS : INGOT_GPU_ECOMM;
+}
+
+// Local and immediate: reduces still in flight are aborted.
+int ingot_gpu_comm_abort(ingot_gpu_comm* comm) {
+    if (!comm) return INGOT_GPU_EINVAL;
+    (void)set_device(comm->device);
+    const bool ok = rccl().abort(comm->nccl) == ncclSuccess;
+    delete comm;
+    return ok ? INGOT_GPU_SUCCESS : INGOT_GPU_ECOMM;
 }
 
 int ingot_gpu_comm_size(const ingot_gpu_comm* comm) { return comm ? comm->nranks : INGOT_GPU_EINVAL; }

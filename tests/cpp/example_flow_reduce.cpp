@@ -112,7 +112,7 @@ int main() {
                 "histogram total %llu\n",
                 ingot_gpu_comm_size(comm), (unsigned long long)counted,
                 (unsigned long long)ok_l3, (unsigned long long)total);
-    ingot_gpu_comm_destroy(comm);
+    bad += ingot_gpu_comm_destroy(comm) != INGOT_GPU_SUCCESS;
     {  // the same reduce through the C++ mirror (include/ingot_amd.hpp)
         ingot::gpu::Context cctx(0);
         ingot::gpu::Comm c(cctx, 1, 0, ingot::gpu::Comm::unique_id());

@@ -27,7 +27,7 @@ def test_comm_argument_errors():
     assert lib.ingot_gpu_comm_create(None, 1, 0, uid, ctypes.byref(out)) == -1
     assert lib.ingot_gpu_flow_hist_allreduce(None, None, 1 << 16, None) == -1
     assert lib.ingot_gpu_comm_size(None) == -1 and lib.ingot_gpu_comm_rank(None) == -1
-    lib.ingot_gpu_comm_destroy(None)  # a no-op
+    assert lib.ingot_gpu_comm_destroy(None) == -1 and lib.ingot_gpu_comm_abort(None) == -1
     assert lib.ingot_gpu_strerror(-6) == b"collective (RCCL) call failed"
     with pytest.raises(ValueError):
         ingot_amd.Comm(None, 1, 0, b"short")
