@@ -1383,6 +1383,12 @@ def main():
     if args.plan:
         plan(args, world, rank)
         return
+    if world > 1:
+        # a rank that stops making progress shows where, on stderr, every
+        # 150 s (a run at N > 1 takes about a minute)
+        import faulthandler
+
+        faulthandler.dump_traceback_later(150, repeat=True)
     if args.rehearse_one_gpu and world > 1:
         # before anything initialises RCCL (tests/test_comm_world2.py: the same
         # settings for the product reduce alone)
@@ -1476,8 +1482,14 @@ def teardown(dist, world, comm, budget_s=None):
     if world > 1:
         log("[bench] teardown: barrier")
         dist.barrier()
-    if comm is not None:  # every rank releases config 5's communicator together
-        ok = bounded("ingot_gpu_comm_destroy", comm.close)
+    if comm is not None:
+        # every rank's streams have drained: at N > 1 the communicator is
+        # released locally (ingot_gpu_comm_abort — the graceful destroy did
+        # not return in the one-GPU RCCL rehearsal); at N = 1 gracefully
+        if world > 1:
+            ok = bounded("ingot_gpu_comm_abort", comm.abort)
+        else:
+            ok = bounded("ingot_gpu_comm_destroy", comm.close)
     if ok and world > 1:
         ok = bounded("destroy_process_group", dist.destroy_process_group)
     if not ok:
@@ -1485,6 +1497,10 @@ def teardown(dist, world, comm, budget_s=None):
         sys.stderr.flush()
         os._exit(0)
     log("[bench] teardown: done")
+    if world > 1:
+        import faulthandler
+
+        faulthandler.cancel_dump_traceback_later()
 
 
 def _summary_entry(line):

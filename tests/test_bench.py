@@ -575,10 +575,10 @@ class Dist:
 
 class Comm:
     def __init__(self, hang): self.hang = hang
-    def close(self):
+    def abort(self):
         if self.hang:
             threading.Event().wait()
-        print("comm closed", flush=True)
+        print("comm aborted", flush=True)
 
 print("line", flush=True)
 bench.teardown(Dist(), 2, Comm({hang}), budget_s=0.5)
@@ -595,4 +595,4 @@ print("after teardown", flush=True)
         if hang:
             assert out == ["line", "barrier"] and "did not return" in r.stderr
         else:
-            assert "pg" in out and "after" in out and "comm" in out
+            assert "pg" in out and "after" in out and "aborted" in out
