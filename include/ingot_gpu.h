@@ -38,7 +38,10 @@
 extern "C" {
 #endif
 
-#define INGOT_GPU_ABI_VERSION 1
+/* 2: ingot_gpu_comm_* / ingot_gpu_flow_hist_allreduce (config 5's reduce);
+ *    host mappings counted per map, ingot_gpu_host_unmap EINVAL for a pointer
+ *    the context never mapped (1: any pointer, hipHostUnregister'd). */
+#define INGOT_GPU_ABI_VERSION 2
 
 /* ---------------------------------------------------------------------------
  * Per-packet status: 0 = Ok, else 1 + the ParseError discriminant in the
