@@ -1463,9 +1463,18 @@ def teardown(dist, world, comm, budget_s=None):
 
     budget = budget_s if budget_s is not None else TEARDOWN_BUDGET_S
 
+    def guarded(what, fn):
+        def run():
+            try:
+                fn()
+            except Exception as e:  # noqa: BLE001 — the run is finished; say so and go on
+                log(f"[bench] teardown: {what} failed: {e}")
+        return run
+
     def bounded(what, fn):
         t0 = time.perf_counter()
         log(f"[bench] teardown: {what}")
+        fn = guarded(what, fn)
         if world <= 1:
             fn()
             return True
