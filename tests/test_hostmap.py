@@ -176,15 +176,18 @@ def test_parse_modify_in_host_memory(torch, ctx, stride):
     want = h_arena.numpy().copy()
     e = edits_array(edits)
     d_arena = ctx.host_map(h_arena)
+    mapped = [h_arena]
     if stride:
         h_lens = _pinned(torch, lens) if lens is not None else None
         d_lens = ctx.host_map(h_lens) if h_lens is not None else None
+        mapped += [h_lens] if h_lens is not None else []
         rc = lib.ingot_gpu_parse_modify(ctx._h, d_arena, None, d_lens, stride, n,
                                         int(Chain.UdpParser), e.ctypes.data, len(e), None, None)
         l_np = None if lens is None else lens.cpu().numpy()
         oracle.parse_modify_batch(want, None, l_np, Chain.UdpParser, edits, stride=stride, n=n)
     else:
         h_off, h_lens = _pinned(torch, off), _pinned(torch, lens)
+        mapped += [h_off, h_lens]
         rc = lib.ingot_gpu_parse_modify(ctx._h, d_arena, ctx.host_map(h_off),
                                         ctx.host_map(h_lens), 0, n, int(Chain.UdpParser),
                                         e.ctypes.data, len(e), None, None)
@@ -192,6 +195,8 @@ def test_parse_modify_in_host_memory(torch, ctx, stride):
                                   edits)
     assert rc == 0
     torch.cuda.synchronize()
+    for h in mapped:
+        ctx.host_unmap(h)
     got = h_arena.numpy()
     diff = np.nonzero(got != want)[0]
     assert diff.size == 0, (diff[:10], got[diff[:10]], want[diff[:10]])
@@ -217,6 +222,8 @@ def test_parse_packed_from_host_capture_buffer(torch, ctx):
                                     ctx.host_map(h_off), work.data_ptr(), wb, None)
     assert rc == 0
     torch.cuda.synchronize()
+    for h in (h_arena, h_lens, h_out, h_off):
+        ctx.host_unmap(h)
     assert h_out.numpy().tobytes() == want.cpu().numpy().tobytes()
     assert (h_off.numpy() == off.cpu().numpy()).all()
 
