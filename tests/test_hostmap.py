@@ -348,3 +348,32 @@ def test_mapping_lifecycle_then_pageable_copies(torch, ctx):
         assert np.array_equal(rec_dev.cpu().numpy(), first_rec)
         assert np.array_equal(boff.cpu().numpy()[-5:], boff[-5:].cpu().numpy())
     torch.cuda.synchronize()
+
+
+def test_registration_shared_across_contexts(torch, ctx):
+    """Registrations are per process: a pageable buffer mapped by two
+    contexts is registered once, stays registered while either mapping
+    lives, and each context unmaps only its own mapping."""
+    lib = _lib.load()
+    hip = _hip()
+    n = 5000
+    arena, off, lens = ingot_amd.gen_frames(GenProfile.MIXED, n, seed=9)
+    want = ctx.parse(arena, off, lens, Chain.GenericUlp).cpu().numpy()
+    raw = np.zeros(arena.numel() + 8192, np.uint8)
+    a = raw[(-raw.ctypes.data) % 4096:][:arena.numel()]
+    a[:] = arena.cpu().numpy()
+    other = ingot_amd.Context(0)
+    da, db = ctx.host_map(a), other.host_map(a)
+    assert da == db and _registered(hip, a.ctypes.data)
+    assert lib.ingot_gpu_host_unmap(other._h, a.ctypes.data + 64) == -1  # not a mapping start
+    ctx.host_unmap(a)
+    assert _registered(hip, a.ctypes.data)  # the other context's mapping keeps it
+    out = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
+    assert lib.ingot_gpu_parse(other._h, db, off.data_ptr(), lens.data_ptr(), n,
+                               int(Chain.GenericUlp), out.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    assert out.cpu().numpy().tobytes() == want.tobytes()
+    assert lib.ingot_gpu_host_unmap(ctx._h, a.ctypes.data) == -1  # ctx holds no mapping now
+    other.host_unmap(a)
+    assert not _registered(hip, a.ctypes.data)
+    other.close()
