@@ -89,6 +89,26 @@ def test_allreduce_argument_errors(torch, comm):
 
 
 @pytest.mark.gpu
+def test_comm_create_argument_errors(torch, ctx):
+    import ctypes
+
+    lib = _lib.load()
+    a, b = ingot_amd.comm_unique_id(), ingot_amd.comm_unique_id()
+    assert a != b  # a fresh id per call
+    buf = (ctypes.c_uint8 * ingot_amd.COMM_ID_BYTES).from_buffer_copy(a)
+    out = ctypes.c_void_p()
+    for nranks, rank in ((0, 0), (1, 1), (2, -1), (2, 2)):
+        assert lib.ingot_gpu_comm_create(ctx._h, nranks, rank, buf, ctypes.byref(out)) == -1
+        assert not out.value
+    assert lib.ingot_gpu_comm_create(ctx._h, 1, 0, None, ctypes.byref(out)) == -1
+    assert lib.ingot_gpu_comm_create(ctx._h, 1, 0, buf, None) == -1
+    # abort releases a one-rank communicator at once
+    c = ingot_amd.Comm(ctx, 1, 0, b)
+    c.abort()
+    c.abort()  # the handle is gone: a no-op
+
+
+@pytest.mark.gpu
 def test_flow_runner_until_collective_with_the_product_reduce(torch, ctx, comm):
     """bench.py's config-5 step (flow kernel, histogram pass, then the reduce
     through ingot_gpu_flow_hist_allreduce) under gate_policy
