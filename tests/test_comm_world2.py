@@ -49,7 +49,15 @@ def _worker(rank, world, port, q):
     from ingot_amd import Chain, GenProfile
     from ingot_amd import dist as idist
 
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # INGOT_WORLD2_PG=nccl: the torch group over RCCL too (two communicators
+    # per process, as bench.py has at N > 1); default gloo
+    backend = os.environ.get("INGOT_WORLD2_PG", "gloo")
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda:0"))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     res = {"rank": rank}
     try:
         ctx = ingot_amd.Context(0)
