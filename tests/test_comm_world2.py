@@ -37,6 +37,9 @@ def _free_port():
 
 
 def _worker(rank, world, port, q):
+    import faulthandler
+
+    faulthandler.dump_traceback_later(40, repeat=True)  # a stalled rank shows where
     os.environ.update(_rank_env())
     os.environ["NCCL_HOSTID"] = f"ingot-rehearsal-rank{rank}"
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -109,6 +112,7 @@ def _worker(rank, world, port, q):
                          "check": idist.flow_hist_check(hists[last], flows[last], ok_l3, BINS),
                          "hist": hists[last].cpu().numpy().view(np.uint32).copy()}
         comm.close()
+        res["closed"] = True
     except Exception as e:  # reported to the test, which fails on it
         res["error"] = repr(e)
     out = [None] * world
