@@ -1353,6 +1353,12 @@ def main():
                     help="minimum bytes of distinct arenas rotated across steps")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl = RCCL over xGMI (default); gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--group-backend", default="gloo", choices=("gloo", "nccl"),
+                    help="backend of the torch.distributed group at N > 1, which carries only "
+                         "control (the communicator id, barriers, max over ranks, checks); "
+                         "config 5's reduce is the library's own RCCL communicator either way. "
+                         "gloo (default): one RCCL communicator per process; nccl: torch's "
+                         "group is a second one (DESIGN.md §6)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="N > 1 ranks on ONE GPU with RCCL: each rank gets its own "
                          "NCCL_HOSTID and the ranks talk over loopback sockets (P2P, SHM, "
@@ -1422,11 +1428,15 @@ def main():
         # RCCL prints a version banner on stdout when a communicator comes up:
         # keep it off the one-line stdout (eager init with device_id, then a
         # barrier, inside the redirect)
+        # The group carries control only; config 5's device reduce is the
+        # library's communicator.  Over gloo (the default) each process holds
+        # one RCCL communicator, not two (the world-2 rehearsal
+        # stalled with torch's group on RCCL as well).
         with _stdout_to_stderr():
-            if args.dist_backend == "nccl":
+            if args.dist_backend == "nccl" and args.group_backend == "nccl":
                 dist.init_process_group("nccl", device_id=dev)
             else:
-                dist.init_process_group(args.dist_backend)
+                dist.init_process_group("gloo")
             dist.barrier()
     ctx = ingot_amd.Context(local)
     from ingot_amd import abi
@@ -1564,6 +1574,8 @@ def _short_line(line, top):
     d = line.get("distributed") or {}
     chk = d.get("flow_hist_check")
     out["distributed"] = {"world_size": d.get("world_size"), "backend": d.get("backend")}
+    if d.get("group"):
+        out["distributed"]["group"] = "control only"
     if d.get("rehearsal"):
         out["distributed"]["rehearsal"] = d["rehearsal"]
     if d.get("collective"):
@@ -2131,6 +2143,10 @@ def run_config(args, config, env):
         },
         "distributed": {
             **idist.world_info(),
+            **({"group": ("torch.distributed group: control only (communicator id, barriers, "
+                          "max over ranks, checks); the data-path reduce is "
+                          + ("RCCL" if args.dist_backend == "nccl" else "gloo"))}
+               if world > 1 else {}),
             **({"rehearsal": f"{world} ranks on one GPU, RCCL over loopback sockets "
                              "(--rehearse-one-gpu): the path runs, the rates mean nothing"}
                if getattr(args, "rehearse_one_gpu", False) and world > 1 else {}),
