@@ -366,6 +366,11 @@ class Comm {
     Comm(Context& ctx, int nranks, int rank, const Id& id) {
         check(ingot_gpu_comm_create(ctx.get(), nranks, rank, id.data(), &h_), "comm_create");
     }
+    // The host's own RCCL communicator (an ncclComm_t), borrowed: it stays
+    // the host's and must outlive this object.
+    Comm(Context& ctx, void* nccl_comm) {
+        check(ingot_gpu_comm_wrap(ctx.get(), nccl_comm, &h_), "comm_wrap");
+    }
     ~Comm() {
         if (h_) (void)ingot_gpu_comm_destroy(h_);
     }

@@ -38,10 +38,11 @@
 extern "C" {
 #endif
 
-/* 2: ingot_gpu_comm_* / ingot_gpu_flow_hist_allreduce (config 5's reduce);
+/* 3: ingot_gpu_comm_wrap (borrow the host's RCCL communicator).
+ * 2: ingot_gpu_comm_* / ingot_gpu_flow_hist_allreduce (config 5's reduce);
  *    host mappings counted per map, ingot_gpu_host_unmap EINVAL for a pointer
  *    the context never mapped (1: any pointer, hipHostUnregister'd). */
-#define INGOT_GPU_ABI_VERSION 2
+#define INGOT_GPU_ABI_VERSION 3
 
 /* ---------------------------------------------------------------------------
  * Per-packet status: 0 = Ok, else 1 + the ParseError discriminant in the
@@ -916,6 +917,16 @@ size_t ingot_gpu_flow_hist_workspace_size(uint64_t n, uint32_t bins);
  * and frees it; ingot_gpu_comm_abort frees it at once, locally, aborting any
  * reduce still in flight (error paths, or a process that is exiting after its
  * streams have drained).  Either way the handle is gone afterwards.
+ *
+ * A host that already holds an RCCL communicator over the same ranks (its
+ * own, or PyTorch's ProcessGroupNCCL) hands it over with ingot_gpu_comm_wrap
+ * instead of creating a second one: one RCCL communicator per process is the
+ * layout that ran clean (with two per process the world-2
+ * rehearsal stalled).  `nccl_comm` is an ncclComm_t of the process's
+ * librccl.so.1; the handle borrows it: size and rank are the communicator's,
+ * its device must be ctx's (else INGOT_GPU_EINVAL), and
+ * ingot_gpu_comm_destroy / _abort free only the handle — the borrowed
+ * communicator stays the host's and must outlive the handle.
  */
 #define INGOT_GPU_ECOMM (-6)    /* a collective (RCCL) call failed */
 #define INGOT_COMM_ID_BYTES 128
@@ -923,6 +934,7 @@ typedef struct ingot_gpu_comm ingot_gpu_comm;
 int ingot_gpu_comm_unique_id(uint8_t id[INGOT_COMM_ID_BYTES]);
 int ingot_gpu_comm_create(ingot_gpu_ctx* ctx, int nranks, int rank,
                           const uint8_t id[INGOT_COMM_ID_BYTES], ingot_gpu_comm** out);
+int ingot_gpu_comm_wrap(ingot_gpu_ctx* ctx, void* nccl_comm, ingot_gpu_comm** out);
 int ingot_gpu_comm_destroy(ingot_gpu_comm* comm);
 int ingot_gpu_comm_abort(ingot_gpu_comm* comm);
 int ingot_gpu_comm_size(const ingot_gpu_comm* comm);

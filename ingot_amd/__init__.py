@@ -698,10 +698,46 @@ class Comm:
         buf = (ctypes.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
         _lib.check(self._lib.ingot_gpu_comm_create(ctx._h, int(nranks), int(rank), buf,
                                                    ctypes.byref(h)), "ingot_gpu_comm_create")
+        self._bind(h, ctx)
+
+    def _bind(self, h, ctx, owner=None):
         self._h = h
+        self._owner = owner  # a borrowed communicator's owner, kept alive
         self.device = ctx.device
         self.size = int(self._lib.ingot_gpu_comm_size(h))
         self.rank = int(self._lib.ingot_gpu_comm_rank(h))
+
+    @classmethod
+    def wrap(cls, ctx: Context, nccl_comm: int, owner=None) -> "Comm":
+        """ingot_gpu_comm_wrap: borrow an RCCL communicator the process
+        already holds (an ncclComm_t address) instead of creating a second
+        one; close()/abort() release only the handle.  `owner` is kept alive
+        with it."""
+        self = cls.__new__(cls)
+        self._lib = _lib.load()
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.ingot_gpu_comm_wrap(ctx._h, ctypes.c_void_p(int(nccl_comm)),
+                                                 ctypes.byref(h)), "ingot_gpu_comm_wrap")
+        self._bind(h, ctx, owner)
+        return self
+
+    @classmethod
+    def from_process_group(cls, ctx: Context, group=None) -> "Comm":
+        """The communicator of torch.distributed's RCCL group (the default
+        group unless `group`) on ctx's device, borrowed: one RCCL
+        communicator per process.  The group must be up on
+        that device (init_process_group(..., device_id=...) or a first
+        collective) and must outlive the handle."""
+        torch = _torch()
+        import torch.distributed as dist
+
+        pg = group if group is not None else dist.group.WORLD
+        backend = pg._get_backend(torch.device("cuda", ctx.device))
+        ptr = backend._comm_ptr()
+        if not ptr:
+            raise RuntimeError("the process group has no RCCL communicator on "
+                               f"cuda:{ctx.device} yet")
+        return cls.wrap(ctx, ptr, owner=pg)
 
     def allreduce_hist(self, hist, stream=None):
         """ingot_gpu_flow_hist_allreduce: in-place sum of a (bins,) u32 / i32

@@ -130,6 +130,8 @@ SIGNATURES = {
     "ingot_gpu_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
     "ingot_gpu_comm_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "ingot_gpu_comm_wrap": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.POINTER(ctypes.c_void_p)]),
     "ingot_gpu_comm_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "ingot_gpu_comm_abort": (ctypes.c_int, [ctypes.c_void_p]),
     "ingot_gpu_comm_size": (ctypes.c_int, [ctypes.c_void_p]),

@@ -10,7 +10,7 @@ import enum
 
 import numpy as np
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class ParseError(enum.IntEnum):

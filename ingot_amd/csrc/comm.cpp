@@ -24,6 +24,7 @@ static_assert(NCCL_UNIQUE_ID_BYTES == INGOT_COMM_ID_BYTES, "communicator id size
 struct ingot_gpu_comm {
     ncclComm_t nccl;
     int device, nranks, rank;
+    bool owned;  // false: borrowed by ingot_gpu_comm_wrap, never finalized here
 };
 
 namespace {
@@ -35,6 +36,9 @@ struct Rccl {
     decltype(&ncclCommDestroy) destroy = nullptr;
     decltype(&ncclCommAbort) abort = nullptr;
     decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclCommCount) count = nullptr;
+    decltype(&ncclCommUserRank) user_rank = nullptr;
+    decltype(&ncclCommCuDevice) cu_device = nullptr;
     bool ok = false;
 };
 
@@ -51,8 +55,11 @@ const Rccl& rccl() {
         r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
         r.abort = (decltype(r.abort))dlsym(h, "ncclCommAbort");
         r.all_reduce = (decltype(r.all_reduce))dlsym(h, "ncclAllReduce");
+        r.count = (decltype(r.count))dlsym(h, "ncclCommCount");
+        r.user_rank = (decltype(r.user_rank))dlsym(h, "ncclCommUserRank");
+        r.cu_device = (decltype(r.cu_device))dlsym(h, "ncclCommCuDevice");
         r.ok = r.get_unique_id && r.init_rank && r.finalize && r.destroy && r.abort &&
-               r.all_reduce;
+               r.all_reduce && r.count && r.user_rank && r.cu_device;
     });
     return r;
 }
@@ -90,7 +97,7 @@ int ingot_gpu_comm_create(ingot_gpu_ctx* ctx, int nranks, int rank,
     std::memcpy(u.internal, id, INGOT_COMM_ID_BYTES);
     ncclComm_t c = nullptr;
     if (r.init_rank(&c, nranks, u, rank) != ncclSuccess) return INGOT_GPU_ECOMM;
-    ingot_gpu_comm* comm = new (std::nothrow) ingot_gpu_comm{c, device, nranks, rank};
+    ingot_gpu_comm* comm = new (std::nothrow) ingot_gpu_comm{c, device, nranks, rank, true};
     if (!comm) {
         (void)r.destroy(c);
         return INGOT_GPU_ENOMEM;
@@ -99,10 +106,35 @@ int ingot_gpu_comm_create(ingot_gpu_ctx* ctx, int nranks, int rank,
     return INGOT_GPU_SUCCESS;
 }
 
+// The host's own communicator, borrowed: its size, rank and device are
+// asked of RCCL, and the device must be the context's.
+int ingot_gpu_comm_wrap(ingot_gpu_ctx* ctx, void* nccl_comm, ingot_gpu_comm** out) {
+    if (!ctx || !nccl_comm || !out) return INGOT_GPU_EINVAL;
+    *out = nullptr;
+    const Rccl& r = rccl();
+    if (!r.ok) return INGOT_GPU_ENODEV;
+    ncclComm_t c = (ncclComm_t)nccl_comm;
+    int nranks = 0, rank = -1, device = -1;
+    if (r.count(c, &nranks) != ncclSuccess || r.user_rank(c, &rank) != ncclSuccess ||
+        r.cu_device(c, &device) != ncclSuccess)
+        return INGOT_GPU_ECOMM;
+    if (device != ingot_gpu_ctx_device(ctx) || nranks < 1 || rank < 0 || rank >= nranks)
+        return INGOT_GPU_EINVAL;
+    ingot_gpu_comm* comm = new (std::nothrow) ingot_gpu_comm{c, device, nranks, rank, false};
+    if (!comm) return INGOT_GPU_ENOMEM;
+    *out = comm;
+    return INGOT_GPU_SUCCESS;
+}
+
 // Graceful: flush every reduce issued and wait until the communicator is
-// quiescent on all ranks (ncclCommFinalize), then free it locally.
+// quiescent on all ranks (ncclCommFinalize), then free it locally.  A
+// borrowed communicator is left to its owner.
 int ingot_gpu_comm_destroy(ingot_gpu_comm* comm) {
     if (!comm) return INGOT_GPU_EINVAL;
+    if (!comm->owned) {
+        delete comm;
+        return INGOT_GPU_SUCCESS;
+    }
     (void)set_device(comm->device);
     const Rccl& r = rccl();
     const bool ok = r.finalize(comm->nccl) == ncclSuccess;
@@ -114,6 +146,10 @@ int ingot_gpu_comm_destroy(ingot_gpu_comm* comm) {
 // Local and immediate: reduces still in flight are aborted.
 int ingot_gpu_comm_abort(ingot_gpu_comm* comm) {
     if (!comm) return INGOT_GPU_EINVAL;
+    if (!comm->owned) {
+        delete comm;
+        return INGOT_GPU_SUCCESS;
+    }
     (void)set_device(comm->device);
     const bool ok = rccl().abort(comm->nccl) == ncclSuccess;
     delete comm;

@@ -158,16 +158,19 @@ def reduce_histogram_async(hist):
 
 
 def product_comm(ctx):
-    """The library's own communicator for config 5's reduce
-    (ingot_gpu_comm_create behind the C ABI), over the same ranks as the
-    torch.distributed group: rank 0 makes the id and the group carries its
-    128 bytes to every rank.  World 1 (no group): a one-rank communicator, so
-    the reduce is the same RCCL call at every N."""
+    """The communicator of config 5's reduce, over the same ranks as the
+    torch.distributed group.  A group over RCCL lends its own communicator
+    (ingot_gpu_comm_wrap): one RCCL communicator per process, never two
+    (DESIGN.md §6).  A gloo group carries rank 0's 128-byte id to every rank
+    for the library's own (ingot_gpu_comm_create).  World 1 (no group): a
+    one-rank communicator, so the reduce is the same RCCL call at every N."""
     import torch.distributed as dist
 
     import ingot_amd
 
     with _stdout_to_stderr():  # RCCL prints its version banner on stdout
+        if _active() and not _gloo():
+            return ingot_amd.Comm.from_process_group(ctx)
         if _active():
             obj = [ingot_amd.comm_unique_id() if dist.get_rank() == 0 else None]
             dist.broadcast_object_list(obj, src=0)

@@ -28,6 +28,7 @@ def test_comm_argument_errors():
     assert lib.ingot_gpu_flow_hist_allreduce(None, None, 1 << 16, None) == -1
     assert lib.ingot_gpu_comm_size(None) == -1 and lib.ingot_gpu_comm_rank(None) == -1
     assert lib.ingot_gpu_comm_destroy(None) == -1 and lib.ingot_gpu_comm_abort(None) == -1
+    assert lib.ingot_gpu_comm_wrap(None, None, ctypes.byref(out)) == -1
     assert lib.ingot_gpu_strerror(-6) == b"collective (RCCL) call failed"
     with pytest.raises(ValueError):
         ingot_amd.Comm(None, 1, 0, b"short")
@@ -157,3 +158,47 @@ def test_flow_runner_until_collective_with_the_product_reduce(torch, ctx, comm):
     w_hist, _ = oracle.flow_hist(arena.cpu().numpy(), off.cpu().numpy(), lens.cpu().numpy(),
                                  Chain.VlanUlp, n=n, bins=bins)
     assert (hists[last].cpu().numpy().view(np.uint32) == w_hist).all()
+
+
+@pytest.mark.gpu
+def test_borrowed_process_group_communicator(torch, ctx):
+    """ingot_gpu_comm_wrap: the reduce over the communicator of torch's own
+    RCCL group (one communicator per process).  Releasing the
+    handle leaves the group's communicator working."""
+    import torch.distributed as dist
+
+    from ingot_amd import dist as idist
+
+    lib = _lib.load()
+    out = ctypes.c_void_p()
+    assert lib.ingot_gpu_comm_wrap(ctx._h, None, ctypes.byref(out)) == -1
+    assert not dist.is_initialized()
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1,
+                            device_id=torch.device("cuda:0"))
+    try:
+        c = ingot_amd.Comm.from_process_group(ctx)
+        assert (c.size, c.rank) == (1, 0)
+        ptr = dist.group.WORLD._get_backend(torch.device("cuda:0"))._comm_ptr()
+        assert lib.ingot_gpu_comm_wrap(ctx._h, ctypes.c_void_p(ptr), None) == -1
+        n, bins = 100_000, 1 << 16
+        arena, off, lens = ingot_amd.gen_frames(GenProfile.FLOWS, n, seed=5)
+        hist = torch.zeros(bins, dtype=torch.int32, device="cuda")
+        ctx.flow_hist(arena, off, lens, Chain.VlanUlp, hist=hist, n=n)
+        c.allreduce_hist(hist)
+        torch.cuda.synchronize()
+        w_hist, _ = oracle.flow_hist(arena.cpu().numpy(), off.cpu().numpy(),
+                                     lens.cpu().numpy(), Chain.VlanUlp, n=n, bins=bins)
+        assert (hist.cpu().numpy().view(np.uint32) == w_hist).all()
+        c.close()  # the handle only
+        c.close()
+        t = torch.ones(4, device="cuda")
+        dist.all_reduce(t)  # the group's communicator still works
+        torch.cuda.synchronize()
+        assert t.tolist() == [1.0] * 4
+        # bench's product_comm at world 1 with a group: its own one-rank
+        # communicator (a group of one is not "active")
+        c1 = idist.product_comm(ctx)
+        assert (c1.size, c1.rank) == (1, 0)
+        c1.close()
+    finally:
+        dist.destroy_process_group()

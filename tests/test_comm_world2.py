@@ -52,8 +52,9 @@ def _worker(rank, world, port, q):
     from ingot_amd import Chain, GenProfile
     from ingot_amd import dist as idist
 
-    # INGOT_WORLD2_PG=nccl: the torch group over RCCL too (two communicators
-    # per process, as bench.py has at N > 1); default gloo
+    # INGOT_WORLD2_PG=nccl: the torch group over RCCL, whose communicator
+    # product_comm borrows (ingot_gpu_comm_wrap, still one per process);
+    # default gloo
     backend = os.environ.get("INGOT_WORLD2_PG", "gloo")
     if backend == "nccl":
         torch.cuda.set_device(0)
