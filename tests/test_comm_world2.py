@@ -11,7 +11,11 @@ ingot_gpu_comm_create at world 2, ingot_gpu_flow_hist_allreduce of each
 rank's flow-kernel histogram (its contiguous shard of the C5 stream), and
 bench.py's C5 FlowRunner under gate_policy "until_collective" — every reduce
 issued after the region's doorbell, no rank left waiting.  The reduced
-histogram equals the oracle's histogram of both shards, bin for bin."""
+histogram equals the oracle's histogram of both shards, bin for bin.
+
+INGOT_WORLD2_PG=nccl runs the torch group over RCCL instead, and
+product_comm then borrows its communicator (ingot_gpu_comm_wrap): one RCCL
+communicator per process either way (DESIGN.md §6 has why)."""
 import os
 import socket
 
