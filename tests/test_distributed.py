@@ -342,3 +342,31 @@ def test_product_comm_id_exchange_gloo():
         assert made == ([0] if r == 0 else [])  # only rank 0 makes the id
         assert (nranks, rank, uid) == (world, r, uid0)
         assert fd1
+
+
+def test_product_comm_borrows_an_rccl_groups_communicator(monkeypatch):
+    """A torch group over RCCL lends its communicator (Comm.from_process_group
+    -> ingot_gpu_comm_wrap): no id is made and no second communicator is
+    created.  The group's state is faked; the GPU side is
+    tests/test_comm.py::test_borrowed_process_group_communicator."""
+    import ingot_amd
+
+    calls = []
+
+    class FakeComm:
+        def __init__(self, *a):
+            calls.append(("create", a))
+
+        @classmethod
+        def from_process_group(cls, ctx, group=None):
+            calls.append(("borrow", ctx))
+            return "borrowed"
+
+    monkeypatch.setattr(idist, "_active", lambda: True)
+    monkeypatch.setattr(idist, "_gloo", lambda: False)
+    monkeypatch.setattr(ingot_amd, "Comm", FakeComm)
+    monkeypatch.setattr(ingot_amd, "comm_unique_id",
+                        lambda: calls.append(("id",)) or b"\0" * 128)
+    assert idist.product_comm("ctx") == "borrowed"
+    assert calls == [("borrow", "ctx")]
+
