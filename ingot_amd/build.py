@@ -129,6 +129,8 @@ def build_cpp_tests(verbose: bool = False) -> list[Path]:
             continue
         cmd = [hipcc(), "-std=c++17", "-O2", f"-I{ROOT / 'include'}", str(src),
                f"-L{LIB.parent}", "-lingot_gpu", "-Wl,-rpath,$ORIGIN/../../../ingot_amd/lib",
+               # example_flow_reduce makes an RCCL communicator of its own
+               "-L/opt/rocm/lib", "-Wl,--as-needed", "-lrccl",
                "-o", str(exe)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:

@@ -91,3 +91,59 @@ def test_cpp_flow_reduce_example_on_device():
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 mismatches" in r.stdout and "rccl reduce over 1 rank(s)" in r.stdout
+    assert "lent communicator: reduce ok" in r.stdout
+
+
+@pytest.mark.gpu
+def test_cpp_flow_reduce_world2_on_one_gpu(tmp_path):
+    """The same C-ABI-only host at world 2: two processes of
+    example_flow_reduce, rank 0's communicator id carried in a file, each rank
+    counting its contiguous shard of 262,144 frames.  Both ranks share the
+    box's one GPU (bench.REHEARSAL_ENV + a host id per rank, as
+    tests/test_comm_world2.py).  Every rank's reduced histogram equals the sum
+    of the ranks' own bincounts and the oracle's histogram of both shards."""
+    import os
+
+    import numpy as np
+    import torch
+
+    import bench
+    import oracle
+    from ingot_amd import Chain, GenProfile
+    from ingot_amd.hostgen import gen_frames_host
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    exe = ROOT / "tests" / "cpp" / "build" / "example_flow_reduce"
+    if not exe.exists():
+        from ingot_amd.build import build_cpp_tests
+
+        build_cpp_tests()
+    world, n, bins = 2, 1 << 18, 1 << 16
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, **bench.REHEARSAL_ENV, NCCL_HOSTID=f"ingot-cpp-rank{r}")
+        procs.append(subprocess.Popen([str(exe), str(world), str(r), str(tmp_path)], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                      text=True))
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=100)[0])
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    print("\n".join(outs))
+    assert [p.returncode for p in procs] == [0] * world, outs
+    local = sum(np.fromfile(tmp_path / f"local.{r}", dtype=np.uint32).astype(np.int64)
+                for r in range(world))
+    want = np.zeros(bins, np.uint32)
+    for r in range(world):
+        a, o, ln = gen_frames_host(GenProfile.FLOWS, n, first=r * n)
+        oracle.flow_hist(a, o, ln, Chain.VlanUlp, bins=bins, hist=want)
+    assert want.sum() > 0 and (local == want).all()
+    for r in range(world):
+        got = np.fromfile(tmp_path / f"hist.{r}", dtype=np.uint32)
+        assert (got == want).all()
