@@ -85,6 +85,12 @@ def test_allreduce_argument_errors(torch, comm):
     h = torch.zeros(1000, dtype=torch.int32, device="cuda")
     assert lib.ingot_gpu_flow_hist_allreduce(comm._h, h.data_ptr(), 1000, None) == -5
     assert lib.ingot_gpu_flow_hist_allreduce(comm._h, None, 1024, None) == -1
+    assert lib.ingot_gpu_flow_hist_allreduce(comm._h, h.data_ptr(), 1 << 25, None) == -5
+    assert lib.ingot_gpu_flow_hist_allreduce(comm._h, h.data_ptr(), 0, None) == -5
+    big = torch.ones(1 << 24, dtype=torch.int32, device="cuda")  # the largest table
+    comm.allreduce_hist(big)
+    torch.cuda.synchronize()
+    assert int(big.sum()) == 1 << 24
     with pytest.raises(ValueError):
         comm.allreduce_hist(torch.zeros(1024, dtype=torch.int64, device="cuda"))
 
