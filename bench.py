@@ -1359,6 +1359,9 @@ def main():
                          "config 5's reduce is the library's own RCCL communicator either way. "
                          "gloo (default): one RCCL communicator per process; nccl: torch's "
                          "group is a second one (DESIGN.md §6)")
+    ap.add_argument("--subline-budget-s", type=float, default=SUBLINE_BUDGET_S,
+                    help="N > 1: seconds the sub-lines may take before the line is printed "
+                         "without the unfinished ones (SublineGuard)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="N > 1 ranks on ONE GPU with RCCL: each rank gets its own "
                          "NCCL_HOSTID and the ranks talk over loopback sockets (P2P, SHM, "
@@ -1453,7 +1456,26 @@ def main():
     # the same rules with its own roofline and CPU baseline.  C4 and C5 are
     # weak-scaled at 8,388,608 frames per GPU: at N = 8 exactly the 64 M-frame
     # jobs BASELINE.json names.
-    subs = run_sublines(args, env, run_config, torch.cuda.empty_cache)
+    done = {}
+    guard = None
+    if world > 1 and subline_names(args):
+        names = subline_names(args)
+
+        def emit_partial():
+            log(f"[bench] sub-lines not finished after {args.subline_budget_s:g} s at N = {world}: "
+                "printing the line without them")
+            if rank == 0 and result is not None:
+                result["sublines"] = {k: v for k, v in done.items() if v is not None}
+                result["sublines_unfinished"] = {
+                    k: f"not finished within {args.subline_budget_s:g} s at N = {world}"
+                    for k in names if k not in done}
+                result["wall_s_command"] = round(time.perf_counter() - T_START, 2)
+                print(json.dumps(jsonable(compact_line(result, args.config))), flush=True)
+
+        guard = SublineGuard(args.subline_budget_s, emit_partial).start()
+    subs = run_sublines(args, env, run_config, torch.cuda.empty_cache, out=done)
+    if guard is not None and not guard.finish():
+        time.sleep(3600)  # the guard is printing the line and ending the process
     if result is not None and subs is not None:
         result["sublines"] = subs
         result["wall_s_command"] = round(time.perf_counter() - T_START, 2)
@@ -1621,6 +1643,8 @@ def compact_line(result, name):
             summary[k]["over_plain_parse"] = pp["flows_over_plain"]
     if result.get("wall_s_command") is not None:
         out["wall_s_command"] = result["wall_s_command"]
+    if result.get("sublines_unfinished"):
+        out["sublines_unfinished"] = result["sublines_unfinished"]
     out["summary"] = summary
     out["full"] = "gpurun_out/bench_full.json"
     return out
@@ -1647,16 +1671,66 @@ def subline_names(args) -> list:
 SUBLINE_WARMUP = 50
 
 
-def run_sublines(args, env, run, release=lambda: None):
+# N > 1: seconds the sub-lines may take, all together, before the line is
+# printed without those not finished (SublineGuard)
+SUBLINE_BUDGET_S = 150.0
+
+
+class SublineGuard:
+    """At N > 1 the default line's main config (C2, no collective) is
+    measured before its sub-lines, and C5's sub-line issues an RCCL
+    all-reduce every step.  Should a collective never complete (DESIGN.md
+    §6: seen only with two ranks sharing one GPU), the measured line must
+    still be printed: after `budget_s` this guard calls `emit` (rank 0 prints
+    the line with the sub-lines finished so far) and ends the process with
+    status 0.  finish() claims the line for the main thread; False means the
+    guard has already fired and is ending the process."""
+
+    def __init__(self, budget_s, emit):
+        import threading
+
+        self._lock = threading.Lock()
+        self._done = False
+        self._emit = emit
+        self._timer = threading.Timer(budget_s, self._fire)
+        self._timer.daemon = True
+
+    def start(self):
+        self._timer.start()
+        return self
+
+    def finish(self) -> bool:
+        with self._lock:
+            if self._done:
+                return False
+            self._done = True
+        self._timer.cancel()
+        return True
+
+    def _fire(self):
+        with self._lock:
+            if self._done:
+                return
+            self._done = True
+        try:
+            self._emit()
+        finally:
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
+
+
+def run_sublines(args, env, run, release=lambda: None, out=None):
     """Each sub-line is `run(sub_args, name, env)` with the main line's steps,
     a warm-up of max(W, SUBLINE_WARMUP) launches, the config's own stream
     count, 16-B records and no variants or host path; every rank runs them in
     the same order (their barriers and collectives pair up).  Returns
-    {name: line} on rank 0, None elsewhere or when there are none."""
+    {name: line} on rank 0, None elsewhere or when there are none; `out`
+    (optional) receives each finished line as it completes."""
     names = subline_names(args)
     if not names:
         return None
-    out = {}
+    out = {} if out is None else out
     for name in names:
         sub = argparse.Namespace(**vars(args))
         sub.config, sub.streams, sub.record, sub.timing = name, STREAMS[name], 16, "launches"

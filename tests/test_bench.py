@@ -2,6 +2,8 @@
 `roofline.achieved`, the config table, and the C5 runner's overlap of the
 per-step histogram all-reduce (every reduce waited before the timed region
 ends; a buffer reused only after its reduce) over several streams."""
+import time
+
 import numpy as np
 import pytest
 
@@ -596,3 +598,36 @@ print("after teardown", flush=True)
             assert out == ["line", "barrier"] and "did not return" in r.stderr
         else:
             assert "pg" in out and "after" in out and "aborted" in out
+
+
+def test_subline_guard_prints_and_ends_a_stalled_run():
+    """bench.SublineGuard at N > 1: sub-lines that never finish (a collective
+    that never completes) leave the process after the budget with status 0,
+    the partial line printed by `emit`; a run that finishes in time claims
+    the line and the guard never fires."""
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = str(Path(bench.__file__).resolve().parent)
+    code = r"""
+import sys, threading, time
+sys.path.insert(0, {root!r})
+import bench
+
+g = bench.SublineGuard({budget}, lambda: print("partial line", flush=True)).start()
+if {stall}:
+    threading.Event().wait()  # a sub-line stuck in a collective
+time.sleep(0.05)
+print("claimed" if g.finish() else "lost", flush=True)
+time.sleep(0.6)
+print("full line", flush=True)
+"""
+    t0 = time.perf_counter()
+    r = subprocess.run([sys.executable, "-c", code.format(root=root, budget=0.3, stall=True)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.split() == ["partial", "line"], r
+    assert time.perf_counter() - t0 < 30
+    r = subprocess.run([sys.executable, "-c", code.format(root=root, budget=0.3, stall=False)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.splitlines() == ["claimed", "full line"], r
