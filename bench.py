@@ -1472,8 +1472,17 @@ def main():
                 result["wall_s_command"] = round(time.perf_counter() - T_START, 2)
                 print(json.dumps(jsonable(compact_line(result, args.config))), flush=True)
 
-        guard = SublineGuard(args.subline_budget_s, emit_partial).start()
-    subs = run_sublines(args, env, run_config, torch.cuda.empty_cache, out=done)
+        # rank 0 (the printer) first: the other ranks outlast it by 5 s, and
+        # a collective that fails when rank 0 leaves only waits for their guard
+        guard = SublineGuard(args.subline_budget_s + (5.0 if rank else 0.0),
+                             emit_partial).start()
+    try:
+        subs = run_sublines(args, env, run_config, torch.cuda.empty_cache, out=done)
+    except Exception as e:  # noqa: BLE001 — only ranks > 0 with a guard, below
+        if guard is None or rank == 0:
+            raise
+        log(f"[bench] rank {rank}: a sub-line failed ({e!r}); the sub-line guard ends the run")
+        time.sleep(3600)
     if guard is not None and not guard.finish():
         time.sleep(3600)  # the guard is printing the line and ending the process
     if result is not None and subs is not None:
