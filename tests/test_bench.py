@@ -513,6 +513,22 @@ def test_compact_line_ends_in_a_summary_of_every_config(tmp_path, monkeypatch):
     assert out["roofline"]["read_frac_records_dram"] == 0.667
 
 
+def test_compact_line_with_unfinished_sublines(tmp_path, monkeypatch):
+    """The line SublineGuard prints: the sub-lines that finished, the others
+    named under sublines_unfinished, the summary of what was measured."""
+    import json
+
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+    main = _fake_line(88_000)
+    result = {**main, "sublines": {"c3": _fake_line(29_000)},
+              "sublines_unfinished": {"c4": "not finished within 150 s at N = 8",
+                                      "c5": "not finished within 150 s at N = 8"}}
+    out = bench.compact_line(result, "c2")
+    assert set(out["sublines"]) == {"c3"} and set(out["summary"]) == {"c2", "c3"}
+    assert set(out["sublines_unfinished"]) == {"c4", "c5"}
+    assert out["value"] == 88_000 and len(json.dumps(out)) < 7000
+
+
 def test_read_chunks_np_equals_read_chunks():
     """The host chunk tables of the CPU baseline's sample equal the device
     path's (read_chunks, run here on CPU tensors)."""
